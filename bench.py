@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident mtbl block-decode throughput on MI355X.
+
+Metric (BASELINE.json): "KV records/s + GiB/s of block bytes decoded, device-resident,
+1/2/4/8 GPU".  Workload (N=1): BASELINE configs[1] = cfg2, 100 k data blocks of 4 KiB,
+16 B keys / 64 B values, restart interval 16, CompressionType::None,
+written by the product Writer from a seeded generator (synthetic data).
+
+A step = one full decode of the resident batch through the C ABI: mtblx_count_blocks
+(k_count + block scan) then mtblx_decode_counted (k_decode), i.e. every block's records
+reconstructed and laid out contiguously in HBM.  Inputs are in HBM before timing starts.
+
+Multi-GPU (torchrun, one rank per GPU): blocks are independent, so every rank decodes
+its own 100 k-block shard (weak scaling, no data-path collective); the only collectives
+are the timing barrier and the max-over-ranks reduction.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "oxidized-mtbl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(data, off, ln, budget_s: float):
+    """CPU restatement of src/block.rs (oracle/, reference semantics) on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pyoracle.build()
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+    nblk = off.size
+    # 1 thread on a bounded sample
+    sample = min(nblk, 20_000)
+    t1, r1, _ = pyoracle.bench_scan(data, off[:sample], ln[:sample], 1, 1)
+    bytes1 = float(ln[:sample].sum(dtype=np.uint64))
+    # T threads over the whole batch, repeated to fill ~budget_s
+    tT, rT, _ = pyoracle.bench_scan(data, off, ln, threads, 1)
+    iters = max(1, int(budget_s / max(tT, 1e-3)))
+    tT, rT, _ = pyoracle.bench_scan(data, off, ln, threads, iters)
+    bytesT = float(ln.sum(dtype=np.uint64)) * iters
+    return {
+        "value": bytesT / tT / 2**30,
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "records_per_s": rT / tT,
+        "single_thread_GiBs": bytes1 / t1 / 2**30,
+        "single_thread_records_per_s": r1 / t1,
+        "sample": f"cfg2 blocks, {threads} threads x {iters} passes over all {nblk} blocks "
+                  f"({tT:.1f} s); 1 thread over the first {sample} blocks ({t1:.2f} s); C restatement of "
+                  f"src/block.rs (oracle/mtbl_oracle.c, -O3), reference Rust crate not buildable here",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--blocks", type=int, default=100_000)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_decode.json"),
+                    help="PMC-derived HBM bytes per k_decode launch (profiles/, from a rocprofv3 --pmc run)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from mtblx import codec, synth
+
+    t = time.time()
+    data, off, ln = synth.cfg2_file(args.blocks, seed=synth.SEED_CFG2 + rank)
+    log(f"[rank {rank}] generated {off.size} blocks / {data.size / 2**20:.1f} MiB in {time.time() - t:.1f}s")
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    stream = torch.cuda.Stream()
+    ws = codec.Workspace(batch.nblk)
+    with torch.cuda.stream(stream):
+        probe = codec.DecodedBlocks(batch.nblk, 0, 0, 0)
+        codec.count_blocks(batch, probe, ws, stream)
+    stream.synchronize()
+    nrec, kbytes, vbytes, _ = probe.totals_host()
+    out = codec.DecodedBlocks(batch.nblk, nrec, kbytes, vbytes)
+    del probe
+    block_bytes = int(ln.sum(dtype=np.uint64))
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        codec.count_blocks(batch, out, ws, stream)
+        if i is not None:
+            ev[i][1].record(stream)
+        codec.decode_counted(batch, out, ws, stream)
+        if i is not None:
+            ev[i][2].record(stream)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+    torch.cuda.synchronize()
+    h = out.totals_host()
+    st = out.status[: batch.nblk]
+    if h[3] != 0 or not bool((st == 0).all().item()) or h[0] != nrec:
+        raise RuntimeError(f"decode failed: totals={h}, bad blocks={int((st != 0).sum().item())}")
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for i in range(args.steps):
+            step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    k_count_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    k_decode_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_bytes = block_bytes * world
+    total_recs = nrec * world
+    value = total_bytes / (elapsed / args.steps) / 2**30
+
+    # roofline of the dominant kernel (k_decode): algorithmic bytes per launch
+    alg_bytes = block_bytes + kbytes + vbytes + 8 * nrec + 24 * batch.nblk
+    achieved = alg_bytes / (k_decode_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    res = {
+        "metric": "KV records/s + GiB/s of block bytes decoded, device-resident",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "records_per_s": round(total_recs / (elapsed / args.steps), 1),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded cfg2 generator, product Writer)",
+        "config": {"workload": "cfg2: 4 KiB blocks, 16 B keys / 64 B values, restart_interval=16, "
+                               "compression=none, device-resident decode",
+                   "blocks_per_gpu": int(batch.nblk), "block_bytes_per_gpu": block_bytes,
+                   "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
+                   "parallelism": f"block-sharded x{world}, no collective"},
+        "kernels_ms": {"k_count+scan": round(k_count_ms, 4), "k_decode": round(k_decode_ms, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_decode", "alg_bytes_per_launch": int(alg_bytes)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(data, off, ln, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

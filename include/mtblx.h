@@ -1,0 +1,110 @@
+/*
+ * mtblx.h — C ABI of the MI355X-native mtbl block codec (libmtblx.so).
+ *
+ * Drop-in boundary for Kerollmops/oxidized-mtbl's block decode seam:
+ *   Reader::block -> Block::init -> BlockIter::{init, seek_to_first, next, get}
+ *   (reference src/reader.rs:140-186, src/block.rs:16-49, :75-93, :119-143, :145-213,
+ *    driven per record by ReaderIntoIter::next src/reader.rs:337-405).
+ * The reference exposes no FFI of its own (Block/BlockIter are crate-private,
+ * src/lib.rs:32-33); these entry points are what a Rust `extern "C"` shim would bind
+ * to replace that seam with one batched device call (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - plain pointers + sizes only; no HIP or torch types (streams are `void*`,
+ *    i.e. a hipStream_t, NULL = the null stream).
+ *  - "device" = memory the kernels read/write (hipMalloc'd or host-pinned mapped).
+ *  - the library never allocates on a hot call: the caller passes every buffer,
+ *    including the workspace sized by mtblx_decode_workspace_bytes().
+ *  - calls are asynchronous on `stream` and re-entrant (no global mutable state).
+ *  - return value: MTBLX_OK or a negative MTBLX_E_* (argument / HIP launch errors).
+ *    Per-block outcomes are reported in `status[]` (MTBLX_ST_*), never by aborting.
+ */
+#ifndef MTBLX_H
+#define MTBLX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTBLX_ABI_VERSION 1
+
+/* ---- API return codes ---- */
+#define MTBLX_OK 0
+#define MTBLX_E_INVAL (-1)    /* bad argument (NULL pointer, workspace too small, ...) */
+#define MTBLX_E_HIP (-2)      /* a HIP runtime call failed                              */
+#define MTBLX_E_NODEV (-3)    /* no gfx950 device visible                               */
+#define MTBLX_E_FORMAT (-4)   /* host-side file/format error (reader API)               */
+
+/* ---- per-block status (status[b]) ----
+ * Exact correspondence with the reference's behaviour on the same bytes:         */
+#define MTBLX_ST_OK 0            /* decoded; identical records to src/block.rs    */
+#define MTBLX_ST_INVALID_BLOCK 1 /* Block::init returns None -> MtblError::InvalidBlock (src/block.rs:16-49) */
+#define MTBLX_ST_CORRUPT 2       /* the reference panics (assert/unwrap/slice, src/block.rs:59,79,131-135,217-235);
+                                    nrec[b] = records the reference yielded before the panic          */
+#define MTBLX_ST_LOOP 3          /* zero-progress entry: the reference yields it forever; emitted once */
+#define MTBLX_ST_UNSUPPORTED 4   /* block >= 4 GiB (u64 restart arrays): not decoded on the device    */
+#define MTBLX_ST_OVERFLOW 5      /* caller's key/value/record capacity exceeded; block not written    */
+
+/* A batch of uncompressed block contents already resident on the device.
+ * Block b occupies data[blk_off[b] .. blk_off[b] + blk_len[b]). */
+typedef struct mtblx_block_batch {
+  const uint8_t* data;      /* device */
+  uint64_t data_len;        /* bytes readable at `data` (bounds for staging loads) */
+  const uint64_t* blk_off;  /* device [nblk] */
+  const uint32_t* blk_len;  /* device [nblk] */
+  uint32_t nblk;
+  uint32_t max_blk_len;     /* host hint: max of blk_len (selects the kernel variant); 0 = unknown */
+} mtblx_block_batch;
+
+/* Output layout (the north star's "keys and values laid out contiguously"):
+ *   records of block b are global records rec_base[b] .. rec_base[b] + nrec[b]
+ *   key of record i of block b  = keys[key_base[b] + (i ? key_end[r-1] : 0) .. key_base[b] + key_end[r]]
+ *   value                        = vals[val_base[b] + (i ? val_end[r-1] : 0) .. val_base[b] + val_end[r]]
+ *   with r = rec_base[b] + i; key_end/val_end are u32 END offsets relative to the block's base.
+ * Records keep the reference's order within and across blocks. */
+typedef struct mtblx_decoded {
+  uint32_t* nrec;       /* device [nblk] */
+  uint64_t* rec_base;   /* device [nblk] exclusive prefix of nrec            */
+  uint64_t* key_base;   /* device [nblk] exclusive prefix of key bytes       */
+  uint64_t* val_base;   /* device [nblk] exclusive prefix of value bytes     */
+  int32_t* status;      /* device [nblk] MTBLX_ST_*                          */
+  uint32_t* key_end;    /* device [rec_cap] */
+  uint32_t* val_end;    /* device [rec_cap] */
+  uint64_t rec_cap;
+  uint8_t* keys;        /* device [keys_cap] */
+  uint64_t keys_cap;
+  uint8_t* vals;        /* device [vals_cap] */
+  uint64_t vals_cap;
+  uint64_t* totals;     /* device [4]: records, key bytes, value bytes, flags (bit0 = overflow) */
+} mtblx_decoded;
+
+/* Library identity / device check. */
+int mtblx_abi_version(void);
+int mtblx_device_ok(void); /* 1 if the current HIP device is gfx950, else 0 */
+
+/* Workspace bytes needed by mtblx_decode_blocks for a batch of nblk blocks. */
+size_t mtblx_decode_workspace_bytes(uint32_t nblk);
+
+/* Decode every block of `in` into `out` (replaces Block::init + the BlockIter scan
+ * seek_to_first/next/get of src/block.rs for each block; see header comment). */
+int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
+/* Sizes only (nrec, status, bases, totals); no key/value bytes are written.
+ * Lets a caller size `out` exactly before mtblx_decode_blocks. */
+int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* Second half of a count/decode split: writes keys/values using the counts and bases a
+ * previous mtblx_count_blocks left in `out` and `workspace` (same batch, same workspace,
+ * same stream).  count + decode_counted == decode_blocks. */
+int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTBLX_H */

@@ -1,0 +1,78 @@
+/*
+ * mtblx_host.h — host-side file layer of libmtblx.so (C ABI), around the device codec.
+ *
+ * Mirrors the reference's public file-level surface that sits either side of the
+ * block codec:
+ *   Writer::{insert, into_inner}        /root/reference/src/writer.rs:112-181
+ *   write_block / shortest separator    src/writer.rs:203-265
+ *   BlockBuilder (host build)           src/block_builder.rs:15-104
+ *   Metadata footer                     src/metadata.rs:27-79
+ *   ReaderBuilder::read framing         src/reader.rs:31-81
+ *   Reader::block framing + CRC         src/reader.rs:140-164
+ *   crc32c                              crate crc32c 0.4 (SSE4.2)
+ * Decoding block contents is NOT done here: every block goes through
+ * mtblx_decode_blocks (mtblx.h) on the device.
+ *
+ * Compression: this round's writer emits CompressionType::None only
+ * (mtblx_writer_new returns NULL otherwise); compressed READ support is host
+ * decompression feeding the same device path.
+ */
+#ifndef MTBLX_HOST_H
+#define MTBLX_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* MtblError (src/error.rs:44-52) */
+#define MTBLX_ERR_NONE 0
+#define MTBLX_ERR_INVALID_METADATA_SIZE 1
+#define MTBLX_ERR_INVALID_INDEX_BLOCK_OFFSET 2
+#define MTBLX_ERR_INVALID_INDEX_LENGTH 3
+#define MTBLX_ERR_INVALID_FORMAT_VERSION 4
+#define MTBLX_ERR_INVALID_COMPRESSION_ALGORITHM 5
+#define MTBLX_ERR_INVALID_BLOCK 6
+#define MTBLX_ERR_IO 7
+
+typedef struct mtblx_footer {
+  uint64_t meta[9];  /* index_block_offset, data_block_size, compression_algorithm, count_entries,
+                        count_data_blocks, bytes_data_blocks, bytes_index_block, bytes_keys, bytes_values */
+  uint32_t version;  /* 0 = FormatV1, 1 = FormatV2 */
+  int32_t err;       /* MTBLX_ERR_* when the call returns MTBLX_E_FORMAT */
+} mtblx_footer;
+
+/* crc32c of n bytes (replaces crc32c::crc32c, src/reader.rs:73,162, src/writer.rs:218) */
+uint32_t mtblx_crc32c(const uint8_t* data, uint64_t n);
+
+/* varint_decode64 (src/varint.rs:78-97): consumed length, 0 = unterminated, -1 = reference panic */
+int mtblx_varint_decode64(const uint8_t* data, uint64_t len, uint64_t* out);
+
+/* Metadata::read_from_bytes + the offset sanity check of ReaderBuilder::read (src/reader.rs:31-49) */
+int mtblx_read_footer(const uint8_t* file, uint64_t len, mtblx_footer* f);
+
+/* framing of the block at file offset `off` (src/reader.rs:140-164): content window + CRC check.
+ * *panic = 1 where the reference panics (out-of-range slice, CRC assert_eq). */
+int mtblx_frame_block(const uint8_t* file, uint64_t len, uint32_t version, uint64_t off, int verify,
+                      uint64_t* content_off, uint64_t* content_len, int* panic);
+
+/* Writer (src/writer.rs).  compression must be 0 (None) this round. */
+typedef struct mtblx_writer mtblx_writer;
+mtblx_writer* mtblx_writer_new(uint64_t block_size, uint64_t restart_interval, uint32_t compression);
+/* MTBLX_OK, or MTBLX_E_FORMAT where the reference panics ("out-of-order key", ...) */
+int mtblx_writer_insert(mtblx_writer* w, const uint8_t* key, uint64_t klen, const uint8_t* val, uint64_t vlen);
+int mtblx_writer_insert_batch(mtblx_writer* w, const uint8_t* keys, const uint64_t* key_end, const uint8_t* vals,
+                              const uint64_t* val_end, uint64_t n);
+/* Writer::into_inner: *out malloc'd (free with mtblx_free) */
+int mtblx_writer_finish(mtblx_writer* w, uint8_t** out, uint64_t* out_len);
+/* data-block directory of the finished file: content offset / length per data block */
+uint64_t mtblx_writer_block_count(const mtblx_writer* w);
+int mtblx_writer_block_dir(const mtblx_writer* w, uint64_t* blk_off, uint32_t* blk_len);
+void mtblx_writer_free(mtblx_writer* w);
+void mtblx_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTBLX_HOST_H */

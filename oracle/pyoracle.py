@@ -1,0 +1,275 @@
+"""ctypes front-end of the CPU ORACLE (oracle/mtbl_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module;
+it is the checker, never the product.  See oracle/mtbl_oracle.h for the restated
+reference semantics (Kerollmops/oxidized-mtbl src/block.rs, src/varint.rs,
+src/block_builder.rs, src/writer.rs, src/reader.rs, src/metadata.rs).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libmtbl_oracle.so")
+
+ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW = range(6)
+END_NONE, END_ERR_OPEN, END_ERR_NEXT, END_PANIC, END_LOOP = range(5)
+ERR_NAMES = {0: None, 1: "InvalidMetadataSize", 2: "InvalidIndexBlockOffset", 3: "InvalidIndexLength",
+             4: "InvalidFormatVersion", 5: "InvalidCompressionAlgorithm", 6: "InvalidBlock", 7: "Io"}
+
+
+def build() -> str:
+    """Compile the oracle (gcc) into oracle/_build/.  Idempotent."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        u8p, u32p, u64p, i32p = (C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_int32))
+        L.oracle_varint_encode32.argtypes = [u8p, C.c_uint32]
+        L.oracle_varint_encode32.restype = C.c_uint32
+        L.oracle_varint_encode64.argtypes = [u8p, C.c_uint64]
+        L.oracle_varint_encode64.restype = C.c_uint32
+        L.oracle_varint_decode32.argtypes = [u8p, C.c_uint64, u32p]
+        L.oracle_varint_decode32.restype = C.c_int32
+        L.oracle_varint_decode64.argtypes = [u8p, C.c_uint64, u64p]
+        L.oracle_varint_decode64.restype = C.c_int32
+        L.oracle_crc32c.argtypes = [u8p, C.c_uint64]
+        L.oracle_crc32c.restype = C.c_uint32
+        L.oracle_decode_blocks.argtypes = [u8p, u64p, u32p, C.c_uint32, u32p, u64p, u64p, i32p, u64p, u64p, u64p,
+                                           u8p, C.c_uint64, u8p, C.c_uint64, u32p, u32p, C.c_uint64]
+        L.oracle_decode_blocks.restype = C.c_int32
+        L.oracle_bench_scan.argtypes = [u8p, u64p, u32p, C.c_uint32, C.c_int, C.c_int, u64p, u64p]
+        L.oracle_bench_scan.restype = C.c_uint64
+        L.oracle_writer_new.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+        L.oracle_writer_new.restype = C.c_void_p
+        L.oracle_writer_insert.argtypes = [C.c_void_p, u8p, C.c_uint64, u8p, C.c_uint64]
+        L.oracle_writer_insert.restype = C.c_int32
+        L.oracle_writer_finish.argtypes = [C.c_void_p, C.POINTER(u8p), u64p]
+        L.oracle_writer_finish.restype = C.c_int32
+        L.oracle_writer_free.argtypes = [C.c_void_p]
+        L.oracle_free.argtypes = [C.c_void_p]
+        L.oracle_build_block.argtypes = [C.c_uint64, C.c_uint64, u8p, u64p, u8p, u64p, C.POINTER(u8p), u64p]
+        L.oracle_build_block.restype = C.c_int32
+        L.oracle_shortest_separator.argtypes = [u8p, C.c_uint64, u8p, C.c_uint64]
+        L.oracle_shortest_separator.restype = C.c_int64
+        L.oracle_file_scan.argtypes = [u8p, C.c_uint64, C.c_int32, C.c_int32, u8p, C.c_uint64, u8p, C.c_uint64,
+                                       C.c_uint64, C.c_void_p]
+        L.oracle_file_scan.restype = C.c_int32
+        L.oracle_scan_free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _u8(buf) -> "C.POINTER(C.c_uint8)":
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data_as(C.POINTER(C.c_uint8))
+    b = bytes(buf)
+    return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8)) if b else C.cast(C.c_char_p(b"\0"), C.POINTER(C.c_uint8))
+
+
+def _ptr(a: np.ndarray, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+# ---------------- varint / crc ----------------
+def varint_encode32(v: int) -> bytes:
+    b = (C.c_uint8 * 10)()
+    n = lib().oracle_varint_encode32(b, v)
+    return bytes(b[:n])
+
+
+def varint_encode64(v: int) -> bytes:
+    b = (C.c_uint8 * 10)()
+    n = lib().oracle_varint_encode64(b, v)
+    return bytes(b[:n])
+
+
+def varint_decode32(data: bytes):
+    """-> (value, consumed) ; consumed == -1 means the reference panics."""
+    v = C.c_uint32(0)
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data if data else b"\0")
+    n = lib().oracle_varint_decode32(buf, len(data), C.byref(v))
+    return v.value, n
+
+
+def varint_decode64(data: bytes):
+    v = C.c_uint64(0)
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data if data else b"\0")
+    n = lib().oracle_varint_decode64(buf, len(data), C.byref(v))
+    return v.value, n
+
+
+def crc32c(data) -> int:
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return lib().oracle_crc32c(_u8(a) if a.size else _u8(b"\0"), a.size)
+
+
+def shortest_separator(start: bytes, limit: bytes):
+    buf = (C.c_uint8 * (len(start) + 2))()
+    buf[: len(start)] = list(start)
+    lim = (C.c_uint8 * max(1, len(limit)))(*limit) if limit else (C.c_uint8 * 1)()
+    n = lib().oracle_shortest_separator(buf, len(start), lim, len(limit))
+    return None if n < 0 else bytes(buf[:n])
+
+
+# ---------------- writer / builder ----------------
+def write_file(records, block_size=8192, restart_interval=16, compression=0) -> bytes:
+    """records: iterable of (key, value) bytes.  Raises RuntimeError where the reference panics."""
+    L = lib()
+    w = L.oracle_writer_new(block_size, restart_interval, compression)
+    try:
+        for k, v in records:
+            k = bytes(k)
+            v = bytes(v)
+            kb = (C.c_uint8 * max(1, len(k))).from_buffer_copy(k or b"\0")
+            vb = (C.c_uint8 * max(1, len(v))).from_buffer_copy(v or b"\0")
+            if L.oracle_writer_insert(w, kb, len(k), vb, len(v)) != 0:
+                raise RuntimeError("reference panics in Writer::insert")
+        out = C.POINTER(C.c_uint8)()
+        n = C.c_uint64(0)
+        if L.oracle_writer_finish(w, C.byref(out), C.byref(n)) != 0:
+            raise RuntimeError("reference panics in Writer::into_inner")
+        data = C.string_at(out, n.value)
+        L.oracle_free(out)
+        return data
+    finally:
+        L.oracle_writer_free(w)
+
+
+def build_block(records, restart_interval=16) -> bytes:
+    keys = b"".join(bytes(k) for k, _ in records)
+    vals = b"".join(bytes(v) for _, v in records)
+    ke = np.cumsum([len(k) for k, _ in records], dtype=np.uint64) if records else np.zeros(1, np.uint64)
+    ve = np.cumsum([len(v) for _, v in records], dtype=np.uint64) if records else np.zeros(1, np.uint64)
+    kb = np.frombuffer(keys or b"\0", np.uint8)
+    vb = np.frombuffer(vals or b"\0", np.uint8)
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_uint64(0)
+    r = lib().oracle_build_block(restart_interval, len(records), _u8(kb), _ptr(ke, C.c_uint64), _u8(vb),
+                                 _ptr(ve, C.c_uint64), C.byref(out), C.byref(n))
+    if r != 0:
+        raise RuntimeError("reference panics in BlockBuilder::add")
+    data = C.string_at(out, n.value)
+    lib().oracle_free(out)
+    return data
+
+
+# ---------------- block decode (batch layout == mtblx_decode_blocks) ----------------
+class Decoded:
+    """Per-block counts + flattened records in the device output layout."""
+
+    def __init__(self, nblk):
+        self.nrec = np.zeros(nblk, np.uint32)
+        self.key_bytes = np.zeros(nblk, np.uint64)
+        self.val_bytes = np.zeros(nblk, np.uint64)
+        self.status = np.zeros(nblk, np.int32)
+        self.rec_base = np.zeros(nblk, np.uint64)
+        self.key_base = np.zeros(nblk, np.uint64)
+        self.val_base = np.zeros(nblk, np.uint64)
+        self.keys = self.vals = self.key_end = self.val_end = None
+
+    def records(self, b):
+        """list of (key, value) of block b"""
+        out = []
+        r0, kb, vb = int(self.rec_base[b]), int(self.key_base[b]), int(self.val_base[b])
+        pk = pv = 0
+        for i in range(int(self.nrec[b])):
+            ke, ve = int(self.key_end[r0 + i]), int(self.val_end[r0 + i])
+            out.append((bytes(self.keys[kb + pk: kb + ke]), bytes(self.vals[vb + pv: vb + ve])))
+            pk, pv = ke, ve
+        return out
+
+
+def decode_blocks(data: np.ndarray, blk_off: np.ndarray, blk_len: np.ndarray) -> Decoded:
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if data.size == 0:
+        data = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(blk_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(blk_len, dtype=np.uint32)
+    nb = off.size
+    d = Decoded(nb)
+    L = lib()
+    z64 = C.POINTER(C.c_uint64)()
+    L.oracle_decode_blocks(_u8(data), _ptr(off, C.c_uint64), _ptr(ln, C.c_uint32), nb, _ptr(d.nrec, C.c_uint32),
+                           _ptr(d.key_bytes, C.c_uint64), _ptr(d.val_bytes, C.c_uint64), _ptr(d.status, C.c_int32),
+                           _ptr(d.rec_base, C.c_uint64), _ptr(d.key_base, C.c_uint64), _ptr(d.val_base, C.c_uint64),
+                           None, 0, None, 0, None, None, 0)
+    nrec = int(d.nrec.sum(dtype=np.uint64))
+    kb = int(d.key_bytes.sum(dtype=np.uint64))
+    vb = int(d.val_bytes.sum(dtype=np.uint64))
+    d.keys = np.zeros(max(kb, 1), np.uint8)
+    d.vals = np.zeros(max(vb, 1), np.uint8)
+    d.key_end = np.zeros(max(nrec, 1), np.uint32)
+    d.val_end = np.zeros(max(nrec, 1), np.uint32)
+    r = L.oracle_decode_blocks(_u8(data), _ptr(off, C.c_uint64), _ptr(ln, C.c_uint32), nb, _ptr(d.nrec, C.c_uint32),
+                               _ptr(d.key_bytes, C.c_uint64), _ptr(d.val_bytes, C.c_uint64),
+                               _ptr(d.status, C.c_int32), _ptr(d.rec_base, C.c_uint64), _ptr(d.key_base, C.c_uint64),
+                               _ptr(d.val_base, C.c_uint64), _u8(d.keys), d.keys.size, _u8(d.vals), d.vals.size,
+                               _ptr(d.key_end, C.c_uint32), _ptr(d.val_end, C.c_uint32), d.key_end.size)
+    assert r == 0, r
+    d.keys, d.vals = d.keys[:kb], d.vals[:vb]
+    d.key_end, d.val_end = d.key_end[:nrec], d.val_end[:nrec]
+    del z64
+    return d
+
+
+def decode_block(block: bytes):
+    """-> (status, [(key, value), ...]) for one block"""
+    a = np.frombuffer(block, np.uint8) if block else np.zeros(0, np.uint8)
+    d = decode_blocks(a, np.array([0], np.uint64), np.array([len(block)], np.uint32))
+    return int(d.status[0]), d.records(0)
+
+
+def bench_scan(data: np.ndarray, blk_off, blk_len, nthreads=1, iters=1):
+    """CPU baseline timing -> (seconds, records, fold)"""
+    off = np.ascontiguousarray(blk_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(blk_len, dtype=np.uint32)
+    ns = C.c_uint64(0)
+    nr = C.c_uint64(0)
+    h = lib().oracle_bench_scan(_u8(data), _ptr(off, C.c_uint64), _ptr(ln, C.c_uint32), off.size, nthreads, iters,
+                                C.byref(ns), C.byref(nr))
+    return ns.value * 1e-9, nr.value, h
+
+
+# ---------------- file-level iteration ----------------
+class _ScanRes(C.Structure):
+    _fields_ = [("end", C.c_int32), ("err", C.c_int32), ("nrec", C.c_uint64), ("keys", C.POINTER(C.c_uint8)),
+                ("vals", C.POINTER(C.c_uint8)), ("key_end", C.POINTER(C.c_uint64)),
+                ("val_end", C.POINTER(C.c_uint64)), ("meta", C.c_uint64 * 9), ("version", C.c_int32)]
+
+
+MODES = {"iter": 0, "get": 1, "prefix": 2, "range": 3, "from": 4}
+
+
+def file_scan(data: bytes, mode="iter", key=b"", key2=b"", verify=True, max_records=1 << 62):
+    """-> dict(end, err, records, meta, version) restating Reader::new + ReaderIntoIter."""
+    a = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    kb = (C.c_uint8 * max(1, len(key))).from_buffer_copy(key or b"\0")
+    k2 = (C.c_uint8 * max(1, len(key2))).from_buffer_copy(key2 or b"\0")
+    r = _ScanRes()
+    lib().oracle_file_scan(_u8(a), len(data), 1 if verify else 0, MODES[mode], kb, len(key), k2, len(key2),
+                           max_records, C.byref(r))
+    recs = []
+    pk = pv = 0
+    for i in range(r.nrec):
+        ke, ve = r.key_end[i], r.val_end[i]
+        recs.append((C.string_at(C.addressof(r.keys.contents) + pk, ke - pk) if ke > pk else b"",
+                     C.string_at(C.addressof(r.vals.contents) + pv, ve - pv) if ve > pv else b""))
+        pk, pv = ke, ve
+    out = dict(end=r.end, err=ERR_NAMES[r.err], records=recs, meta=list(r.meta), version=r.version)
+    lib().oracle_scan_free(C.byref(r))
+    return out

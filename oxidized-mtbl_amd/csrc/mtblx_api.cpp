@@ -1,0 +1,65 @@
+// mtblx_api.cpp — C ABI entry points of libmtblx.so (declared in include/mtblx.h).
+//
+// Thin, allocation-free glue: argument checks, then the kernel pipeline in decode.hip
+// on the caller's stream.  See include/mtblx.h for the contract and the reference
+// interfaces each entry point replaces.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "mtblx.h"
+
+extern "C" size_t mtblx_impl_scan_parts(uint32_t nblk);
+extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
+                              hipStream_t s);
+
+extern "C" int mtblx_abi_version(void) { return MTBLX_ABI_VERSION; }
+
+extern "C" int mtblx_device_ok(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+  return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+extern "C" size_t mtblx_decode_workspace_bytes(uint32_t nblk) {
+  return (size_t)nblk * 16u + mtblx_impl_scan_parts(nblk) * 24u + 256u;
+}
+
+static int check_common(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb) {
+  if (!in || !out) return MTBLX_E_INVAL;
+  if (in->nblk == 0) return MTBLX_OK;
+  if (!in->data || !in->blk_off || !in->blk_len) return MTBLX_E_INVAL;
+  if (!out->nrec || !out->rec_base || !out->key_base || !out->val_base || !out->status || !out->totals)
+    return MTBLX_E_INVAL;
+  if (!ws || wsb < mtblx_decode_workspace_bytes(in->nblk)) return MTBLX_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(ws) & 7u) != 0) return MTBLX_E_INVAL;
+  return 1;
+}
+
+extern "C" int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
+                                  void* stream) {
+  int c = check_common(in, out, ws, wsb);
+  if (c != 1) return c;
+  return mtblx_impl_run(in, out, ws, 0, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
+                                    void* stream) {
+  int c = check_common(in, out, ws, wsb);
+  if (c != 1) return c;
+  if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
+      (!out->val_end && out->rec_cap))
+    return MTBLX_E_INVAL;
+  return mtblx_impl_run(in, out, ws, 2, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
+                                   void* stream) {
+  int c = check_common(in, out, ws, wsb);
+  if (c != 1) return c;
+  if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
+      (!out->val_end && out->rec_cap))
+    return MTBLX_E_INVAL;
+  return mtblx_impl_run(in, out, ws, 1, reinterpret_cast<hipStream_t>(stream));
+}

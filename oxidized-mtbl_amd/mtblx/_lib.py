@@ -1,0 +1,88 @@
+"""ctypes binding of libmtblx.so (include/mtblx.h, include/mtblx_host.h).
+
+The library is built in-tree (``make -C oxidized-mtbl_amd``).  There is no fallback:
+if the shared object is missing, importing the codec raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmtblx.so")
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+i32p = C.POINTER(C.c_int32)
+
+MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT = 0, -1, -2, -3, -4
+ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW = range(6)
+
+# every symbol the public headers declare (checked by tests/test_abi.py)
+EXPORTS = [
+    "mtblx_abi_version", "mtblx_device_ok", "mtblx_decode_workspace_bytes", "mtblx_decode_blocks",
+    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
+    "mtblx_writer_new", "mtblx_writer_insert", "mtblx_writer_insert_batch", "mtblx_writer_finish",
+    "mtblx_writer_block_count", "mtblx_writer_block_dir", "mtblx_writer_free", "mtblx_free",
+]
+
+
+class BlockBatch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("data_len", C.c_uint64), ("blk_off", C.c_void_p), ("blk_len", C.c_void_p),
+                ("nblk", C.c_uint32), ("max_blk_len", C.c_uint32)]
+
+
+class Decoded(C.Structure):
+    _fields_ = [("nrec", C.c_void_p), ("rec_base", C.c_void_p), ("key_base", C.c_void_p), ("val_base", C.c_void_p),
+                ("status", C.c_void_p), ("key_end", C.c_void_p), ("val_end", C.c_void_p), ("rec_cap", C.c_uint64),
+                ("keys", C.c_void_p), ("keys_cap", C.c_uint64), ("vals", C.c_void_p), ("vals_cap", C.c_uint64),
+                ("totals", C.c_void_p)]
+
+
+class Footer(C.Structure):
+    _fields_ = [("meta", C.c_uint64 * 9), ("version", C.c_uint32), ("err", C.c_int32)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libmtblx.so not built ({LIB_PATH}); run `make -C oxidized-mtbl_amd` "
+                              "(no CPU fallback exists for the device codec)")
+        L = C.CDLL(LIB_PATH)
+        L.mtblx_abi_version.restype = C.c_int
+        L.mtblx_device_ok.restype = C.c_int
+        L.mtblx_decode_workspace_bytes.argtypes = [C.c_uint32]
+        L.mtblx_decode_workspace_bytes.restype = C.c_size_t
+        for f in (L.mtblx_decode_blocks, L.mtblx_count_blocks, L.mtblx_decode_counted):
+            f.argtypes = [C.POINTER(BlockBatch), C.POINTER(Decoded), C.c_void_p, C.c_size_t, C.c_void_p]
+            f.restype = C.c_int
+        L.mtblx_crc32c.argtypes = [u8p, C.c_uint64]
+        L.mtblx_crc32c.restype = C.c_uint32
+        L.mtblx_varint_decode64.argtypes = [u8p, C.c_uint64, u64p]
+        L.mtblx_varint_decode64.restype = C.c_int
+        L.mtblx_read_footer.argtypes = [u8p, C.c_uint64, C.POINTER(Footer)]
+        L.mtblx_read_footer.restype = C.c_int
+        L.mtblx_frame_block.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int, u64p, u64p,
+                                        C.POINTER(C.c_int)]
+        L.mtblx_frame_block.restype = C.c_int
+        L.mtblx_writer_new.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+        L.mtblx_writer_new.restype = C.c_void_p
+        L.mtblx_writer_insert.argtypes = [C.c_void_p, u8p, C.c_uint64, u8p, C.c_uint64]
+        L.mtblx_writer_insert.restype = C.c_int
+        L.mtblx_writer_insert_batch.argtypes = [C.c_void_p, u8p, u64p, u8p, u64p, C.c_uint64]
+        L.mtblx_writer_insert_batch.restype = C.c_int
+        L.mtblx_writer_finish.argtypes = [C.c_void_p, C.POINTER(u8p), u64p]
+        L.mtblx_writer_finish.restype = C.c_int
+        L.mtblx_writer_block_count.argtypes = [C.c_void_p]
+        L.mtblx_writer_block_count.restype = C.c_uint64
+        L.mtblx_writer_block_dir.argtypes = [C.c_void_p, u64p, u32p]
+        L.mtblx_writer_block_dir.restype = C.c_int
+        L.mtblx_writer_free.argtypes = [C.c_void_p]
+        L.mtblx_free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib

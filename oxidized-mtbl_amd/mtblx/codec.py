@@ -1,0 +1,176 @@
+"""Device block codec: Python front-end of mtblx_decode_blocks (include/mtblx.h).
+
+PyTorch is plumbing only (device memory, streams); the decode runs in libmtblx.so's
+HIP kernels.  Replaces the reference's per-block ``Block::init`` + ``BlockIter`` scan
+(/root/reference/src/block.rs:16-238) with one batched device call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import BlockBatch, Decoded
+
+
+def _require_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("mtblx device codec needs a ROCm GPU (gfx950); none visible")
+    L = _lib.lib()
+    if L.mtblx_device_ok() != 1:
+        raise RuntimeError("mtblx device codec: current device is not gfx950 (MI355X)")
+    return L
+
+
+def _u(t: torch.Tensor) -> int:
+    return t.data_ptr() if t is not None and t.numel() else 0
+
+
+@dataclass
+class DeviceBatch:
+    """Uncompressed block contents resident in HBM.  data: uint8; blk_off: int64 (u64); blk_len: int32 (u32)."""
+    data: torch.Tensor
+    blk_off: torch.Tensor
+    blk_len: torch.Tensor
+    max_blk_len: int
+
+    @property
+    def nblk(self) -> int:
+        return int(self.blk_off.numel())
+
+    @staticmethod
+    def from_host(data: np.ndarray, blk_off: np.ndarray, blk_len: np.ndarray, device="cuda") -> "DeviceBatch":
+        d = torch.from_numpy(np.ascontiguousarray(data, np.uint8)).to(device)
+        o = torch.from_numpy(np.ascontiguousarray(blk_off, np.uint64).view(np.int64)).to(device)
+        ln = np.ascontiguousarray(blk_len, np.uint32)
+        n = torch.from_numpy(ln.view(np.int32)).to(device)
+        return DeviceBatch(d, o, n, int(ln.max()) if ln.size else 0)
+
+    def cstruct(self) -> BlockBatch:
+        return BlockBatch(_u(self.data), int(self.data.numel()), _u(self.blk_off), _u(self.blk_len), self.nblk,
+                          int(self.max_blk_len))
+
+
+class DecodedBlocks:
+    """Device outputs in the layout of include/mtblx.h (mtblx_decoded)."""
+
+    def __init__(self, nblk: int, rec_cap: int, keys_cap: int, vals_cap: int, device="cuda"):
+        z = lambda n, dt: torch.zeros(max(int(n), 1), dtype=dt, device=device)  # noqa: E731
+        self.nblk = nblk
+        self.nrec = z(nblk, torch.int32)
+        self.rec_base = z(nblk, torch.int64)
+        self.key_base = z(nblk, torch.int64)
+        self.val_base = z(nblk, torch.int64)
+        self.status = z(nblk, torch.int32)
+        self.key_end = z(rec_cap, torch.int32)
+        self.val_end = z(rec_cap, torch.int32)
+        self.keys = z(keys_cap, torch.uint8)
+        self.vals = z(vals_cap, torch.uint8)
+        self.totals = z(4, torch.int64)
+        self.rec_cap, self.keys_cap, self.vals_cap = int(rec_cap), int(keys_cap), int(vals_cap)
+
+    def cstruct(self) -> Decoded:
+        return Decoded(_u(self.nrec), _u(self.rec_base), _u(self.key_base), _u(self.val_base), _u(self.status),
+                       _u(self.key_end), _u(self.val_end), self.rec_cap, _u(self.keys), self.keys_cap,
+                       _u(self.vals), self.vals_cap, _u(self.totals))
+
+    # ---------------- host views ----------------
+    def totals_host(self):
+        t = self.totals.cpu().numpy().view(np.uint64)
+        return int(t[0]), int(t[1]), int(t[2]), int(t[3])
+
+    def to_host(self) -> "HostDecoded":
+        nr, kb, vb, flags = self.totals_host()
+        return HostDecoded(
+            nrec=self.nrec[: self.nblk].cpu().numpy().view(np.uint32),
+            rec_base=self.rec_base[: self.nblk].cpu().numpy().view(np.uint64),
+            key_base=self.key_base[: self.nblk].cpu().numpy().view(np.uint64),
+            val_base=self.val_base[: self.nblk].cpu().numpy().view(np.uint64),
+            status=self.status[: self.nblk].cpu().numpy(),
+            key_end=self.key_end[: min(nr, self.rec_cap)].cpu().numpy().view(np.uint32),
+            val_end=self.val_end[: min(nr, self.rec_cap)].cpu().numpy().view(np.uint32),
+            keys=self.keys[: min(kb, self.keys_cap)].cpu().numpy(),
+            vals=self.vals[: min(vb, self.vals_cap)].cpu().numpy(),
+            totals=(nr, kb, vb, flags),
+        )
+
+
+@dataclass
+class HostDecoded:
+    nrec: np.ndarray
+    rec_base: np.ndarray
+    key_base: np.ndarray
+    val_base: np.ndarray
+    status: np.ndarray
+    key_end: np.ndarray
+    val_end: np.ndarray
+    keys: np.ndarray
+    vals: np.ndarray
+    totals: tuple
+
+    def records(self, b: int):
+        out = []
+        r0, kb, vb = int(self.rec_base[b]), int(self.key_base[b]), int(self.val_base[b])
+        pk = pv = 0
+        for i in range(int(self.nrec[b])):
+            ke, ve = int(self.key_end[r0 + i]), int(self.val_end[r0 + i])
+            out.append((bytes(self.keys[kb + pk: kb + ke]), bytes(self.vals[vb + pv: vb + ve])))
+            pk, pv = ke, ve
+        return out
+
+
+class Workspace:
+    def __init__(self, nblk: int, device="cuda"):
+        L = _lib.lib()
+        self.nbytes = int(L.mtblx_decode_workspace_bytes(nblk))
+        self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+
+
+def _stream_handle(stream) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def count_blocks(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=None) -> None:
+    L = _require_device()
+    b, o = batch.cstruct(), out.cstruct()
+    rc = L.mtblx_count_blocks(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
+                              C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_count_blocks failed: {rc}")
+
+
+def decode_into(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=None) -> None:
+    """Asynchronous decode on `stream` into preallocated outputs (the timed hot call)."""
+    L = _require_device()
+    b, o = batch.cstruct(), out.cstruct()
+    rc = L.mtblx_decode_blocks(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
+                               C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_decode_blocks failed: {rc}")
+
+
+def decode_counted(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=None) -> None:
+    """Decode using the counts a previous count_blocks(batch, out, ws) left behind."""
+    L = _require_device()
+    b, o = batch.cstruct(), out.cstruct()
+    rc = L.mtblx_decode_counted(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
+                                C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_decode_counted failed: {rc}")
+
+
+def decode_blocks(batch: DeviceBatch, stream=None) -> DecodedBlocks:
+    """Size exactly (count pass), allocate, decode.  Synchronises once for the sizes."""
+    _require_device()
+    ws = Workspace(batch.nblk)
+    probe = DecodedBlocks(batch.nblk, 0, 0, 0)
+    count_blocks(batch, probe, ws, stream)
+    torch.cuda.synchronize()
+    nr, kb, vb, _ = probe.totals_host()
+    out = DecodedBlocks(batch.nblk, nr, kb, vb)
+    decode_into(batch, out, ws, stream)
+    return out

@@ -1,0 +1,62 @@
+"""Deterministic synthetic workloads for BASELINE.json's configs.
+
+cfg1  10 k keys "{:010}" / value "{:010}" * (1 + i % 8), 4 KiB blocks (examples/dump.rs plumbing)
+cfg2  4 KiB blocks, 16 B keys = be64(c_i) || 8 random bytes with c_i = sum of gaps ~ U[1, 2^20)
+      (strictly increasing, neighbours share ~5 B), 64 random value bytes, restart interval 16,
+      CompressionType::None, seed 0x6d74626c02.
+Files are produced by the product Writer (writer.py -> src/writer.rs semantics).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .writer import Writer
+
+SEED_CFG2 = 0x6D74626C02
+SEED_CFG3 = 0x6D74626C03
+SEED_CFG4 = 0x6D74626C04
+
+
+def cfg1_records(n=10_000):
+    for i in range(n):
+        k = f"{i:010}"
+        yield k.encode(), (k * (1 + i % 8)).encode()
+
+
+def cfg2_arrays(nrec: int, seed: int = SEED_CFG2, key_tail: int = 8, val_len: int = 64):
+    """keys (nrec*16 u8), values (nrec*64 u8) in record order."""
+    rng = np.random.default_rng(seed)
+    gaps = rng.integers(1, 1 << 20, nrec, dtype=np.uint64)
+    c = np.cumsum(gaps, dtype=np.uint64)
+    klen = 8 + key_tail
+    keys = np.empty((nrec, klen), np.uint8)
+    keys[:, :8] = c.astype(">u8").view(np.uint8).reshape(nrec, 8)
+    keys[:, 8:] = rng.integers(0, 256, (nrec, key_tail), dtype=np.uint8)
+    vals = rng.integers(0, 256, (nrec, val_len), dtype=np.uint8)
+    return keys.reshape(-1), vals.reshape(-1), klen, val_len
+
+
+def write_arrays(keys, vals, klen, vlen, block_size=4096, restart_interval=16):
+    n = keys.size // klen
+    w = Writer(block_size, restart_interval)
+    ke = np.arange(1, n + 1, dtype=np.uint64) * np.uint64(klen)
+    ve = np.arange(1, n + 1, dtype=np.uint64) * np.uint64(vlen)
+    w.insert_batch(keys, ke, vals, ve)
+    data = w.into_inner_np()
+    off, ln = w.block_dir
+    return data, off, ln
+
+
+def cfg2_file(nblocks: int = 100_000, block_size: int = 4096, seed: int = SEED_CFG2):
+    """-> (file bytes as uint8 array, blk_off[nblocks], blk_len[nblocks]); exactly `nblocks` data blocks
+    of the file are returned in the directory (the file may hold a few more)."""
+    # ~51 records per 4 KiB block; generous estimate then trim the directory
+    per_block = max(1, (block_size - 64) // 79)
+    nrec = int(nblocks * per_block * 1.02) + 64
+    keys, vals, kl, vl = cfg2_arrays(nrec, seed)
+    data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
+    while off.size < nblocks:  # extremely unlikely; extend
+        nrec = int(nrec * 1.1)
+        keys, vals, kl, vl = cfg2_arrays(nrec, seed)
+        data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
+    return data, off[:nblocks].copy(), ln[:nblocks].copy()

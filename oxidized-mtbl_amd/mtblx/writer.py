@@ -1,0 +1,153 @@
+"""Writer / WriterBuilder mirror (reference /root/reference/src/writer.rs:15-201).
+
+Same names, argument meaning and error behaviour: ``insert`` of an out-of-order key is a
+panic in the reference (src/writer.rs:119-123); here it raises ``OutOfOrderKey`` and the
+writer is poisoned.  ``block_size`` is clamped to MIN_BLOCK_SIZE = 1024 (:43-46).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+
+DEFAULT_BLOCK_SIZE = 8192            # src/lib.rs:5
+DEFAULT_BLOCK_RESTART_INTERVAL = 16  # src/lib.rs:4
+MIN_BLOCK_SIZE = 1024                # src/lib.rs:6
+
+
+class CompressionType:
+    """src/compression.rs:6-15"""
+    None_ = 0
+    Snappy = 1
+    Zlib = 2
+    Lz4 = 3
+    Lz4hc = 4
+    Zstd = 5
+
+
+class OutOfOrderKey(RuntimeError):
+    """the reference panics with "out-of-order key" (src/writer.rs:121)"""
+
+
+class WriterBuilder:
+    def __init__(self):
+        self._compression = CompressionType.None_
+        self._level = 0
+        self._block_size = DEFAULT_BLOCK_SIZE
+        self._interval = DEFAULT_BLOCK_RESTART_INTERVAL
+
+    def compression_type(self, c: int) -> "WriterBuilder":
+        self._compression = c
+        return self
+
+    def compression_level(self, level: int) -> "WriterBuilder":
+        self._level = level
+        return self
+
+    def block_size(self, n: int) -> "WriterBuilder":
+        self._block_size = max(int(n), MIN_BLOCK_SIZE)
+        return self
+
+    def block_restart_interval(self, n: int) -> "WriterBuilder":
+        self._interval = int(n)
+        return self
+
+    def memory(self) -> "Writer":
+        return Writer(self._block_size, self._interval, self._compression)
+
+    build = memory
+
+
+class Writer:
+    def __init__(self, block_size=DEFAULT_BLOCK_SIZE, restart_interval=DEFAULT_BLOCK_RESTART_INTERVAL,
+                 compression=CompressionType.None_):
+        L = _lib.lib()
+        self._w = L.mtblx_writer_new(int(block_size), int(restart_interval), int(compression))
+        if not self._w:
+            raise NotImplementedError("compressed writing is not implemented in this round (CompressionType.None_ "
+                                      "only)")
+        self.block_dir = None
+
+    @staticmethod
+    def memory() -> "Writer":
+        return WriterBuilder().memory()
+
+    @staticmethod
+    def builder() -> WriterBuilder:
+        return WriterBuilder()
+
+    def insert(self, key, val) -> None:
+        k = bytes(key.encode() if isinstance(key, str) else key)
+        v = bytes(val.encode() if isinstance(val, str) else val)
+        kb = (C.c_uint8 * max(1, len(k))).from_buffer_copy(k or b"\0")
+        vb = (C.c_uint8 * max(1, len(v))).from_buffer_copy(v or b"\0")
+        rc = _lib.lib().mtblx_writer_insert(self._w, kb, len(k), vb, len(v))
+        if rc == _lib.MTBLX_E_FORMAT:
+            raise OutOfOrderKey("out-of-order key")
+        if rc != 0:
+            raise RuntimeError(f"mtblx_writer_insert: {rc}")
+
+    def insert_batch(self, keys: np.ndarray, key_end: np.ndarray, vals: np.ndarray, val_end: np.ndarray) -> None:
+        """Bulk insert of n records given as concatenated bytes + u64 end offsets."""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        vals = np.ascontiguousarray(vals, np.uint8)
+        ke = np.ascontiguousarray(key_end, np.uint64)
+        ve = np.ascontiguousarray(val_end, np.uint64)
+        if keys.size == 0:
+            keys = np.zeros(1, np.uint8)
+        if vals.size == 0:
+            vals = np.zeros(1, np.uint8)
+        rc = _lib.lib().mtblx_writer_insert_batch(self._w, keys.ctypes.data_as(_lib.u8p), ke.ctypes.data_as(_lib.u64p),
+                                                  vals.ctypes.data_as(_lib.u8p), ve.ctypes.data_as(_lib.u64p),
+                                                  ke.size)
+        if rc == _lib.MTBLX_E_FORMAT:
+            raise OutOfOrderKey("out-of-order key")
+        if rc != 0:
+            raise RuntimeError(f"mtblx_writer_insert_batch: {rc}")
+
+    def into_inner(self) -> bytes:
+        """Writer::into_inner: the finished .mtbl bytes.  Also records the data-block directory."""
+        L = _lib.lib()
+        out = _lib.u8p()
+        n = C.c_uint64(0)
+        rc = L.mtblx_writer_finish(self._w, C.byref(out), C.byref(n))
+        if rc != 0:
+            raise RuntimeError(f"mtblx_writer_finish: {rc}")
+        data = C.string_at(out, n.value)
+        L.mtblx_free(out)
+        nb = int(L.mtblx_writer_block_count(self._w))
+        off = np.zeros(max(nb, 1), np.uint64)
+        ln = np.zeros(max(nb, 1), np.uint32)
+        L.mtblx_writer_block_dir(self._w, off.ctypes.data_as(_lib.u64p), ln.ctypes.data_as(_lib.u32p))
+        self.block_dir = (off[:nb], ln[:nb])
+        return data
+
+    def into_inner_np(self) -> np.ndarray:
+        """Same as into_inner, returned as a uint8 array without an extra bytes copy."""
+        L = _lib.lib()
+        out = _lib.u8p()
+        n = C.c_uint64(0)
+        rc = L.mtblx_writer_finish(self._w, C.byref(out), C.byref(n))
+        if rc != 0:
+            raise RuntimeError(f"mtblx_writer_finish: {rc}")
+        arr = np.empty(n.value, np.uint8)
+        C.memmove(arr.ctypes.data, out, n.value)
+        L.mtblx_free(out)
+        nb = int(L.mtblx_writer_block_count(self._w))
+        off = np.zeros(max(nb, 1), np.uint64)
+        ln = np.zeros(max(nb, 1), np.uint32)
+        L.mtblx_writer_block_dir(self._w, off.ctypes.data_as(_lib.u64p), ln.ctypes.data_as(_lib.u32p))
+        self.block_dir = (off[:nb], ln[:nb])
+        return arr
+
+    finish = into_inner
+
+    def __del__(self):
+        try:
+            if getattr(self, "_w", None):
+                _lib.lib().mtblx_writer_free(self._w)
+                self._w = None
+        except Exception:
+            pass

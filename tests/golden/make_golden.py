@@ -1,0 +1,124 @@
+"""Generate / verify the golden fixtures under tests/golden/.
+
+1. kat.json: known-answer vectors HAND-DERIVED in SURVEY.md §2.2 from the reference's
+   src/writer.rs, src/block_builder.rs, src/metadata.rs (the reference publishes no
+   fixtures and cannot be built here).  They pin the reference tests `one_key` and
+   `empty` (src/writer.rs:272-298) byte-exactly.
+2. one_key.mtbl / empty.mtbl: the files those vectors describe, written by the oracle
+   and checked against kat.json before being (re)written.
+3. quirk_blocks.json: hand-constructed single blocks with the outcome derived by hand
+   from src/block.rs (status + records) — pins the oracle's panic / None / loop /
+   Vec-capacity semantics independently of its code.
+
+Usage:  python tests/golden/make_golden.py [--check]
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+# --- SURVEY.md §2.2 (hand derivation) ---
+KAT = {
+    "crc32c_check": {"input": "123456789", "crc": "e3069283"},
+    "one_key": {
+        "insert": [["hello", "I'm the one"]],
+        "data_block_content": "00050b68656c6c6f49276d20746865206f6e650000000001000000",
+        "data_block_crc": "3f400b02",
+        "index_block_content": "00050168656c6c6f000000000001000000",
+        "index_block_crc": "deec1759",
+        "file_len": 566,
+        "metadata": [32, 8192, 0, 1, 1, 32, 22, 5, 11],
+        "first_54": "1b020b403f00050b68656c6c6f49276d20746865206f6e650000000001000000115917ecde00050168656c6c6f000000000001000000",
+        "sha256": "ba687784368babc7a8bf12033fafd36091e0c05eaa28c5838bace82a023b26b7",
+    },
+    "empty": {
+        "index_block_content": "0000000001000000",
+        "index_block_crc": "516d1832",
+        "file_len": 525,
+        "metadata": [0, 8192, 0, 0, 0, 0, 13, 0, 0],
+        "sha256": "d19adf5e336a2b4b6e92c178a3e919026ee4f6899e161367af361fdcf9935435",
+    },
+}
+
+# --- hand-derived single-block outcomes (src/block.rs; release-mode arithmetic) ---
+# status: 0 OK, 1 INVALID_BLOCK (Block::init None), 2 CORRUPT (panic), 3 LOOP (never terminates)
+QUIRKS = [
+    {"name": "len3_invalid", "block": "000000", "status": 1, "records": [],
+     "why": "len < 4 -> Block::init None (block.rs:19-20)"},
+    {"name": "len6_corrupt", "block": "000000000000", "status": 2, "records": [],
+     "why": "len in [4,8): num_restarts assert (block.rs:59)"},
+    {"name": "zero_restarts", "block": "0000000000000000", "status": 2, "records": [],
+     "why": "n == 0 passes Block::init, BlockIter::init asserts n > 0 (block.rs:79)"},
+    {"name": "too_many_restarts", "block": "0000000005000000", "status": 1, "records": [],
+     "why": "4*(n+1) > len wraps (release) -> 64-bit branch wraps -> > len-4 -> None"},
+    {"name": "empty_block", "block": "0000000001000000", "status": 0, "records": [],
+     "why": "restart[0] = 0 = restart_offset -> no entries"},
+    {"name": "one_entry", "block": "000101414200000000" "01000000", "status": 0, "records": [["41", "42"]],
+     "why": "fast-path header (0,1,1)"},
+    {"name": "first_shared_nonzero", "block": "010101414200000000" "01000000", "status": 2, "records": [],
+     "why": "fresh key Vec has capacity 0 < shared=1: assert (block.rs:132)"},
+    {"name": "vec_capacity_quirk", "block": "0002006162" "05010063" "090000" "00000000" "01000000", "status": 2,
+     "records": [["6162", ""], ["616263", ""]],
+     "why": "e1 shared=5 > len 2 but <= capacity 8: truncate no-op -> 'abc'; e2 shared=9 > capacity 8 -> panic"},
+    {"name": "unterminated_loop", "block": "8080808080" "00000000" "01000000", "status": 3, "records": [["", ""]],
+     "why": "5 continuation bytes: varint len 0, cursor never advances, next == current forever"},
+    {"name": "noncanonical_varints", "block": "8000810080" "0041" "00000000" "01000000", "status": 0,
+     "records": [["41", ""]], "why": "slow path: shared=0 (80 00), non_shared=1 (81 00), value_length=0 (80 00)"},
+    {"name": "restart0_not_zero", "block": "0001014142" "0001014344" "05000000" "01000000", "status": 0,
+     "records": [["43", "44"]], "why": "the scan starts at restart_point(0) = 5, skipping the first entry"},
+    {"name": "restart0_at_end", "block": "0001014142" "05000000" "01000000", "status": 0, "records": [],
+     "why": "restart_point(0) >= restart_offset -> iterator invalid at once"},
+    {"name": "header_truncated", "block": "0001" "00000000" "01000000", "status": 2, "records": [],
+     "why": "limit - p = 2 < 3 -> decode_entry Err -> unwrap panic (block.rs:217-219,131)"},
+    {"name": "entry_overruns", "block": "00050041" "00000000" "01000000", "status": 2, "records": [],
+     "why": "non_shared + value_length = 5 > limit - p = 1 (block.rs:235)"},
+    {"name": "u32_sum_overflow", "block": "00" "8080808008" "8080808008" "00000000" "01000000", "status": 2,
+     "records": [], "why": "non_shared = value_length = 2^31: u32 sum overflows; the record is never yielded"},
+    {"name": "second_entry_corrupt", "block": "0001014142" "00050043" "00000000" "01000000", "status": 2,
+     "records": [["41", "42"]], "why": "first record yielded, second overruns limit -> panic"},
+]
+
+
+def build_files():
+    import pyoracle as o
+    one = o.write_file([(b"hello", b"I'm the one")])
+    empty = o.write_file([])
+    return one, empty
+
+
+def check(one, empty):
+    import pyoracle as o
+    assert o.crc32c(b"123456789") == int(KAT["crc32c_check"]["crc"], 16)
+    k = KAT["one_key"]
+    assert len(one) == k["file_len"]
+    assert one[:54].hex() == k["first_54"]
+    assert hashlib.sha256(one).hexdigest() == k["sha256"]
+    assert o.crc32c(bytes.fromhex(k["data_block_content"])) == int(k["data_block_crc"], 16)
+    assert o.crc32c(bytes.fromhex(k["index_block_content"])) == int(k["index_block_crc"], 16)
+    e = KAT["empty"]
+    assert len(empty) == e["file_len"]
+    assert hashlib.sha256(empty).hexdigest() == e["sha256"]
+    assert o.crc32c(bytes.fromhex(e["index_block_content"])) == int(e["index_block_crc"], 16)
+
+
+def main():
+    one, empty = build_files()
+    check(one, empty)
+    if "--check" in sys.argv:
+        assert open(os.path.join(HERE, "one_key.mtbl"), "rb").read() == one
+        assert open(os.path.join(HERE, "empty.mtbl"), "rb").read() == empty
+        print("golden fixtures OK")
+        return
+    open(os.path.join(HERE, "one_key.mtbl"), "wb").write(one)
+    open(os.path.join(HERE, "empty.mtbl"), "wb").write(empty)
+    json.dump(KAT, open(os.path.join(HERE, "kat.json"), "w"), indent=1)
+    json.dump(QUIRKS, open(os.path.join(HERE, "quirk_blocks.json"), "w"), indent=1)
+    print("wrote tests/golden/{one_key,empty}.mtbl, kat.json, quirk_blocks.json")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+"""GPU parity: the HIP decoder (through the C ABI) vs the CPU oracle, bit-exact.
+
+All cases run in ONE process.  Sizes are small enough for the oracle to finish in
+seconds; the full BASELINE cfg2 size is checked through size-independent properties
+(decode(encode(x)) == x against the generator's own records, totals == footer counts).
+"""
+import numpy as np
+import pytest
+
+import corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mtblx import codec
+    return codec
+
+
+def device_decode(data, off, ln):
+    codec = _dev()
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    out = codec.decode_blocks(batch)
+    import torch
+    torch.cuda.synchronize()
+    return out.to_host()
+
+
+def assert_same(dev, orc, nblk):
+    assert np.array_equal(dev.status, orc.status), np.nonzero(dev.status != orc.status)[0][:10]
+    assert np.array_equal(dev.nrec, orc.nrec), np.nonzero(dev.nrec != orc.nrec)[0][:10]
+    assert np.array_equal(dev.rec_base, orc.rec_base)
+    assert np.array_equal(dev.key_base, orc.key_base)
+    assert np.array_equal(dev.val_base, orc.val_base)
+    nr = int(orc.nrec.sum())
+    assert dev.totals[0] == nr and dev.totals[1] == orc.keys.size and dev.totals[2] == orc.vals.size
+    assert dev.totals[3] == 0
+    assert np.array_equal(dev.key_end, orc.key_end)
+    assert np.array_equal(dev.val_end, orc.val_end)
+    if not np.array_equal(dev.keys, orc.keys):
+        bad = np.nonzero(dev.keys != orc.keys)[0]
+        raise AssertionError(f"key bytes differ at {bad[:10]} (of {bad.size})")
+    assert np.array_equal(dev.vals, orc.vals)
+
+
+def run_both(oracle, blocks, rng=None, lead=0):
+    data, off, ln = corpus.pack(blocks, lead=lead, rng=rng)
+    orc = oracle.decode_blocks(data, off, ln)
+    dev = device_decode(data, off, ln)
+    assert_same(dev, orc, len(blocks))
+    return orc
+
+
+def test_quirk_blocks(oracle):
+    q = corpus.quirk_blocks()
+    orc = run_both(oracle, [b for _, b, _ in q])
+    for i, (_, _, exp) in enumerate(q):
+        assert orc.status[i] == exp["status"]
+
+
+def test_builder_blocks_all_shapes(oracle):
+    blocks = corpus.builder_blocks(oracle, seed=5, count=300, max_bytes=8100)
+    orc = run_both(oracle, blocks, rng=np.random.default_rng(1), lead=3)
+    assert (orc.status == 0).all()
+
+
+def test_mutated_blocks(oracle):
+    blocks = corpus.mutated_blocks(oracle, seed=9, count=800)
+    orc = run_both(oracle, blocks, rng=np.random.default_rng(2))
+    # the corpus must exercise every outcome
+    assert {0, 1, 2} <= set(orc.status.tolist())
+
+
+def test_large_blocks_generic_path(oracle):
+    rng = np.random.default_rng(4)
+    blocks = []
+    for n in (200, 400, 900):
+        recs = corpus.random_records(rng, n, 4, 60, 10, 120)
+        blocks.append(oracle.build_block(recs))
+    assert max(len(b) for b in blocks) > 8192
+    run_both(oracle, blocks + corpus.builder_blocks(oracle, seed=6, count=20))
+
+
+def test_block_at_end_of_buffer(oracle):
+    """last block ends exactly at data_len: staging must not read past the buffer"""
+    blocks = corpus.builder_blocks(oracle, seed=12, count=7, max_bytes=4000)
+    for lead in (0, 1, 5, 15):
+        run_both(oracle, blocks, lead=lead)
+
+
+def test_cfg2_sample_vs_oracle(oracle):
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(3000)
+    orc = oracle.decode_blocks(data, off, ln)
+    dev = device_decode(data, off, ln)
+    assert_same(dev, orc, off.size)
+
+
+def test_overflow_reported(oracle):
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(64)
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    orc = oracle.decode_blocks(data, off, ln)
+    out = codec.DecodedBlocks(off.size, int(orc.nrec.sum()), orc.keys.size // 2, orc.vals.size)
+    ws = codec.Workspace(off.size)
+    codec.decode_into(batch, out, ws)
+    torch.cuda.synchronize()
+    h = out.to_host()
+    assert h.totals[3] & 1
+    st = h.status
+    assert (st[: off.size // 2 - 1] == 0).all() and (st[off.size // 2 + 1:] == 5).all()
+
+
+def test_cfg2_full_roundtrip_property():
+    """BASELINE cfg2 at full size (100 k blocks): decode(encode(x)) == x for every record."""
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    nblk = 100_000
+    data, off, ln = synth.cfg2_file(nblk)
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    out = codec.decode_blocks(batch)
+    torch.cuda.synchronize()
+    nr, kb, vb, flags = out.totals_host()
+    assert flags == 0
+    assert (out.status[:nblk] == 0).all().item()
+    kl, vl = 16, 64
+    # regenerate the writer's input records (same generator call as synth.cfg2_file)
+    dk = out.keys[:kb].cpu().numpy()
+    dv = out.vals[:vb].cpu().numpy()
+    assert kb == nr * kl and vb == nr * vl
+    big_keys, big_vals, _, _ = synth.cfg2_arrays(int(nblk * ((4096 - 64) // 79) * 1.02) + 64)
+    assert np.array_equal(dk, big_keys[: kb])
+    assert np.array_equal(dv, big_vals[: vb])
+    ke = out.key_end[:nr].cpu().numpy().view(np.uint32)
+    nrec = out.nrec[:nblk].cpu().numpy()
+    rb = np.concatenate([[0], np.cumsum(nrec)[:-1]])
+    # last record of every block ends at 16 * nrec of that block
+    assert np.array_equal(ke[rb + nrec - 1], 16 * nrec.astype(np.uint32))

@@ -1,0 +1,182 @@
+"""CPU tests: the oracle against the golden vectors and the reference's own test scenarios,
+and the product's host layer (Writer, framing, CRC) against the oracle.  No GPU needed."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import corpus
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def kat():
+    return json.load(open(os.path.join(GOLD, "kat.json")))
+
+
+# ---------------- oracle pinned by the golden vectors ----------------
+def test_crc32c_check_value(oracle):
+    assert oracle.crc32c(b"123456789") == 0xE3069283
+
+
+def test_kat_one_key_file(oracle):
+    k = kat()["one_key"]
+    f = oracle.write_file([(b"hello", b"I'm the one")])
+    assert len(f) == k["file_len"]
+    assert f[:54].hex() == k["first_54"]
+    assert hashlib.sha256(f).hexdigest() == k["sha256"]
+    assert f == open(os.path.join(GOLD, "one_key.mtbl"), "rb").read()
+
+
+def test_kat_empty_file(oracle):
+    e = kat()["empty"]
+    f = oracle.write_file([])
+    assert len(f) == e["file_len"]
+    assert hashlib.sha256(f).hexdigest() == e["sha256"]
+
+
+def test_kat_block_contents(oracle):
+    k = kat()["one_key"]
+    st, recs = oracle.decode_block(bytes.fromhex(k["data_block_content"]))
+    assert st == 0 and recs == [(b"hello", b"I'm the one")]
+    st, recs = oracle.decode_block(bytes.fromhex(k["index_block_content"]))
+    assert st == 0 and recs == [(b"hello", b"\x00")]
+    assert oracle.crc32c(bytes.fromhex(k["data_block_content"])) == int(k["data_block_crc"], 16)
+
+
+@pytest.mark.parametrize("name,block,exp", corpus.quirk_blocks(), ids=[q[0] for q in corpus.quirk_blocks()])
+def test_quirk_blocks_hand_derived(oracle, name, block, exp):
+    st, recs = oracle.decode_block(block)
+    assert st == exp["status"], exp["why"]
+    assert recs == [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in exp["records"]], exp["why"]
+
+
+# ---------------- the reference's own tests, restated ----------------
+def test_reference_writer_empty(oracle):
+    """src/writer.rs:272-281 `empty`"""
+    r = oracle.file_scan(oracle.write_file([]))
+    assert r["end"] == oracle.END_NONE and r["records"] == []
+
+
+def test_reference_writer_one_key(oracle):
+    """src/writer.rs:283-298 `one_key`"""
+    r = oracle.file_scan(oracle.write_file([(b"hello", b"I'm the one")]))
+    assert len(r["records"]) == 1
+
+
+def test_reference_separator_too_short(oracle):
+    """src/writer.rs:300-305 `bytes_shortest_separator_to_short` must not panic"""
+    assert oracle.shortest_separator(bytes([49, 115, 116]), bytes([50])) is not None
+
+
+def test_varint_roundtrip_u32(oracle):
+    """src/varint.rs:103-111 qc_codec_u32 (seeded sweep instead of quickcheck)"""
+    rng = np.random.default_rng(7)
+    vals = [0, 1, 127, 128, 16383, 16384, (1 << 21) - 1, 1 << 21, (1 << 28) - 1, 1 << 28, 2**32 - 1]
+    vals += [int(x) for x in rng.integers(0, 2**32, 3000, dtype=np.uint64)]
+    for v in vals:
+        enc = oracle.varint_encode32(v)
+        assert oracle.varint_decode32(enc) == (v, len(enc))
+
+
+def test_varint_roundtrip_u64(oracle):
+    """src/varint.rs:113-120 qc_codec_u64"""
+    rng = np.random.default_rng(8)
+    vals = [0, 1, 2**35, 2**56 - 1, 2**63, 2**64 - 1] + [int(x) for x in rng.integers(0, 2**63, 3000, dtype=np.uint64)]
+    for v in vals:
+        enc = oracle.varint_encode64(v)
+        assert oracle.varint_decode64(enc) == (v, len(enc))
+
+
+def test_varint_decode32_quirks(oracle):
+    # unterminated within the 5-byte window: len 0, value = b0 & 0x7f (src/varint.rs:1-10,45-46)
+    assert oracle.varint_decode32(bytes([0x85, 0x80, 0x80, 0x80, 0x80, 0x01])) == (5, 0)
+    # 5th byte unmasked, high bits fall off the u32 (src/varint.rs:54)
+    assert oracle.varint_decode32(bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x7F])) == (0xFFFFFFFF, 5)
+    # empty slice: the reference indexes data[0] -> panic
+    assert oracle.varint_decode32(b"")[1] == -1
+
+
+# ---------------- file-level iteration (examples/dump.rs, cfg1) ----------------
+def test_cfg1_dump_roundtrip(oracle):
+    from mtblx import synth
+    recs = list(synth.cfg1_records())
+    f = oracle.write_file(recs, block_size=4096)
+    r = oracle.file_scan(f)
+    assert r["end"] == oracle.END_NONE
+    assert r["records"] == recs
+    assert r["meta"][3] == len(recs) and r["meta"][1] == 4096
+
+
+def test_get_prefix_range(oracle):
+    recs = [(f"k{i:05}".encode(), f"v{i}".encode()) for i in range(0, 3000, 3)]
+    f = oracle.write_file(recs, block_size=1024)
+    assert oracle.file_scan(f, "get", b"k00300")["records"] == [(b"k00300", b"v300")]
+    assert oracle.file_scan(f, "get", b"k00301")["records"] == []
+    pre = oracle.file_scan(f, "prefix", b"k001")["records"]
+    assert pre == [r for r in recs if r[0].startswith(b"k001")]
+    rng = oracle.file_scan(f, "range", b"k00100", b"k00200")["records"]
+    assert rng == [r for r in recs if b"k00100" <= r[0] <= b"k00200"]
+    frm = oracle.file_scan(f, "from", b"k02990")["records"]
+    assert frm == [r for r in recs if r[0] >= b"k02990"]
+
+
+def test_crc_mismatch_panics(oracle):
+    f = bytearray(oracle.write_file([(b"a", b"b"), (b"c", b"d")]))
+    f[8] ^= 1  # inside the data block content
+    assert oracle.file_scan(bytes(f))["end"] == oracle.END_PANIC
+    assert oracle.file_scan(bytes(f), verify=False)["end"] != oracle.END_PANIC
+
+
+def test_bad_magic_and_size(oracle):
+    f = bytearray(oracle.write_file([(b"a", b"b")]))
+    assert oracle.file_scan(bytes(f[:100]))["err"] == "InvalidMetadataSize"
+    f[-1] ^= 0xFF
+    assert oracle.file_scan(bytes(f))["err"] == "InvalidFormatVersion"
+
+
+# ---------------- product host layer vs oracle ----------------
+def test_product_writer_matches_oracle(oracle):
+    import mtblx
+    rng = np.random.default_rng(11)
+    for trial in range(30):
+        bs = int(rng.choice([1024, 1500, 4096, 8192]))
+        iv = int(rng.choice([1, 4, 16, 33]))
+        recs = corpus.random_records(rng, int(rng.integers(0, 400)), 0, 60, 0, 300)
+        w = mtblx.WriterBuilder().block_size(bs).block_restart_interval(iv).memory()
+        for k, v in recs:
+            w.insert(k, v)
+        assert w.into_inner() == oracle.write_file(recs, block_size=bs, restart_interval=iv), trial
+
+
+def test_product_writer_out_of_order(oracle):
+    import mtblx
+    w = mtblx.Writer.memory()
+    w.insert(b"b", b"1")
+    with pytest.raises(mtblx.OutOfOrderKey):
+        w.insert(b"a", b"2")
+
+
+def test_product_crc32c_matches_oracle(oracle, mtblx_lib):
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 7, 8, 9, 63, 64, 1000, 4099]:
+        a = rng.integers(0, 256, max(n, 1), dtype=np.uint8)
+        got = mtblx_lib.mtblx_crc32c(a.ctypes.data_as(C.POINTER(C.c_uint8)), n)
+        assert got == oracle.crc32c(a[:n].tobytes() if n else b"")
+
+
+def test_product_block_dir(oracle):
+    """the Writer's data-block directory points at exactly the framed contents"""
+    import mtblx
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(50)
+    raw = data.tobytes()
+    r = oracle.file_scan(raw)
+    assert r["end"] == oracle.END_NONE
+    dec = oracle.decode_blocks(data, off, ln)
+    assert (dec.status == 0).all() and int(dec.nrec.sum()) <= len(r["records"])
+    flat = [rec for b in range(off.size) for rec in dec.records(b)]
+    assert flat == r["records"][: len(flat)]

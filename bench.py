@@ -6,9 +6,9 @@ Metric (BASELINE.json): "KV records/s + GiB/s of block bytes decoded, device-res
 16 B keys / 64 B values, restart interval 16, CompressionType::None (SURVEY.md §8d),
 written by the product Writer from a seeded generator (synthetic data).
 
-A step = one full decode of the resident batch through the C ABI: mtblx_count_blocks
-(k_count + block scan) then mtblx_decode_counted (k_decode), i.e. every block's records
-reconstructed and laid out contiguously in HBM.  Inputs are in HBM before timing starts.
+A step = one full decode of the resident batch through the C ABI (mtblx_decode_blocks:
+one single-pass k_decode_tiles launch), i.e. every block's records reconstructed and laid
+out contiguously in HBM.  Inputs are in HBM before timing starts.
 
 Multi-GPU (torchrun, one rank per GPU): blocks are independent, so every rank decodes
 its own 100 k-block shard (weak scaling, no data-path collective); the only collectives
@@ -79,8 +79,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=100_000)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_decode.json"),
-                    help="PMC-derived HBM bytes per k_decode launch (profiles/, from a rocprofv3 --pmc run)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_decode_tiles.json"),
+                    help="PMC-derived HBM bytes per k_decode_tiles launch (profiles/, from a rocprofv3 --pmc run)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,18 +109,15 @@ def main():
     del probe
     block_bytes = int(ln.sum(dtype=np.uint64))
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
+        # one mtblx_decode_blocks call = 2 tiny memsets (look-back words, totals) + k_decode_tiles
         if i is not None:
             ev[i][0].record(stream)
-        codec.count_blocks(batch, out, ws, stream)
+        codec.decode_into(batch, out, ws, stream)
         if i is not None:
             ev[i][1].record(stream)
-        codec.decode_counted(batch, out, ws, stream)
-        if i is not None:
-            ev[i][2].record(stream)
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
@@ -146,14 +143,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    k_count_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-    k_decode_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    k_decode_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     ms_per_step = elapsed * 1e3 / args.steps
     total_bytes = block_bytes * world
     total_recs = nrec * world
     value = total_bytes / (elapsed / args.steps) / 2**30
 
-    # roofline of the dominant kernel (k_decode): algorithmic bytes per launch
+    # roofline of the (only) kernel k_decode_tiles: algorithmic bytes per launch
     alg_bytes = block_bytes + kbytes + vbytes + 8 * nrec + 24 * batch.nblk
     achieved = alg_bytes / (k_decode_ms * 1e-3) / 1e9
     traffic = None
@@ -182,10 +178,10 @@ def main():
                    "blocks_per_gpu": int(batch.nblk), "block_bytes_per_gpu": block_bytes,
                    "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
                    "parallelism": f"block-sharded x{world}, no collective"},
-        "kernels_ms": {"k_count+scan": round(k_count_ms, 4), "k_decode": round(k_decode_ms, 4)},
+        "kernels_ms": {"k_decode_tiles (events incl. 2 memsets)": round(k_decode_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_decode", "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel": "k_decode_tiles", "alg_bytes_per_launch": int(alg_bytes)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(data, off, ln, args.cpu_seconds)

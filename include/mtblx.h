@@ -98,9 +98,9 @@ int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, v
 int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* workspace,
                        size_t workspace_bytes, void* stream);
 
-/* Second half of a count/decode split: writes keys/values using the counts and bases a
- * previous mtblx_count_blocks left in `out` and `workspace` (same batch, same workspace,
- * same stream).  count + decode_counted == decode_blocks. */
+/* Second half of a count/decode split (count to size the outputs, then write).  The
+ * kernel is single-pass (counting fused into the decode), so this is the same work as
+ * mtblx_decode_blocks; kept so callers written against the split stay valid. */
 int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* workspace,
                          size_t workspace_bytes, void* stream);
 

@@ -1,26 +1,18 @@
-// decode.hip — MI355X (gfx950) kernels for mtbl data-block decode.
+// decode.hip — MI355X (gfx950) kernel for mtbl data-block decode.
 //
 // Replaces the reference's per-record CPU scan of one block
 //   Block::init            /root/reference/src/block.rs:16-49
 //   BlockIter::init        src/block.rs:75-93
 //   seek_to_first / next / get / parse_next_key / decode_entry   src/block.rs:119-238
 //   varint_decode32        src/varint.rs:44-61
-// with a batched device decode of many blocks, laid out contiguously (include/mtblx.h).
-//
-// Kernel pipeline (two-pass form; DESIGN.md "Kernels"):
-//   k_count   one wave per block: stage block HBM->LDS, walk the restart intervals in
-//             parallel (one lane per interval), validate the "regular" fast path, count
-//             records / key bytes / value bytes.  Irregular blocks run the exact serial
-//             emulation (generic path) in lane 0 instead.
-//   k_scan_*  exclusive prefix sums over blocks -> rec_base / key_base / val_base.
-//   k_decode  one wave per block: stage, walk twice (counts, then per-record metadata
-//             into LDS), then every lane copies whole records: value bytes LDS->HBM,
-//             key bytes resolved through the shared-prefix chain straight from the
-//             staged suffix bytes (no per-key serial rebuild).
+// with ONE single-pass launch over a batch of blocks, output laid out contiguously
+// (include/mtblx.h).  See k_decode_tiles below and DESIGN.md "Kernels".
 //
 // Everything is integer/byte work: HBM-bandwidth bound, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "mtblx.h"
 
@@ -122,105 +114,6 @@ __device__ __forceinline__ uint32_t dec32(const uint4& W, uint32_t k, uint32_t a
 }
 
 // ----------------------------------------------------------------------------------
-// per-wave LDS state of the fast path
-// ----------------------------------------------------------------------------------
-template <int STAGE>
-struct alignas(16) WaveLds {
-  static constexpr int kMaxRec = STAGE / 16;   // avg record >= 16 B, else generic path
-  static constexpr int kMaxInt = 256;          // restart intervals handled by the fast path
-  uint8_t stage[STAGE + 64];                   // 16 B front pad; block byte i at boff + i
-  uint16_t rpos[kMaxRec];                      // block offset of the key suffix
-  uint16_t rsh[kMaxRec];                       // shared
-  uint16_t rns[kMaxRec];                       // non_shared
-  uint16_t rvl[kMaxRec];                       // value_length
-  uint16_t rks[kMaxRec];                       // key start, relative to the block's key base
-  uint16_t rvs[kMaxRec];                       // value start, relative to the block's value base
-  uint16_t ibr[kMaxInt];                       // per-interval record base
-  uint16_t ibk[kMaxInt];                       // per-interval key-byte base
-  uint16_t ibv[kMaxInt];                       // per-interval value-byte base
-};
-
-// Stage block [gbase, gbase+L) into lds.stage; returns boff (stage offset of byte 0).
-// data_lo/data_hi bound the readable device range.
-__device__ __forceinline__ uint32_t stage_block(uint8_t* stage, const uint8_t* gptr, uint32_t L,
-                                                const uint8_t* data_lo, const uint8_t* data_hi, int lane) {
-  uintptr_t ga = reinterpret_cast<uintptr_t>(gptr);
-  uintptr_t a0 = ga & ~uintptr_t(15);
-  uint32_t delta = (uint32_t)(ga - a0);
-  uint32_t nch = (delta + L + 15u) >> 4;
-  uintptr_t lo = reinterpret_cast<uintptr_t>(data_lo), hi = reinterpret_cast<uintptr_t>(data_hi);
-  for (uint32_t c = lane; c < nch; c += kWave) {
-    uintptr_t a = a0 + 16u * c;
-    uint4 v;
-    if (a >= lo && a + 16 <= hi) {
-      v = *reinterpret_cast<const uint4*>(a);
-    } else {
-      uint8_t t[16];
-      for (int i = 0; i < 16; ++i) t[i] = (a + i >= lo && a + i < hi) ? *reinterpret_cast<const uint8_t*>(a + i) : 0;
-      v = make_uint4((uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24,
-                     (uint32_t)t[4] | (uint32_t)t[5] << 8 | (uint32_t)t[6] << 16 | (uint32_t)t[7] << 24,
-                     (uint32_t)t[8] | (uint32_t)t[9] << 8 | (uint32_t)t[10] << 16 | (uint32_t)t[11] << 24,
-                     (uint32_t)t[12] | (uint32_t)t[13] << 8 | (uint32_t)t[14] << 16 | (uint32_t)t[15] << 24);
-    }
-    *reinterpret_cast<uint4*>(stage + 16 + 16 * c) = v;
-  }
-  return 16u + delta;
-}
-
-// One restart interval [s, e) of a staged block.  Fast-path preconditions:
-// every entry decodes without a reference panic, the interval's first entry has
-// shared == 0, later entries have shared <= previous key length, the walk lands exactly
-// on e.  Under these the reference's linear chain (src/block.rs:119-143) visits exactly
-// these entries and rebuilds exactly these keys.  Returns false if not satisfied.
-template <bool PASS2, int STAGE>
-__device__ __forceinline__ bool walk_interval(WaveLds<STAGE>& S, uint32_t boff, uint32_t L, uint32_t R,
-                                              uint32_t s, uint32_t e, uint32_t& cnt, uint32_t& kb, uint32_t& vb,
-                                              uint32_t rbase, uint32_t kbase, uint32_t vbase, uint32_t* key_end,
-                                              uint32_t* val_end) {
-  cnt = kb = vb = 0;
-  if (!(s < e && e <= R)) return false;
-  uint32_t p = s, prevlen = 0;
-  bool first = true;
-  while (p < e) {
-    if (R - p < 3u) return false;                         // decode_entry Err -> panic
-    uint4 W = lds_win16(S.stage, boff + p);
-    uint32_t sh = W.x & 0xffu, ns = (W.x >> 8) & 0xffu, vl = (W.x >> 16) & 0xffu, h = 3;
-    if ((sh | ns | vl) >= 128u) {                         // slow header path
-      uint32_t l0 = dec32(W, 0, L - p, sh);
-      if (l0 == 0) return false;
-      uint32_t l1 = dec32(W, l0, L - p - l0, ns);
-      if (l1 == 0) return false;
-      uint32_t l2 = dec32(W, l0 + l1, L - p - l0 - l1, vl);
-      if (l2 == 0) return false;
-      h = l0 + l1 + l2;
-      if (p + h > R) return false;                        // assert!(p <= limit)
-    }
-    if ((uint64_t)ns + vl > (uint64_t)(R - p - h)) return false;
-    if (first ? (sh != 0) : (sh > prevlen)) return false;
-    uint32_t klen = sh + ns;
-    if (klen > 0xFFFFu) return false;
-    if (PASS2) {
-      uint32_t r = rbase + cnt;
-      S.rpos[r] = (uint16_t)(p + h);
-      S.rsh[r] = (uint16_t)sh;
-      S.rns[r] = (uint16_t)ns;
-      S.rvl[r] = (uint16_t)vl;
-      S.rks[r] = (uint16_t)(kbase + kb);
-      S.rvs[r] = (uint16_t)(vbase + vb);
-      key_end[r] = kbase + kb + klen;
-      val_end[r] = vbase + vb + vl;
-    }
-    cnt += 1;
-    kb += klen;
-    vb += vl;
-    prevlen = klen;
-    first = false;
-    p += h + ns + vl;
-  }
-  return p == e;
-}
-
-// ----------------------------------------------------------------------------------
 // generic path: exact serial emulation of the reference on one block, lane 0 only,
 // reading HBM directly.  Handles every quirk (DESIGN.md "Reference quirks").
 // ----------------------------------------------------------------------------------
@@ -319,116 +212,209 @@ __device__ GenOut generic_block(const uint8_t* d, uint64_t L, uint8_t* keys, uin
 }
 
 // ----------------------------------------------------------------------------------
-// fast-path block analysis shared by count and decode
+// single-pass tiled decoder
 // ----------------------------------------------------------------------------------
-struct FastInfo {
-  bool ok;
-  uint32_t nrec, kb, vb;
-  uint32_t L, R, n, boff;
+// A tile = up to `bpt` consecutive blocks of the batch, staged together in the LDS of
+// one workgroup (256 threads).  Workgroups are persistent and take tiles t = blockIdx.x,
+// + gridDim.x, ... (static round-robin; the grid never exceeds the resident capacity).
+// Per tile:
+//   stage -> parse trailers -> walk (one thread per restart interval, across all blocks
+//   of the tile) -> tile-local scans -> publish the tile aggregate -> decoupled
+//   look-back for the tile's global (record, key byte, value byte) prefix -> per-block
+//   outputs -> second walk writes per-record metadata -> every thread copies records.
+// Blocks that are not "regular" (see walk_interval) run the exact serial emulation.
+
+constexpr uint32_t kNotStaged = 0xFFFFFFFFu;
+constexpr uint64_t kFlagA = 1ull << 62;   // look-back word holds the tile aggregate
+constexpr uint64_t kFlagP = 2ull << 62;   // look-back word holds the inclusive prefix
+constexpr uint64_t kValMask = (1ull << 62) - 1;
+constexpr int kThreads = 256;
+
+template <int TB_, int MAXREC_, int MAXINT_, int MAXBLK_>
+struct TileCfg {
+  static constexpr int TB = TB_;          // staging bytes
+  static constexpr int MAXREC = MAXREC_;  // records with metadata per tile
+  static constexpr int MAXINT = MAXINT_;  // restart intervals per tile
+  static constexpr int MAXBLK = MAXBLK_;  // blocks per tile
 };
 
-// Walk pass 1 over all intervals of a staged block; fills S.ib* with exclusive bases.
-template <int STAGE>
-__device__ FastInfo fast_analyze(WaveLds<STAGE>& S, uint32_t boff, uint32_t L, int lane) {
-  FastInfo fi{false, 0, 0, 0, L, 0, 0, boff};
-  if (L < 8 || L > (uint32_t)STAGE) return fi;
-  uint32_t n = lds_rd32(S.stage, boff + L - 4);
-  if (n == 0 || (uint64_t)(n + 1ull) * 4ull > L) return fi;
-  if (n > (uint32_t)WaveLds<STAGE>::kMaxInt) return fi;
-  uint32_t R = L - 4u * (n + 1u);
-  fi.R = R;
-  fi.n = n;
-  bool ok = true;
-  uint32_t rb = 0, kbt = 0, vbt = 0;
-  for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
-    uint32_t i = c0 + lane;
-    uint32_t cnt = 0, kb = 0, vb = 0;
-    bool lok = true;
-    if (i < n) {
-      uint32_t s = lds_rd32(S.stage, boff + R + 4u * i);
-      uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, boff + R + 4u * (i + 1)) : R;
-      lok = walk_interval<false>(S, boff, L, R, s, e, cnt, kb, vb, 0, 0, 0, nullptr, nullptr);
+template <class C>
+struct alignas(16) TileLds {
+  uint8_t stage[C::TB];
+  // per block of the tile
+  uint32_t boff[C::MAXBLK];   // stage offset of block byte 0 (kNotStaged if not staged)
+  uint32_t blen[C::MAXBLK];
+  uint32_t bR[C::MAXBLK];     // restart offset
+  uint32_t bn[C::MAXBLK];     // restart count
+  uint32_t bint0[C::MAXBLK + 1];
+  uint32_t bok[C::MAXBLK];    // 1 = regular fast path
+  uint32_t bwr[C::MAXBLK];    // 1 = outputs of this block are written
+  int32_t bst[C::MAXBLK];
+  uint32_t bcnt[C::MAXBLK], bkb[C::MAXBLK], bvb[C::MAXBLK];   // block totals
+  uint32_t brb[C::MAXBLK], bkbb[C::MAXBLK], bvbb[C::MAXBLK];  // tile-relative block bases
+  // per restart interval: counts after walk 1, exclusive tile-relative bases after the scan
+  uint32_t icnt[C::MAXINT + 1], ikb[C::MAXINT + 1], ivb[C::MAXINT + 1];
+  uint8_t iblk[C::MAXINT];
+  // per record (fast blocks), tile-relative index
+  uint16_t rpos[C::MAXREC];   // block offset of the key suffix
+  uint16_t rsh[C::MAXREC];
+  uint16_t rns[C::MAXREC];
+  uint16_t rvl[C::MAXREC];
+  uint32_t rks[C::MAXREC];    // tile-relative key start
+  uint32_t rvs[C::MAXREC];    // tile-relative value start
+  uint8_t rblk[C::MAXREC];
+  // tile scalars
+  uint64_t tpre[3];           // global exclusive prefix of the tile (records, key bytes, value bytes)
+  uint32_t ttot[3];           // tile totals
+  uint32_t nfastrec;
+  uint32_t wsum[4][3];        // per-wave scan totals
+};
+
+// Stage one block into a 16-byte aligned slot; returns the offset of block byte 0 within
+// the slot (the block's global misalignment).  Reads stay inside [lo, hi).
+__device__ __forceinline__ uint32_t stage_slot(uint8_t* slot, const uint8_t* gptr, uint32_t L, uintptr_t lo,
+                                               uintptr_t hi, int lane) {
+  uintptr_t ga = reinterpret_cast<uintptr_t>(gptr);
+  uintptr_t a0 = ga & ~uintptr_t(15);
+  uint32_t delta = (uint32_t)(ga - a0);
+  uint32_t nch = (delta + L + 15u) >> 4;
+  uint32_t c = lane;
+  // main body: 4 independent 16-byte loads in flight per lane
+  for (; c + 3 * kWave < nch; c += 4 * kWave) {
+    uintptr_t a = a0 + 16u * c;
+    if (a >= lo && a + 16 * (3 * kWave) + 16 <= hi) {
+      uint4 v0 = *reinterpret_cast<const uint4*>(a);
+      uint4 v1 = *reinterpret_cast<const uint4*>(a + 16 * kWave);
+      uint4 v2 = *reinterpret_cast<const uint4*>(a + 32 * kWave);
+      uint4 v3 = *reinterpret_cast<const uint4*>(a + 48 * kWave);
+      *reinterpret_cast<uint4*>(slot + 16 * c) = v0;
+      *reinterpret_cast<uint4*>(slot + 16 * (c + kWave)) = v1;
+      *reinterpret_cast<uint4*>(slot + 16 * (c + 2 * kWave)) = v2;
+      *reinterpret_cast<uint4*>(slot + 16 * (c + 3 * kWave)) = v3;
+    } else {
+      break;
     }
-    ok = ok && (__ballot(!lok) == 0ull);
-    uint32_t ic = wave_incl_scan(cnt, lane);
-    uint32_t ik = wave_incl_scan(kb, lane);
-    uint32_t iv = wave_incl_scan(vb, lane);
-    if (i < n) {
-      S.ibr[i] = (uint16_t)(rb + ic - cnt);
-      S.ibk[i] = (uint16_t)(kbt + ik - kb);
-      S.ibv[i] = (uint16_t)(vbt + iv - vb);
-    }
-    rb += __shfl(ic, kWave - 1, kWave);
-    kbt += __shfl(ik, kWave - 1, kWave);
-    vbt += __shfl(iv, kWave - 1, kWave);
-    if (rb > (uint32_t)WaveLds<STAGE>::kMaxRec || kbt > 0xFFFFu) ok = false;
   }
-  fi.ok = ok;
-  fi.nrec = rb;
-  fi.kb = kbt;
-  fi.vb = vbt;
-  return fi;
+  for (; c < nch; c += kWave) {
+    uintptr_t a = a0 + 16u * c;
+    uint4 v;
+    if (a >= lo && a + 16 <= hi) {
+      v = *reinterpret_cast<const uint4*>(a);
+    } else {
+      uint32_t t[4] = {0, 0, 0, 0};
+      for (int i = 0; i < 16; ++i)
+        if (a + i >= lo && a + i < hi) t[i >> 2] |= (uint32_t)(*reinterpret_cast<const uint8_t*>(a + i)) << (8 * (i & 3));
+      v = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    *reinterpret_cast<uint4*>(slot + 16 * c) = v;
+  }
+  return delta;
 }
 
-// ----------------------------------------------------------------------------------
-// kernels
-// ----------------------------------------------------------------------------------
-struct CountArgs {
+// One restart interval [s, e) of a staged block (block byte 0 at stage offset bo).
+// Regular-path preconditions (DESIGN.md "fast path"): every entry decodes without a
+// reference panic; varints are terminated; the interval's first entry has shared == 0;
+// later entries have shared <= previous key length (so Vec capacity never matters);
+// field values fit 16 bits; the walk lands exactly on e.  Under these the reference's
+// linear chain (src/block.rs:119-143) visits exactly these entries and rebuilds exactly
+// these keys.  Returns false if they do not hold.
+template <bool WRITE, class C>
+__device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32_t L, uint32_t R, uint32_t s,
+                                              uint32_t e, uint32_t& cnt, uint32_t& kb, uint32_t& vb, uint32_t rbase,
+                                              uint32_t kbase, uint32_t vbase, uint32_t blk, uint32_t rlo,
+                                              uint32_t rhi, uint32_t* key_end, uint32_t* val_end,
+                                              uint32_t kend0, uint32_t vend0) {
+  cnt = kb = vb = 0;
+  if (!(s < e && e <= R)) return false;
+  uint32_t p = s, prevlen = 0;
+  bool first = true;
+  while (p < e) {
+    if (R - p < 3u) return false;                         // decode_entry Err -> panic
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(S.stage + ((bo + p) & ~3u));
+    uint32_t sft = ((bo + p) & 3u) * 8u;
+    uint32_t hw = __builtin_amdgcn_alignbit(w[1], w[0], sft);
+    uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu, h = 3;
+    if ((hw & 0x808080u) != 0u) {                         // slow header path
+      uint4 W = lds_win16(S.stage, bo + p);
+      uint32_t l0 = dec32(W, 0, L - p, sh);
+      if (l0 == 0) return false;
+      uint32_t l1 = dec32(W, l0, L - p - l0, ns);
+      if (l1 == 0) return false;
+      uint32_t l2 = dec32(W, l0 + l1, L - p - l0 - l1, vl);
+      if (l2 == 0) return false;
+      h = l0 + l1 + l2;
+      if (p + h > R) return false;                        // assert!(p <= limit)
+      if ((sh | ns | vl) > 0xFFFFu) return false;
+    }
+    if (ns + vl > R - p - h) return false;                // no overflow: both < 2^16
+    if (first ? (sh != 0) : (sh > prevlen)) return false;
+    const uint32_t klen = sh + ns;
+    if (klen > 0xFFFFu) return false;
+    if (WRITE) {
+      const uint32_t r = rbase + cnt;
+      if (r >= rlo && r < rhi) {
+        const uint32_t q = r - rlo;
+        S.rpos[q] = (uint16_t)(p + h);
+        S.rsh[q] = (uint16_t)sh;
+        S.rns[q] = (uint16_t)ns;
+        S.rvl[q] = (uint16_t)vl;
+        S.rks[q] = kbase + kb;
+        S.rvs[q] = vbase + vb;
+        S.rblk[q] = (uint8_t)blk;
+      }
+      if (key_end) {
+        key_end[cnt] = kend0 + kb + klen;
+        val_end[cnt] = vend0 + vb + vl;
+      }
+    }
+    cnt += 1;
+    kb += klen;
+    vb += vl;
+    prevlen = klen;
+    first = false;
+    p += h + ns + vl;
+  }
+  return p == e;
+}
+
+// exclusive scan of 3 u32 per thread over the workgroup; returns the workgroup totals
+template <class C>
+__device__ __forceinline__ void wg_excl_scan3(TileLds<C>& S, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t tot[3]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane), ic = wave_incl_scan(c, lane);
+  if (lane == kWave - 1) { S.wsum[wv][0] = ia; S.wsum[wv][1] = ib; S.wsum[wv][2] = ic; }
+  __syncthreads();
+  uint32_t oa = 0, ob = 0, oc = 0;
+  tot[0] = tot[1] = tot[2] = 0;
+  for (int k = 0; k < kThreads / kWave; ++k) {
+    if (k < wv) { oa += S.wsum[k][0]; ob += S.wsum[k][1]; oc += S.wsum[k][2]; }
+    tot[0] += S.wsum[k][0]; tot[1] += S.wsum[k][1]; tot[2] += S.wsum[k][2];
+  }
+  a = oa + ia - a;
+  b = ob + ib - b;
+  c = oc + ic - c;
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+
+struct TileArgs {
   const uint8_t* data;
   uint64_t data_len;
   const uint64_t* blk_off;
   const uint32_t* blk_len;
   uint32_t nblk;
+  uint32_t bpt;     // blocks per tile
+  uint32_t slot;    // staging slot bytes per block (multiple of 16)
+  uint32_t ntiles;
   uint32_t* nrec;
-  uint64_t* kb;
-  uint64_t* vb;
-  int32_t* status;
-};
-
-template <int STAGE, int WPG>
-__global__ void __launch_bounds__(WPG * 64) k_count(CountArgs a) {
-  __shared__ WaveLds<STAGE> lds[WPG];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const uint32_t b = blockIdx.x * WPG + w;
-  if (b >= a.nblk) return;
-  WaveLds<STAGE>& S = lds[w];
-  const uint32_t L = a.blk_len[b];
-  const uint8_t* g = a.data + a.blk_off[b];
-  FastInfo fi{false, 0, 0, 0, L, 0, 0, 0};
-  if (L >= 8 && L <= (uint32_t)STAGE) {
-    uint32_t boff = stage_block(S.stage, g, L, a.data, a.data + a.data_len, lane);
-    wave_sync();
-    fi = fast_analyze<STAGE>(S, boff, L, lane);
-  }
-  if (fi.ok) {
-    if (lane == 0) {
-      a.nrec[b] = fi.nrec;
-      a.kb[b] = fi.kb;
-      a.vb[b] = fi.vb;
-      a.status[b] = MTBLX_ST_OK;
-    }
-  } else if (lane == 0) {
-    GenOut o = generic_block<false>(g, L, nullptr, nullptr, nullptr, nullptr);
-    a.nrec[b] = o.nrec;
-    a.kb[b] = o.kb;
-    a.vb[b] = o.vb;
-    a.status[b] = o.st;
-  }
-}
-
-struct DecodeArgs {
-  const uint8_t* data;
-  uint64_t data_len;
-  const uint64_t* blk_off;
-  const uint32_t* blk_len;
-  uint32_t nblk;
-  const uint32_t* nrec;
-  const uint64_t* kbytes;
-  const uint64_t* vbytes;
-  const uint64_t* rec_base;
-  const uint64_t* key_base;
-  const uint64_t* val_base;
+  uint64_t* rec_base;
+  uint64_t* key_base;
+  uint64_t* val_base;
   int32_t* status;
   uint32_t* key_end;
   uint32_t* val_end;
@@ -438,178 +424,297 @@ struct DecodeArgs {
   uint8_t* vals;
   uint64_t vals_cap;
   uint64_t* totals;
+  uint64_t* lb;     // [ntiles * 3] look-back words, zeroed before launch
+  int write;
 };
 
-template <int STAGE, int WPG>
-__global__ void __launch_bounds__(WPG * 64) k_decode(DecodeArgs a) {
-  __shared__ WaveLds<STAGE> lds[WPG];
+// Decoupled look-back (wave 0): publish the tile aggregate, walk predecessors back in
+// windows of 64 until every quantity meets an inclusive prefix; publish our own.
+// Look-back words are single 8-byte agent-scope atomics: the value IS the flag, so no
+// fence is needed (MI355X_MICROARCH.md, hand-off granules).  Spins are bounded: on
+// timeout bit1 of totals[3] is set instead of hanging.
+__device__ void tile_lookback(uint64_t* lb, uint32_t t, const uint32_t agg[3], uint64_t pre[3], uint64_t* totals) {
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const uint32_t b = blockIdx.x * WPG + w;
-  if (b >= a.nblk) return;
-  WaveLds<STAGE>& S = lds[w];
-  const uint32_t L = a.blk_len[b];
-  const uint8_t* g = a.data + a.blk_off[b];
-  const uint64_t rb = a.rec_base[b], kb0 = a.key_base[b], vb0 = a.val_base[b];
-  const uint32_t nr = a.nrec[b];
-  if (rb + nr > a.rec_cap || kb0 + a.kbytes[b] > a.keys_cap || vb0 + a.vbytes[b] > a.vals_cap) {
-    if (lane == 0) {
-      a.status[b] = MTBLX_ST_OVERFLOW;
-      atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 1ull);
-    }
+  if (t == 0) {
+    if (lane < 3) __hip_atomic_store(&lb[lane], kFlagP | agg[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pre[0] = pre[1] = pre[2] = 0;
     return;
   }
-  uint32_t* key_end = a.key_end + rb;
-  uint32_t* val_end = a.val_end + rb;
-  uint8_t* keys = a.keys + kb0;
-  uint8_t* vals = a.vals + vb0;
-
-  FastInfo fi{false, 0, 0, 0, L, 0, 0, 0};
-  uint32_t boff = 0;
-  if (L >= 8 && L <= (uint32_t)STAGE) {
-    boff = stage_block(S.stage, g, L, a.data, a.data + a.data_len, lane);
-    wave_sync();
-    fi = fast_analyze<STAGE>(S, boff, L, lane);
-  }
-  if (!fi.ok) {
-    if (lane == 0) generic_block<true>(g, L, keys, vals, key_end, val_end);
-    return;
-  }
-  // pass 2: per-record metadata into LDS, key_end/val_end to HBM
-  const uint32_t R = fi.R, n = fi.n;
-  for (uint32_t i = lane; i < n; i += kWave) {
-    uint32_t s = lds_rd32(S.stage, boff + R + 4u * i);
-    uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, boff + R + 4u * (i + 1)) : R;
-    uint32_t c, k, v;
-    walk_interval<true>(S, boff, L, R, s, e, c, k, v, S.ibr[i], S.ibk[i], S.ibv[i], key_end, val_end);
-  }
-  wave_sync();
-  // copy: one lane per record
-  for (uint32_t r = lane; r < fi.nrec; r += kWave) {
-    const uint32_t vl = S.rvl[r];
-    const uint32_t vsrc = boff + S.rpos[r] + S.rns[r];
-    uint8_t* vd = vals + S.rvs[r];
-    for (uint32_t o = 0; o < vl; o += 16) {
-      uint4 wv = lds_win16(S.stage, vsrc + o);
-      uint32_t m = vl - o;
-      store_bytes(vd + o, wv, m < 16 ? m : 16);
-    }
-    const uint32_t shr = S.rsh[r];
-    const uint32_t klen = shr + S.rns[r];
-    uint8_t* kd = keys + S.rks[r];
-    for (uint32_t j0 = 0; j0 < klen; j0 += 16) {
-      const uint32_t jend = (j0 + 16 < klen) ? j0 + 16 : klen;
-      uint4 outw = make_uint4(0, 0, 0, 0);
-      uint32_t j = j0;
-      while (j < jend) {
-        // source of key byte j: the latest record s <= r with shared_s <= j
-        uint32_t s = r, m = klen, shs = shr;
-        while (shs > j) {
-          m = shs < m ? shs : m;
-          --s;
-          shs = S.rsh[s];
+  if (lane < 3)
+    __hip_atomic_store(&lb[3ull * t + lane], kFlagA | agg[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t acc[3] = {0, 0, 0};
+  bool done[3] = {false, false, false};
+  int64_t base = (int64_t)t - 1;
+  bool timeout = false;
+  while (!(done[0] && done[1] && done[2])) {
+    const int64_t p = base - lane;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (done[q]) continue;
+      uint64_t w = kFlagP;  // before tile 0: inclusive prefix 0
+      if (p >= 0) {
+        uint32_t spins = 0;
+        for (;;) {
+          w = __hip_atomic_load(&lb[3ull * p + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (w >> 62) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 24)) { timeout = true; w = kFlagP; break; }
         }
-        const uint32_t seg = m < jend ? m : jend;
-        const uint32_t src = boff + S.rpos[s] + (j - shs);
-        uint4 wv = lds_win16(S.stage, src - (j - j0));
-        merge_bytes(outw, wv, (int)(j - j0), (int)(seg - j0));
-        j = seg;
       }
-      store_bytes(kd + j0, outw, jend - j0);
+      const uint64_t pm = __ballot((w >> 62) == 2u);
+      uint64_t v = w & kValMask;
+      if (pm) {
+        const int first = __builtin_ctzll(pm);
+        if (lane > first) v = 0;
+        done[q] = true;
+      }
+      acc[q] += wave_sum64(v);
     }
+    base -= kWave;
   }
+  if (lane < 3) {
+    uint64_t incl = acc[lane] + agg[lane];
+    __hip_atomic_store(&lb[3ull * t + lane], kFlagP | incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (timeout && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(totals + 3), 2ull);
+  pre[0] = acc[0];
+  pre[1] = acc[1];
+  pre[2] = acc[2];
 }
 
-// ----------------------------------------------------------------------------------
-// scan over blocks: (nrec, key bytes, value bytes) -> exclusive bases + totals
-// ----------------------------------------------------------------------------------
-constexpr int kScanThreads = 256;
-constexpr int kScanItems = 8;
-constexpr int kScanTile = kScanThreads * kScanItems;
+template <class C>
+__global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
+  __shared__ TileLds<C> S;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(a.data), hi = lo + a.data_len;
 
-struct Trip {
-  uint64_t r, k, v;
-};
-__device__ __forceinline__ Trip tadd(Trip a, Trip b) { return Trip{a.r + b.r, a.k + b.k, a.v + b.v}; }
+  for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uint32_t b0 = t * a.bpt;
+    const uint32_t nb = min(a.bpt, a.nblk - b0);
 
-__device__ Trip block_excl_scan(Trip x, Trip* sh, Trip& total) {
-  // Hillis-Steele over 256 threads in LDS (scan kernels are a tiny share of the time)
-  const int t = threadIdx.x;
-  sh[t] = x;
-  __syncthreads();
-  for (int d = 1; d < kScanThreads; d <<= 1) {
-    Trip y = (t >= d) ? sh[t - d] : Trip{0, 0, 0};
-    __syncthreads();
-    if (t >= d) sh[t] = tadd(sh[t], y);
-    __syncthreads();
-  }
-  total = sh[kScanThreads - 1];
-  Trip incl = sh[t];
-  __syncthreads();
-  return Trip{incl.r - x.r, incl.k - x.k, incl.v - x.v};
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_scan_partial(const uint32_t* nrec, const uint64_t* kb,
-                                                                const uint64_t* vb, uint32_t nblk, Trip* part) {
-  __shared__ Trip sh[kScanThreads];
-  Trip acc{0, 0, 0};
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  for (int i = 0; i < kScanItems; ++i) {
-    uint64_t b = base + (uint64_t)i * kScanThreads + threadIdx.x;
-    if (b < nblk) acc = tadd(acc, Trip{nrec[b], kb[b], vb[b]});
-  }
-  Trip tot;
-  block_excl_scan(acc, sh, tot);
-  if (threadIdx.x == 0) part[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_scan_top(Trip* part, uint32_t nparts, uint64_t* totals) {
-  __shared__ Trip sh[kScanThreads];
-  Trip carry{0, 0, 0};
-  for (uint32_t c0 = 0; c0 < nparts; c0 += kScanThreads) {
-    uint32_t i = c0 + threadIdx.x;
-    Trip x = (i < nparts) ? part[i] : Trip{0, 0, 0};
-    Trip tot;
-    Trip ex = block_excl_scan(x, sh, tot);
-    if (i < nparts) part[i] = tadd(carry, ex);
-    carry = tadd(carry, tot);
-  }
-  if (threadIdx.x == 0) {
-    totals[0] = carry.r;
-    totals[1] = carry.k;
-    totals[2] = carry.v;
-    totals[3] = 0;
-  }
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_scan_final(const uint32_t* nrec, const uint64_t* kb,
-                                                              const uint64_t* vb, uint32_t nblk, const Trip* part,
-                                                              uint64_t* rec_base, uint64_t* key_base,
-                                                              uint64_t* val_base) {
-  __shared__ Trip sh[kScanThreads];
-  // thread t owns items base + t*kScanItems .. +kScanItems (contiguous)
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-  Trip loc[kScanItems];
-  Trip acc{0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    uint64_t b = base + i;
-    loc[i] = (b < nblk) ? Trip{nrec[b], kb[b], vb[b]} : Trip{0, 0, 0};
-    acc = tadd(acc, loc[i]);
-  }
-  Trip tot;
-  Trip ex = tadd(part[blockIdx.x], block_excl_scan(acc, sh, tot));
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    uint64_t b = base + i;
-    if (b < nblk) {
-      rec_base[b] = ex.r;
-      key_base[b] = ex.k;
-      val_base[b] = ex.v;
+    // ---- 1. stage: wave w stages blocks w, w+4, ... ----
+    for (uint32_t j = wv; j < nb; j += kThreads / kWave) {
+      const uint32_t L = a.blk_len[b0 + j];
+      const uint8_t* g = a.data + a.blk_off[b0 + j];
+      const uint32_t so = 16u + j * a.slot;
+      uint32_t bo = kNotStaged;
+      if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)C::TB) bo = so + stage_slot(S.stage + so, g, L, lo, hi, lane);
+      if (lane == 0) { S.boff[j] = bo; S.blen[j] = L; }
     }
-    ex = tadd(ex, loc[i]);
+    __syncthreads();
+
+    // ---- 2. trailers (Block::init, src/block.rs:16-49) ----
+    if (tid < (int)nb) {
+      const uint32_t j = tid, L = S.blen[j], bo = S.boff[j];
+      uint32_t n = 0, R = 0, ok = 0;
+      if (bo != kNotStaged && L >= 8) {
+        n = lds_rd32(S.stage, bo + L - 4);
+        if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
+      }
+      S.bn[j] = ok ? n : 0;
+      S.bR[j] = R;
+      S.bok[j] = ok;
+      S.bwr[j] = 1;
+      S.bst[j] = MTBLX_ST_OK;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t f = 0;
+      for (uint32_t j = 0; j < nb; ++j) {
+        S.bint0[j] = f;
+        if (S.bok[j] && f + S.bn[j] <= (uint32_t)C::MAXINT) f += S.bn[j];
+        else S.bok[j] = 0;
+      }
+      S.bint0[nb] = f;
+    }
+    __syncthreads();
+    const uint32_t nint = S.bint0[nb];
+
+    // ---- 3. walk 1: one thread per restart interval across the tile ----
+    for (uint32_t f = tid; f < nint; f += kThreads) {
+      uint32_t j = 0;
+      while (S.bint0[j + 1] <= f) ++j;
+      const uint32_t i = f - S.bint0[j], bo = S.boff[j], L = S.blen[j], R = S.bR[j], n = S.bn[j];
+      const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
+      const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
+      uint32_t cnt, kb, vb;
+      const bool ok = walk_interval<false, C>(S, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0, nullptr, nullptr, 0, 0) &&
+                      cnt <= (uint32_t)C::MAXREC;
+      S.icnt[f] = cnt;
+      S.ikb[f] = kb;
+      S.ivb[f] = vb;
+      S.iblk[f] = (uint8_t)j;
+      if (!ok) S.bok[j] = 0;
+    }
+    __syncthreads();
+
+    // ---- 4. irregular blocks: exact serial count (generic path, lane per block) ----
+    if (tid < (int)nb && !S.bok[tid]) {
+      const uint32_t j = tid, bo = S.boff[j], L = S.blen[j];
+      const uint8_t* d = (bo != kNotStaged) ? (S.stage + bo) : (a.data + a.blk_off[b0 + j]);
+      GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
+      S.bcnt[j] = o.nrec;
+      S.bkb[j] = (uint32_t)o.kb;
+      S.bvb[j] = (uint32_t)o.vb;
+      S.bst[j] = o.st;
+    }
+    // scan of interval counts (regular blocks only) -> tile-relative interval bases
+    // (MAXINT <= 256: one interval per thread)
+    {
+      uint32_t xc = 0, xk = 0, xv = 0;
+      const uint32_t f = tid;
+      if (f < nint && S.bok[S.iblk[f]]) { xc = S.icnt[f]; xk = S.ikb[f]; xv = S.ivb[f]; }
+      uint32_t tot[3];
+      wg_excl_scan3(S, xc, xk, xv, tot);
+      if (f < nint) { S.icnt[f] = xc; S.ikb[f] = xk; S.ivb[f] = xv; }
+      if (tid == 0) { S.icnt[nint] = tot[0]; S.ikb[nint] = tot[1]; S.ivb[nint] = tot[2]; }
+    }
+    __syncthreads();
+    // block totals + tile-relative block bases (serial over <= MAXBLK blocks)
+    if (tid == 0) {
+      uint32_t rr = 0, rk = 0, rv = 0, fastrec = 0;
+      for (uint32_t j = 0; j < nb; ++j) {
+        if (S.bok[j]) {
+          const uint32_t fa = S.bint0[j], fb = S.bint0[j + 1];
+          S.bcnt[j] = S.icnt[fb] - S.icnt[fa];
+          S.bkb[j] = S.ikb[fb] - S.ikb[fa];
+          S.bvb[j] = S.ivb[fb] - S.ivb[fa];
+          fastrec += S.bcnt[j];
+        }
+        S.brb[j] = rr; S.bkbb[j] = rk; S.bvbb[j] = rv;
+        rr += S.bcnt[j]; rk += S.bkb[j]; rv += S.bvb[j];
+      }
+      S.ttot[0] = rr; S.ttot[1] = rk; S.ttot[2] = rv;
+      S.nfastrec = fastrec;
+    }
+    __syncthreads();
+
+    // ---- 5. publish aggregate + decoupled look-back (wave 0) ----
+    if (wv == 0) {
+      uint64_t pre[3];
+      const uint32_t agg[3] = {S.ttot[0], S.ttot[1], S.ttot[2]};
+      tile_lookback(a.lb, t, agg, pre, a.totals);
+      if (lane == 0) {
+        S.tpre[0] = pre[0]; S.tpre[1] = pre[1]; S.tpre[2] = pre[2];
+        if (t == a.ntiles - 1) {
+          a.totals[0] = pre[0] + agg[0];
+          a.totals[1] = pre[1] + agg[1];
+          a.totals[2] = pre[2] + agg[2];
+        }
+      }
+    }
+    __syncthreads();
+    const uint64_t pr = S.tpre[0], pk = S.tpre[1], pv = S.tpre[2];
+
+    // ---- 6. per-block outputs + capacity check ----
+    if (tid < (int)nb) {
+      const uint32_t j = tid, b = b0 + j;
+      const uint64_t rb = pr + S.brb[j], kb = pk + S.bkbb[j], vb = pv + S.bvbb[j];
+      a.nrec[b] = S.bcnt[j];
+      a.rec_base[b] = rb;
+      a.key_base[b] = kb;
+      a.val_base[b] = vb;
+      int32_t st = S.bst[j];
+      if (a.write && (rb + S.bcnt[j] > a.rec_cap || kb + S.bkb[j] > a.keys_cap || vb + S.bvb[j] > a.vals_cap)) {
+        st = MTBLX_ST_OVERFLOW;
+        S.bwr[j] = 0;
+        atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 1ull);
+      }
+      a.status[b] = st;
+    }
+    if (!a.write) { __syncthreads(); continue; }
+    __syncthreads();
+
+    // ---- 7. walk 2 (metadata) + copy, in chunks of whole intervals of <= MAXREC records ----
+    // icnt[f] = regular records before interval f (irregular blocks contribute 0), so
+    // icnt is the metadata slot numbering and is monotone: chunks are found by search.
+    for (uint32_t fa = 0; fa < nint;) {
+      uint32_t fb;
+      {
+        const uint32_t lim = S.icnt[fa] + (uint32_t)C::MAXREC;
+        if (S.icnt[nint] <= lim) {
+          fb = nint;
+        } else {  // largest fb with icnt[fb] <= lim (walk 1 guarantees one interval fits)
+          uint32_t l = fa + 1, h = nint;
+          while (l < h) {
+            const uint32_t m = (l + h + 1) / 2;
+            if (S.icnt[m] <= lim) l = m; else h = m - 1;
+          }
+          fb = l;
+        }
+      }
+      const uint32_t rlo = S.icnt[fa], rhi = S.icnt[fb];
+      for (uint32_t f = fa + tid; f < fb; f += kThreads) {
+        const uint32_t j = S.iblk[f];
+        if (!S.bok[j]) continue;
+        const uint32_t fj = S.bint0[j];
+        const uint32_t i = f - fj, bo = S.boff[j], L = S.blen[j], R = S.bR[j], n = S.bn[j];
+        const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
+        const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
+        const uint32_t kin = S.ikb[f] - S.ikb[fj], vin = S.ivb[f] - S.ivb[fj];  // bytes before f in block
+        const uint32_t rin = S.icnt[f] - S.icnt[fj];                             // records before f in block
+        uint32_t* ke = S.bwr[j] ? a.key_end + pr + S.brb[j] + rin : nullptr;
+        uint32_t* ve = S.bwr[j] ? a.val_end + pr + S.brb[j] + rin : nullptr;
+        uint32_t c, k, v;
+        walk_interval<true, C>(S, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi,
+                               ke, ve, kin, vin);
+      }
+      __syncthreads();
+      // copy: one thread per record
+      for (uint32_t q = tid; q < rhi - rlo; q += kThreads) {
+        const uint32_t j = S.rblk[q];
+        if (!S.bwr[j]) continue;
+        const uint32_t bo = S.boff[j];
+        const uint32_t vl = S.rvl[q];
+        const uint32_t vsrc = bo + S.rpos[q] + S.rns[q];
+        uint8_t* vd = a.vals + pv + S.rvs[q];
+        for (uint32_t o = 0; o < vl; o += 16) {
+          uint4 wv4 = lds_win16(S.stage, vsrc + o);
+          const uint32_t m = vl - o;
+          store_bytes(vd + o, wv4, m < 16 ? m : 16);
+        }
+        const uint32_t shr = S.rsh[q];
+        const uint32_t klen = shr + S.rns[q];
+        uint8_t* kd = a.keys + pk + S.rks[q];
+        for (uint32_t j0 = 0; j0 < klen; j0 += 16) {
+          const uint32_t jend = (j0 + 16 < klen) ? j0 + 16 : klen;
+          uint4 outw = make_uint4(0, 0, 0, 0);
+          uint32_t jj = j0;
+          while (jj < jend) {
+            // source of key byte jj: the latest record s <= q with shared_s <= jj (same interval;
+            // the interval's first record has shared 0 and lies in this chunk)
+            uint32_t sidx = q, m = klen, shs = shr;
+            while (shs > jj) {
+              m = shs < m ? shs : m;
+              --sidx;
+              shs = S.rsh[sidx];
+            }
+            const uint32_t seg = m < jend ? m : jend;
+            const uint32_t src = bo + S.rpos[sidx] + (jj - shs);
+            uint4 w4 = lds_win16(S.stage, src - (jj - j0));
+            merge_bytes(outw, w4, (int)(jj - j0), (int)(seg - j0));
+            jj = seg;
+          }
+          store_bytes(kd + j0, outw, jend - j0);
+        }
+      }
+      __syncthreads();
+      fa = fb;
+    }
+
+    // ---- 8. irregular blocks: exact serial write (lane per block) ----
+    if (tid < (int)nb && !S.bok[tid] && S.bwr[tid]) {
+      const uint32_t j = tid, bo = S.boff[j], L = S.blen[j];
+      const uint8_t* d = (bo != kNotStaged) ? (S.stage + bo) : (a.data + a.blk_off[b0 + j]);
+      generic_block<true>(d, L, a.keys + pk + S.bkbb[j], a.vals + pv + S.bvbb[j], a.key_end + pr + S.brb[j],
+                          a.val_end + pr + S.brb[j]);
+    }
+    __syncthreads();
   }
 }
+
+using CfgSmall = TileCfg<32768, 512, 128, 16>;
+using CfgLarge = TileCfg<67584, 1024, 256, 4>;
 
 }  // namespace mtblx
 
@@ -618,51 +723,67 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_final(const uint32_t* nre
 // ----------------------------------------------------------------------------------
 using namespace mtblx;
 
-extern "C" size_t mtblx_impl_scan_parts(uint32_t nblk) { return (nblk + kScanTile - 1) / kScanTile; }
+namespace {
+struct Plan {
+  uint32_t bpt, slot, ntiles;
+  bool large;
+};
 
-template <int STAGE, int WPG>
-static hipError_t launch_count(const CountArgs& c, hipStream_t s) {
-  dim3 grid((c.nblk + WPG - 1) / WPG);
-  hipLaunchKernelGGL((k_count<STAGE, WPG>), grid, dim3(WPG * 64), 0, s, c);
-  return hipGetLastError();
-}
-template <int STAGE, int WPG>
-static hipError_t launch_decode(const DecodeArgs& d, hipStream_t s) {
-  dim3 grid((d.nblk + WPG - 1) / WPG);
-  hipLaunchKernelGGL((k_decode<STAGE, WPG>), grid, dim3(WPG * 64), 0, s, d);
-  return hipGetLastError();
+Plan make_plan(uint32_t nblk, uint32_t max_len) {
+  Plan p{};
+  const uint32_t slot = ((max_len + 15u + 15u) / 16u) * 16u;
+  uint32_t usable = CfgSmall::TB - 48;
+  if (max_len != 0 && slot <= usable) {
+    p.large = false;
+    p.slot = slot;
+    p.bpt = std::min<uint32_t>(usable / slot, CfgSmall::MAXBLK);
+  } else {
+    usable = CfgLarge::TB - 48;
+    p.large = true;
+    p.slot = (max_len != 0 && slot <= usable) ? slot : usable;
+    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / p.slot, CfgLarge::MAXBLK));
+  }
+  p.ntiles = (nblk + p.bpt - 1) / p.bpt;
+  return p;
 }
 
-// ws layout: kb[nblk] u64 | vb[nblk] u64 | parts[nparts] Trip
+template <class C>
+int resident_grid(uint32_t ntiles) {
+  static int cached = 0;
+  if (!cached) {
+    int dev = 0, ncu = 0, occ = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_decode_tiles<C>, kThreads, 0) != hipSuccess || occ < 1)
+      occ = 1;
+    int lds_lim = (int)((160u * 1024u) / sizeof(TileLds<C>));
+    if (lds_lim < 1) lds_lim = 1;
+    cached = std::max(1, ncu * std::min(occ, lds_lim));
+  }
+  return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
+}
+}  // namespace
+
+extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) {
+  // worst case: one block per tile
+  return (size_t)nblk * 24u + 64u;
+}
+
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
                               hipStream_t s) {
   const uint32_t nblk = in->nblk;
-  uint64_t* kb = reinterpret_cast<uint64_t*>(ws);
-  uint64_t* vb = kb + nblk;
-  Trip* parts = reinterpret_cast<Trip*>(vb + nblk);
-  const uint32_t nparts = (uint32_t)mtblx_impl_scan_parts(nblk);
-  const uint32_t mx = in->max_blk_len ? in->max_blk_len : 0xFFFFFFFFu;
-
-  CountArgs c{in->data, in->data_len, in->blk_off, in->blk_len, nblk, out->nrec, kb, vb, out->status};
-  hipError_t e = hipSuccess;
-  if (write == 2) goto decode;  // counts + bases already in out/ws (mtblx_decode_counted)
-  if (mx <= 4096) e = launch_count<4096, 4>(c, s);
-  else e = launch_count<8192, 2>(c, s);
-  if (e != hipSuccess) return MTBLX_E_HIP;
-
-  hipLaunchKernelGGL(k_scan_partial, dim3(nparts), dim3(kScanThreads), 0, s, (const uint32_t*)out->nrec,
-                     (const uint64_t*)kb, (const uint64_t*)vb, nblk, parts);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, s, parts, nparts, out->totals);
-  hipLaunchKernelGGL(k_scan_final, dim3(nparts), dim3(kScanThreads), 0, s, (const uint32_t*)out->nrec,
-                     (const uint64_t*)kb, (const uint64_t*)vb, nblk, (const Trip*)parts, out->rec_base, out->key_base,
-                     out->val_base);
-  if (hipGetLastError() != hipSuccess) return MTBLX_E_HIP;
-  if (!write) return MTBLX_OK;
-decode:
-  DecodeArgs d{in->data,      in->data_len,   in->blk_off, in->blk_len,  nblk,          out->nrec,     kb,
-               vb,            out->rec_base,  out->key_base, out->val_base, out->status, out->key_end, out->val_end,
-               out->rec_cap,  out->keys,      out->keys_cap, out->vals,    out->vals_cap, out->totals};
-  if (mx <= 4096) e = launch_decode<4096, 4>(d, s);
-  else e = launch_decode<8192, 2>(d, s);
-  return e == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+  const Plan p = make_plan(nblk, in->max_blk_len);
+  uint64_t* lb = reinterpret_cast<uint64_t*>(ws);
+  if (hipMemsetAsync(lb, 0, (size_t)p.ntiles * 24u, s) != hipSuccess) return MTBLX_E_HIP;
+  if (hipMemsetAsync(out->totals, 0, 32, s) != hipSuccess) return MTBLX_E_HIP;
+  TileArgs a{in->data,     in->data_len,  in->blk_off,  in->blk_len,   nblk,         p.bpt,         p.slot,
+             p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
+             out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
+             lb,           write ? 1 : 0};
+  if (p.large) {
+    hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_decode_tiles<CfgSmall>, dim3(resident_grid<CfgSmall>(p.ntiles)), dim3(kThreads), 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -8,7 +8,7 @@
 
 #include "mtblx.h"
 
-extern "C" size_t mtblx_impl_scan_parts(uint32_t nblk);
+extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk);
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
                               hipStream_t s);
 
@@ -23,7 +23,7 @@ extern "C" int mtblx_device_ok(void) {
 }
 
 extern "C" size_t mtblx_decode_workspace_bytes(uint32_t nblk) {
-  return (size_t)nblk * 16u + mtblx_impl_scan_parts(nblk) * 24u + 256u;
+  return mtblx_impl_ws_bytes(nblk) + 256u;
 }
 
 static int check_common(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb) {
@@ -51,7 +51,8 @@ extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_dec
   if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
       (!out->val_end && out->rec_cap))
     return MTBLX_E_INVAL;
-  return mtblx_impl_run(in, out, ws, 2, reinterpret_cast<hipStream_t>(stream));
+  // single-pass kernel: counting is fused into the decode, so this is a full decode
+  return mtblx_impl_run(in, out, ws, 1, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,

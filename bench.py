@@ -79,10 +79,14 @@ def main():
     ap.add_argument("--blocks", type=int, default=100_000)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic: load libmtblx_stamps.so and report per-phase cycles per tile (not a measurement)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_decode_tiles.json"),
                     help="PMC-derived HBM bytes per k_decode_tiles launch (profiles/, from a rocprofv3 --pmc run)")
     args = ap.parse_args()
 
+    if args.stamps:
+        os.environ["MTBLX_LIB"] = os.path.join(ROOT, "oxidized-mtbl_amd", "mtblx", "libmtblx_stamps.so")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -183,6 +187,12 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_decode_tiles", "alg_bytes_per_launch": int(alg_bytes)},
     }
+    if args.stamps:
+        d = ws.buf[:72].cpu().numpy().view(np.uint64).astype(np.float64)
+        names = ["stage", "trailers+walk1", "generic+scan", "lookback", "block-out", "walk2", "copy", "loop/generic-w"]
+        ntl = max(d[8], 1)
+        res["phase_cycles_per_tile"] = {n: round(d[k] / ntl, 1) for k, n in enumerate(names)}
+        res["stamps_note"] = "diagnostic build (s_memtime, thread 0 of each workgroup), last step only; shares, not time"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(data, off, ln, args.cpu_seconds)
     if rank == 0:

@@ -268,6 +268,8 @@ struct alignas(16) TileLds {
   uint32_t ttot[3];           // tile totals
   uint32_t nfastrec;
   uint32_t wsum[4][3];        // per-wave scan totals
+  uint32_t lbfirst[4][3];     // look-back: first P lane per wave
+  uint64_t lbsum[4][3];       // look-back: per-wave partial sums
 };
 
 // Stage one block into a 16-byte aligned slot; returns the offset of block byte 0 within
@@ -425,61 +427,79 @@ struct TileArgs {
   uint64_t vals_cap;
   uint64_t* totals;
   uint64_t* lb;     // [ntiles * 3] look-back words, zeroed before launch
+  uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
   int write;
 };
 
-// Decoupled look-back (wave 0): publish the tile aggregate, walk predecessors back in
-// windows of 64 until every quantity meets an inclusive prefix; publish our own.
-// Look-back words are single 8-byte agent-scope atomics: the value IS the flag, so no
-// fence is needed (MI355X_MICROARCH.md, hand-off granules).  Spins are bounded: on
-// timeout bit1 of totals[3] is set instead of hanging.
-__device__ void tile_lookback(uint64_t* lb, uint32_t t, const uint32_t agg[3], uint64_t pre[3], uint64_t* totals) {
-  const int lane = threadIdx.x & 63;
+// Decoupled look-back over a workgroup-wide window: publish the tile aggregate (flag A),
+// then read predecessors back in windows of 256 tiles (one per thread) until every
+// quantity meets an inclusive prefix (flag P); publish our own P.  A 256-wide window
+// lets the inclusive-prefix front advance 256 tiles per round trip, so the tiles of a
+// persistent round do not serialise on each other.  Look-back words are single 8-byte
+// agent-scope atomics: the value IS the flag, no fence needed (MI355X_MICROARCH.md,
+// hand-off granules).  Spins are bounded: on timeout bit1 of totals[3] is set.
+template <class C>
+__device__ void tile_lookback(TileLds<C>& S, uint64_t* lb, uint32_t t, uint64_t* totals) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t agg[3] = {S.ttot[0], S.ttot[1], S.ttot[2]};
   if (t == 0) {
-    if (lane < 3) __hip_atomic_store(&lb[lane], kFlagP | agg[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pre[0] = pre[1] = pre[2] = 0;
+    if (tid < 3) __hip_atomic_store(&lb[tid], kFlagP | agg[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) { S.tpre[0] = S.tpre[1] = S.tpre[2] = 0; }
     return;
   }
-  if (lane < 3)
-    __hip_atomic_store(&lb[3ull * t + lane], kFlagA | agg[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 3)
+    __hip_atomic_store(&lb[3ull * t + tid], kFlagA | agg[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t acc[3] = {0, 0, 0};
   bool done[3] = {false, false, false};
   int64_t base = (int64_t)t - 1;
   bool timeout = false;
   while (!(done[0] && done[1] && done[2])) {
-    const int64_t p = base - lane;
+    const int64_t p = base - tid;
+    uint64_t w[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
+      w[q] = kFlagP;  // before tile 0: inclusive prefix 0
       if (done[q]) continue;
-      uint64_t w = kFlagP;  // before tile 0: inclusive prefix 0
       if (p >= 0) {
         uint32_t spins = 0;
         for (;;) {
-          w = __hip_atomic_load(&lb[3ull * p + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (w >> 62) break;
+          w[q] = __hip_atomic_load(&lb[3ull * p + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (w[q] >> 62) break;
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 24)) { timeout = true; w = kFlagP; break; }
+          if (++spins > (1u << 22)) { timeout = true; w[q] = kFlagP; break; }
         }
       }
-      const uint64_t pm = __ballot((w >> 62) == 2u);
-      uint64_t v = w & kValMask;
-      if (pm) {
-        const int first = __builtin_ctzll(pm);
-        if (lane > first) v = 0;
-        done[q] = true;
-      }
-      acc[q] += wave_sum64(v);
+      const uint64_t pm = __ballot((w[q] >> 62) == 2u);
+      if (lane == 0) S.lbfirst[wv][q] = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
     }
-    base -= kWave;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (done[q]) continue;
+      uint32_t gfirst = kThreads;
+      for (int k = 0; k < kThreads / kWave; ++k)
+        if (S.lbfirst[k][q] < 64u) { gfirst = k * kWave + S.lbfirst[k][q]; break; }
+      uint64_t v = w[q] & kValMask;
+      if ((uint32_t)tid > gfirst) v = 0;
+      const uint64_t ws = wave_sum64(v);
+      if (lane == 0) S.lbsum[wv][q] = ws;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (done[q]) continue;
+      for (int k = 0; k < kThreads / kWave; ++k) acc[q] += S.lbsum[k][q];
+      for (int k = 0; k < kThreads / kWave; ++k)
+        if (S.lbfirst[k][q] < 64u) done[q] = true;
+    }
+    __syncthreads();
+    base -= kThreads;
   }
-  if (lane < 3) {
-    uint64_t incl = acc[lane] + agg[lane];
-    __hip_atomic_store(&lb[3ull * t + lane], kFlagP | incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (timeout && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(totals + 3), 2ull);
-  pre[0] = acc[0];
-  pre[1] = acc[1];
-  pre[2] = acc[2];
+  if (tid < 3)
+    __hip_atomic_store(&lb[3ull * t + tid], kFlagP | (acc[tid] + agg[tid]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(totals + 3), 2ull);
+  if (tid == 0) { S.tpre[0] = acc[0]; S.tpre[1] = acc[1]; S.tpre[2] = acc[2]; }
 }
 
 template <class C>
@@ -487,10 +507,21 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
   __shared__ TileLds<C> S;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uintptr_t lo = reinterpret_cast<uintptr_t>(a.data), hi = lo + a.data_len;
+#ifdef MTBLX_STAMPS
+  // diagnostic build only: per-phase cycles of thread 0 (s_memtime), summed over tiles
+  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime(), ntl = 0;
+#define STAMP(k) do { if (tid == 0) { const uint64_t _t = __builtin_amdgcn_s_memtime(); tacc[k] += _t - tprev; tprev = _t; } } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
 
   for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
     const uint32_t b0 = t * a.bpt;
     const uint32_t nb = min(a.bpt, a.nblk - b0);
+#ifdef MTBLX_STAMPS
+    ++ntl;
+#endif
+    STAMP(7);
 
     // ---- 1. stage: wave w stages blocks w, w+4, ... ----
     for (uint32_t j = wv; j < nb; j += kThreads / kWave) {
@@ -502,6 +533,7 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
       if (lane == 0) { S.boff[j] = bo; S.blen[j] = L; }
     }
     __syncthreads();
+    STAMP(0);
 
     // ---- 2. trailers (Block::init, src/block.rs:16-49) ----
     if (tid < (int)nb) {
@@ -548,6 +580,7 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
     }
     __syncthreads();
 
+    STAMP(1);
     // ---- 4. irregular blocks: exact serial count (generic path, lane per block) ----
     if (tid < (int)nb && !S.bok[tid]) {
       const uint32_t j = tid, bo = S.boff[j], L = S.blen[j];
@@ -589,21 +622,16 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
     }
     __syncthreads();
 
-    // ---- 5. publish aggregate + decoupled look-back (wave 0) ----
-    if (wv == 0) {
-      uint64_t pre[3];
-      const uint32_t agg[3] = {S.ttot[0], S.ttot[1], S.ttot[2]};
-      tile_lookback(a.lb, t, agg, pre, a.totals);
-      if (lane == 0) {
-        S.tpre[0] = pre[0]; S.tpre[1] = pre[1]; S.tpre[2] = pre[2];
-        if (t == a.ntiles - 1) {
-          a.totals[0] = pre[0] + agg[0];
-          a.totals[1] = pre[1] + agg[1];
-          a.totals[2] = pre[2] + agg[2];
-        }
-      }
-    }
+    // ---- 5. publish aggregate + decoupled look-back (whole workgroup) ----
+    STAMP(2);
+    tile_lookback<C>(S, a.lb, t, a.totals);
     __syncthreads();
+    if (tid == 0 && t == a.ntiles - 1) {
+      a.totals[0] = S.tpre[0] + S.ttot[0];
+      a.totals[1] = S.tpre[1] + S.ttot[1];
+      a.totals[2] = S.tpre[2] + S.ttot[2];
+    }
+    STAMP(3);
     const uint64_t pr = S.tpre[0], pk = S.tpre[1], pv = S.tpre[2];
 
     // ---- 6. per-block outputs + capacity check ----
@@ -625,6 +653,7 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
     if (!a.write) { __syncthreads(); continue; }
     __syncthreads();
 
+    STAMP(4);
     // ---- 7. walk 2 (metadata) + copy, in chunks of whole intervals of <= MAXREC records ----
     // icnt[f] = regular records before interval f (irregular blocks contribute 0), so
     // icnt is the metadata slot numbering and is monotone: chunks are found by search.
@@ -660,6 +689,7 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
                                ke, ve, kin, vin);
       }
       __syncthreads();
+      STAMP(5);
       // copy: one thread per record
       for (uint32_t q = tid; q < rhi - rlo; q += kThreads) {
         const uint32_t j = S.rblk[q];
@@ -699,6 +729,7 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
         }
       }
       __syncthreads();
+      STAMP(6);
       fa = fb;
     }
 
@@ -711,6 +742,12 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
     }
     __syncthreads();
   }
+#ifdef MTBLX_STAMPS
+  if (tid == 0 && a.dbg) {
+    for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)tacc[k]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 8), (unsigned long long)ntl);
+  }
+#endif
 }
 
 using CfgSmall = TileCfg<32768, 512, 128, 16>;
@@ -764,22 +801,21 @@ int resident_grid(uint32_t ntiles) {
 }
 }  // namespace
 
-extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) {
-  // worst case: one block per tile
-  return (size_t)nblk * 24u + 64u;
-}
+// workspace: [0, 256) diagnostic stamps | look-back words (worst case one block per tile)
+extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
 
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
                               hipStream_t s) {
   const uint32_t nblk = in->nblk;
   const Plan p = make_plan(nblk, in->max_blk_len);
-  uint64_t* lb = reinterpret_cast<uint64_t*>(ws);
-  if (hipMemsetAsync(lb, 0, (size_t)p.ntiles * 24u, s) != hipSuccess) return MTBLX_E_HIP;
+  uint64_t* dbg = reinterpret_cast<uint64_t*>(ws);
+  uint64_t* lb = dbg + 32;
+  if (hipMemsetAsync(ws, 0, 256u + (size_t)p.ntiles * 24u, s) != hipSuccess) return MTBLX_E_HIP;
   if (hipMemsetAsync(out->totals, 0, 32, s) != hipSuccess) return MTBLX_E_HIP;
   TileArgs a{in->data,     in->data_len,  in->blk_off,  in->blk_len,   nblk,         p.bpt,         p.slot,
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
-             lb,           write ? 1 : 0};
+             lb,           dbg,           write ? 1 : 0};
   if (p.large) {
     hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
   } else {

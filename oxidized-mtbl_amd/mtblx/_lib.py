@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmtblx.so")
+# MTBLX_LIB selects the diagnostic stamps build (bench.py --stamps); default is the product build
+LIB_PATH = os.environ.get("MTBLX_LIB") or os.path.join(_HERE, "libmtblx.so")
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)

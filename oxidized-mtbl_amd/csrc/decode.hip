@@ -216,128 +216,158 @@ __device__ GenOut generic_block(const uint8_t* d, uint64_t L, uint8_t* keys, uin
 // ----------------------------------------------------------------------------------
 // A tile = up to `bpt` consecutive blocks of the batch, staged together in the LDS of
 // one workgroup (256 threads).  Workgroups are persistent and take tiles t = blockIdx.x,
-// + gridDim.x, ... (static round-robin; the grid never exceeds the resident capacity).
+// + G, + 2G ... (G = gridDim.x, never more than the resident capacity).
 // Per tile:
-//   stage -> parse trailers -> walk (one thread per restart interval, across all blocks
-//   of the tile) -> tile-local scans -> publish the tile aggregate -> decoupled
-//   look-back for the tile's global (record, key byte, value byte) prefix -> per-block
-//   outputs -> second walk writes per-record metadata -> every thread copies records.
-// Blocks that are not "regular" (see walk_interval) run the exact serial emulation.
+//   stage (from registers prefetched during the previous tile) -> prefetch the next tile
+//   -> trailers -> walk 1 (one thread per restart interval across the tile, counts)
+//   -> interval scan -> publish the tile aggregate -> issue the look-back loads
+//   -> walk 2 (per-record metadata into LDS, hides the look-back latency)
+//   -> finish the look-back -> per-block outputs -> copy (one thread per record)
+//   -> irregular blocks (exact serial emulation).
+//
+// Look-back ("rolling"): prefix(t) = incl(t - G) + sum of the aggregates of tiles
+// t-G+1 .. t-1.  incl(t - G) is this workgroup's own previous tile, so only the
+// aggregates of the other G-1 tiles of the trailing window are read: one packed 8-byte
+// agent-scope atomic per tile (the value IS the flag; no fences), <= 4 loads per thread,
+// issued before walk 2 and consumed after it.
 
 constexpr uint32_t kNotStaged = 0xFFFFFFFFu;
-constexpr uint64_t kFlagA = 1ull << 62;   // look-back word holds the tile aggregate
-constexpr uint64_t kFlagP = 2ull << 62;   // look-back word holds the inclusive prefix
-constexpr uint64_t kValMask = (1ull << 62) - 1;
 constexpr int kThreads = 256;
+constexpr int kMaxLookbackLoads = 4;               // G - 1 <= 4 * 256
+constexpr uint64_t kReady = 1ull << 63;
+constexpr uint32_t kField = (1u << 21) - 1;        // 21-bit fields: nrec | vbytes | kbytes
+constexpr int kPrefetch = 8;                       // uint4 per thread prefetched (32 KiB tiles)
 
-template <int TB_, int MAXREC_, int MAXINT_, int MAXBLK_>
+template <int TB_, int MAXREC_, int MAXINT_, int MAXBLK_, bool PREFETCH_, int MINW_>
 struct TileCfg {
+  static constexpr int MINW = MINW_;     // workgroups per CU to keep resident (__launch_bounds__)
   static constexpr int TB = TB_;          // staging bytes
-  static constexpr int MAXREC = MAXREC_;  // records with metadata per tile
-  static constexpr int MAXINT = MAXINT_;  // restart intervals per tile
-  static constexpr int MAXBLK = MAXBLK_;  // blocks per tile
+  static constexpr int MAXREC = MAXREC_;  // records with metadata per chunk
+  static constexpr int MAXINT = MAXINT_;  // restart intervals per tile (<= kThreads)
+  static constexpr int MAXBLK = MAXBLK_;  // blocks per tile (<= 64)
+  static constexpr bool PREFETCH = PREFETCH_;
+};
+
+// per-record metadata, 16 bytes: one ds_write_b128 / ds_read_b128
+struct Rec {
+  uint32_t pos_sh;   // pos (block offset of the key suffix) | shared << 16
+  uint32_t ns_vl;    // non_shared | value_length << 16
+  uint32_t ks;       // tile-relative key start
+  uint32_t vs_blk;   // tile-relative value start (< 2^24: bounded by the staging bytes) | block << 24
 };
 
 template <class C>
 struct alignas(16) TileLds {
   uint8_t stage[C::TB];
+  Rec rec[C::MAXREC];
   // per block of the tile
   uint32_t boff[C::MAXBLK];   // stage offset of block byte 0 (kNotStaged if not staged)
   uint32_t blen[C::MAXBLK];
   uint32_t bR[C::MAXBLK];     // restart offset
-  uint32_t bn[C::MAXBLK];     // restart count
+  uint32_t bn[C::MAXBLK];     // restart count (0 = irregular)
   uint32_t bint0[C::MAXBLK + 1];
   uint32_t bok[C::MAXBLK];    // 1 = regular fast path
   uint32_t bwr[C::MAXBLK];    // 1 = outputs of this block are written
   int32_t bst[C::MAXBLK];
   uint32_t bcnt[C::MAXBLK], bkb[C::MAXBLK], bvb[C::MAXBLK];   // block totals
   uint32_t brb[C::MAXBLK], bkbb[C::MAXBLK], bvbb[C::MAXBLK];  // tile-relative block bases
-  // per restart interval: counts after walk 1, exclusive tile-relative bases after the scan
+  uint32_t brf[C::MAXBLK];    // first metadata slot (regular records before the block)
+  // per restart interval: counts after walk 1, exclusive bases after the scan
   uint32_t icnt[C::MAXINT + 1], ikb[C::MAXINT + 1], ivb[C::MAXINT + 1];
   uint8_t iblk[C::MAXINT];
-  // per record (fast blocks), tile-relative index
-  uint16_t rpos[C::MAXREC];   // block offset of the key suffix
-  uint16_t rsh[C::MAXREC];
-  uint16_t rns[C::MAXREC];
-  uint16_t rvl[C::MAXREC];
-  uint32_t rks[C::MAXREC];    // tile-relative key start
-  uint32_t rvs[C::MAXREC];    // tile-relative value start
-  uint8_t rblk[C::MAXREC];
   // tile scalars
   uint64_t tpre[3];           // global exclusive prefix of the tile (records, key bytes, value bytes)
-  uint32_t ttot[3];           // tile totals
+  uint64_t tinc[3];           // inclusive prefix of this workgroup's previous tile
+  uint32_t ttot[3];
   uint32_t nfastrec;
-  uint32_t wsum[4][3];        // per-wave scan totals
-  uint32_t lbfirst[4][3];     // look-back: first P lane per wave
-  uint64_t lbsum[4][3];       // look-back: per-wave partial sums
+  uint32_t contig;            // 1 = tile staged as one contiguous byte range
+  uint32_t wsum[4][3];
+  uint64_t lbsum[4][3];
 };
 
-// Stage one block into a 16-byte aligned slot; returns the offset of block byte 0 within
-// the slot (the block's global misalignment).  Reads stay inside [lo, hi).
-__device__ __forceinline__ uint32_t stage_slot(uint8_t* slot, const uint8_t* gptr, uint32_t L, uintptr_t lo,
-                                               uintptr_t hi, int lane) {
-  uintptr_t ga = reinterpret_cast<uintptr_t>(gptr);
-  uintptr_t a0 = ga & ~uintptr_t(15);
-  uint32_t delta = (uint32_t)(ga - a0);
-  uint32_t nch = (delta + L + 15u) >> 4;
-  uint32_t c = lane;
-  // main body: 4 independent 16-byte loads in flight per lane
-  for (; c + 3 * kWave < nch; c += 4 * kWave) {
-    uintptr_t a = a0 + 16u * c;
-    if (a >= lo && a + 16 * (3 * kWave) + 16 <= hi) {
-      uint4 v0 = *reinterpret_cast<const uint4*>(a);
-      uint4 v1 = *reinterpret_cast<const uint4*>(a + 16 * kWave);
-      uint4 v2 = *reinterpret_cast<const uint4*>(a + 32 * kWave);
-      uint4 v3 = *reinterpret_cast<const uint4*>(a + 48 * kWave);
-      *reinterpret_cast<uint4*>(slot + 16 * c) = v0;
-      *reinterpret_cast<uint4*>(slot + 16 * (c + kWave)) = v1;
-      *reinterpret_cast<uint4*>(slot + 16 * (c + 2 * kWave)) = v2;
-      *reinterpret_cast<uint4*>(slot + 16 * (c + 3 * kWave)) = v3;
-    } else {
-      break;
-    }
-  }
-  for (; c < nch; c += kWave) {
-    uintptr_t a = a0 + 16u * c;
-    uint4 v;
-    if (a >= lo && a + 16 <= hi) {
-      v = *reinterpret_cast<const uint4*>(a);
-    } else {
-      uint32_t t[4] = {0, 0, 0, 0};
-      for (int i = 0; i < 16; ++i)
-        if (a + i >= lo && a + i < hi) t[i >> 2] |= (uint32_t)(*reinterpret_cast<const uint8_t*>(a + i)) << (8 * (i & 3));
-      v = make_uint4(t[0], t[1], t[2], t[3]);
-    }
-    *reinterpret_cast<uint4*>(slot + 16 * c) = v;
-  }
+struct TileArgs {
+  const uint8_t* data;
+  uint64_t data_len;
+  const uint64_t* blk_off;
+  const uint32_t* blk_len;
+  uint32_t nblk;
+  uint32_t bpt;     // blocks per tile
+  uint32_t slot;    // per-block staging slot bytes (fallback layout)
+  uint32_t ntiles;
+  uint32_t* nrec;
+  uint64_t* rec_base;
+  uint64_t* key_base;
+  uint64_t* val_base;
+  int32_t* status;
+  uint32_t* key_end;
+  uint32_t* val_end;
+  uint64_t rec_cap;
+  uint8_t* keys;
+  uint64_t keys_cap;
+  uint8_t* vals;
+  uint64_t vals_cap;
+  uint64_t* totals;
+  uint64_t* lb;     // [ntiles] packed tile aggregates, zeroed before launch
+  uint64_t* lbx;    // [ntiles] exact key bytes when the packed field saturates
+  uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
+  int write;
+};
+
+
+// Contiguous range of tile t: [r0, r1) of the data buffer (r0 16-aligned), or r1 = 0 if the
+// tile's blocks do not sit in one range that fits the staging buffer.
+__device__ __forceinline__ void tile_range(const TileArgs& a, uint32_t t, uint32_t tb, uint64_t& r0, uint64_t& r1) {
+  const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
+  const uint64_t s = a.blk_off[b0];
+  const uint64_t e = a.blk_off[b0 + nb - 1] + a.blk_len[b0 + nb - 1];
+  const uint64_t base = reinterpret_cast<uintptr_t>(a.data);
+  r0 = ((base + s) & ~15ull) - base;   // may be "negative" (wraps) if data is unaligned: clamp
+  if (base + s < 16 || ((base + s) & ~15ull) < base) r0 = 0;
+  r1 = (e > s && e - r0 + 48 <= tb) ? e : 0;
+}
+
+// prefetch chunk c (16 B) of a contiguous range into v (zero-filled outside the buffer)
+__device__ __forceinline__ uint4 load_chunk(const TileArgs& a, uint64_t off) {
+  if (off + 16 <= a.data_len) return *reinterpret_cast<const uint4*>(a.data + off);
+  uint32_t t[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 16; ++i)
+    if (off + i < a.data_len) t[i >> 2] |= (uint32_t)a.data[off + i] << (8 * (i & 3));
+  return make_uint4(t[0], t[1], t[2], t[3]);
+}
+
+// Stage one block into a 16-byte aligned slot (fallback layout); returns the offset of
+// block byte 0 within the slot.
+__device__ __forceinline__ uint32_t stage_slot(const TileArgs& a, uint8_t* slot, uint64_t off, uint32_t L, int lane) {
+  const uint64_t base = reinterpret_cast<uintptr_t>(a.data);
+  const uint64_t a0 = ((base + off) & ~15ull) - base;
+  const uint32_t delta = (uint32_t)(off - a0);
+  const uint32_t nch = (delta + L + 15u) >> 4;
+  for (uint32_t c = lane; c < nch; c += kWave) *reinterpret_cast<uint4*>(slot + 16 * c) = load_chunk(a, a0 + 16ull * c);
   return delta;
 }
 
-// One restart interval [s, e) of a staged block (block byte 0 at stage offset bo).
-// Regular-path preconditions (DESIGN.md "fast path"): every entry decodes without a
-// reference panic; varints are terminated; the interval's first entry has shared == 0;
-// later entries have shared <= previous key length (so Vec capacity never matters);
-// field values fit 16 bits; the walk lands exactly on e.  Under these the reference's
-// linear chain (src/block.rs:119-143) visits exactly these entries and rebuilds exactly
-// these keys.  Returns false if they do not hold.
+// Tight walk of restart interval [s, e) of a staged block (byte 0 at stage offset bo).
+// Regular-path preconditions (DESIGN.md "regular blocks"): every entry decodes without a
+// reference panic; varints are terminated; the first entry has shared == 0 and later
+// ones shared <= previous key length (so Vec capacity never matters); fields fit 16
+// bits; the walk lands exactly on e.  Under these the reference's linear chain
+// (src/block.rs:119-143) visits exactly these entries and rebuilds exactly these keys.
 template <bool WRITE, class C>
 __device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32_t L, uint32_t R, uint32_t s,
-                                              uint32_t e, uint32_t& cnt, uint32_t& kb, uint32_t& vb, uint32_t rbase,
+                                              uint32_t e, uint32_t& cnt, uint32_t& kb, uint32_t& vb, uint32_t slot0,
                                               uint32_t kbase, uint32_t vbase, uint32_t blk, uint32_t rlo,
-                                              uint32_t rhi, uint32_t* key_end, uint32_t* val_end,
-                                              uint32_t kend0, uint32_t vend0) {
+                                              uint32_t rhi) {
   cnt = kb = vb = 0;
   if (!(s < e && e <= R)) return false;
   uint32_t p = s, prevlen = 0;
-  bool first = true;
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(S.stage);
   while (p < e) {
-    if (R - p < 3u) return false;                         // decode_entry Err -> panic
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(S.stage + ((bo + p) & ~3u));
-    uint32_t sft = ((bo + p) & 3u) * 8u;
-    uint32_t hw = __builtin_amdgcn_alignbit(w[1], w[0], sft);
+    const uint32_t ad = bo + p;
+    uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
     uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu, h = 3;
-    if ((hw & 0x808080u) != 0u) {                         // slow header path
-      uint4 W = lds_win16(S.stage, bo + p);
+    if (__builtin_expect((hw & 0x808080u) != 0u, 0)) {  // multi-byte varint header (slow path)
+      if (R - p < 3u) return false;
+      uint4 W = lds_win16(S.stage, ad);
       uint32_t l0 = dec32(W, 0, L - p, sh);
       if (l0 == 0) return false;
       uint32_t l1 = dec32(W, l0, L - p - l0, ns);
@@ -348,35 +378,28 @@ __device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32
       if (p + h > R) return false;                        // assert!(p <= limit)
       if ((sh | ns | vl) > 0xFFFFu) return false;
     }
-    if (ns + vl > R - p - h) return false;                // no overflow: both < 2^16
-    if (first ? (sh != 0) : (sh > prevlen)) return false;
+    // R - p >= h + ns + vl covers decode_entry's `limit - p >= 3` and the slice assert
+    if (R - p < h + ns + vl) return false;
+    if (sh > prevlen) return false;                       // first entry: prevlen = 0 -> shared == 0
     const uint32_t klen = sh + ns;
-    if (klen > 0xFFFFu) return false;
     if (WRITE) {
-      const uint32_t r = rbase + cnt;
+      const uint32_t r = slot0 + cnt;
       if (r >= rlo && r < rhi) {
-        const uint32_t q = r - rlo;
-        S.rpos[q] = (uint16_t)(p + h);
-        S.rsh[q] = (uint16_t)sh;
-        S.rns[q] = (uint16_t)ns;
-        S.rvl[q] = (uint16_t)vl;
-        S.rks[q] = kbase + kb;
-        S.rvs[q] = vbase + vb;
-        S.rblk[q] = (uint8_t)blk;
-      }
-      if (key_end) {
-        key_end[cnt] = kend0 + kb + klen;
-        val_end[cnt] = vend0 + vb + vl;
+        Rec x;
+        x.pos_sh = (p + h) | (sh << 16);
+        x.ns_vl = ns | (vl << 16);
+        x.ks = kbase + kb;
+        x.vs_blk = (vbase + vb) | (blk << 24);
+        S.rec[r - rlo] = x;
       }
     }
     cnt += 1;
     kb += klen;
     vb += vl;
     prevlen = klen;
-    first = false;
     p += h + ns + vl;
   }
-  return p == e;
+  return p == e && (prevlen <= 0xFFFFu);
 }
 
 // exclusive scan of 3 u32 per thread over the workgroup; returns the workgroup totals
@@ -404,109 +427,15 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
-struct TileArgs {
-  const uint8_t* data;
-  uint64_t data_len;
-  const uint64_t* blk_off;
-  const uint32_t* blk_len;
-  uint32_t nblk;
-  uint32_t bpt;     // blocks per tile
-  uint32_t slot;    // staging slot bytes per block (multiple of 16)
-  uint32_t ntiles;
-  uint32_t* nrec;
-  uint64_t* rec_base;
-  uint64_t* key_base;
-  uint64_t* val_base;
-  int32_t* status;
-  uint32_t* key_end;
-  uint32_t* val_end;
-  uint64_t rec_cap;
-  uint8_t* keys;
-  uint64_t keys_cap;
-  uint8_t* vals;
-  uint64_t vals_cap;
-  uint64_t* totals;
-  uint64_t* lb;     // [ntiles * 3] look-back words, zeroed before launch
-  uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
-  int write;
-};
-
-// Decoupled look-back over a workgroup-wide window: publish the tile aggregate (flag A),
-// then read predecessors back in windows of 256 tiles (one per thread) until every
-// quantity meets an inclusive prefix (flag P); publish our own P.  A 256-wide window
-// lets the inclusive-prefix front advance 256 tiles per round trip, so the tiles of a
-// persistent round do not serialise on each other.  Look-back words are single 8-byte
-// agent-scope atomics: the value IS the flag, no fence needed (MI355X_MICROARCH.md,
-// hand-off granules).  Spins are bounded: on timeout bit1 of totals[3] is set.
-template <class C>
-__device__ void tile_lookback(TileLds<C>& S, uint64_t* lb, uint32_t t, uint64_t* totals) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint64_t agg[3] = {S.ttot[0], S.ttot[1], S.ttot[2]};
-  if (t == 0) {
-    if (tid < 3) __hip_atomic_store(&lb[tid], kFlagP | agg[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0) { S.tpre[0] = S.tpre[1] = S.tpre[2] = 0; }
-    return;
-  }
-  if (tid < 3)
-    __hip_atomic_store(&lb[3ull * t + tid], kFlagA | agg[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t acc[3] = {0, 0, 0};
-  bool done[3] = {false, false, false};
-  int64_t base = (int64_t)t - 1;
-  bool timeout = false;
-  while (!(done[0] && done[1] && done[2])) {
-    const int64_t p = base - tid;
-    uint64_t w[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      w[q] = kFlagP;  // before tile 0: inclusive prefix 0
-      if (done[q]) continue;
-      if (p >= 0) {
-        uint32_t spins = 0;
-        for (;;) {
-          w[q] = __hip_atomic_load(&lb[3ull * p + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (w[q] >> 62) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 22)) { timeout = true; w[q] = kFlagP; break; }
-        }
-      }
-      const uint64_t pm = __ballot((w[q] >> 62) == 2u);
-      if (lane == 0) S.lbfirst[wv][q] = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      if (done[q]) continue;
-      uint32_t gfirst = kThreads;
-      for (int k = 0; k < kThreads / kWave; ++k)
-        if (S.lbfirst[k][q] < 64u) { gfirst = k * kWave + S.lbfirst[k][q]; break; }
-      uint64_t v = w[q] & kValMask;
-      if ((uint32_t)tid > gfirst) v = 0;
-      const uint64_t ws = wave_sum64(v);
-      if (lane == 0) S.lbsum[wv][q] = ws;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      if (done[q]) continue;
-      for (int k = 0; k < kThreads / kWave; ++k) acc[q] += S.lbsum[k][q];
-      for (int k = 0; k < kThreads / kWave; ++k)
-        if (S.lbfirst[k][q] < 64u) done[q] = true;
-    }
-    __syncthreads();
-    base -= kThreads;
-  }
-  if (tid < 3)
-    __hip_atomic_store(&lb[3ull * t + tid], kFlagP | (acc[tid] + agg[tid]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(totals + 3), 2ull);
-  if (tid == 0) { S.tpre[0] = acc[0]; S.tpre[1] = acc[1]; S.tpre[2] = acc[2]; }
+__device__ __forceinline__ uint64_t pack_agg(uint32_t r, uint32_t k, uint32_t v) {
+  return kReady | ((uint64_t)r << 42) | ((uint64_t)v << 21) | (uint64_t)(k < kField ? k : kField);
 }
 
 template <class C>
-__global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
+__global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) {
   __shared__ TileLds<C> S;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uintptr_t lo = reinterpret_cast<uintptr_t>(a.data), hi = lo + a.data_len;
+  const uint32_t G = gridDim.x;
 #ifdef MTBLX_STAMPS
   // diagnostic build only: per-phase cycles of thread 0 (s_memtime), summed over tiles
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime(), ntl = 0;
@@ -514,8 +443,23 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
 #else
 #define STAMP(k) do { } while (0)
 #endif
+  if (tid == 0) { S.tinc[0] = S.tinc[1] = S.tinc[2] = 0; }
 
-  for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+  // prefetch registers for the next tile's contiguous range
+  uint4 pf[kPrefetch];
+  uint64_t pr0 = 0, pr1 = 0;
+  if (C::PREFETCH && blockIdx.x < a.ntiles) {
+    tile_range(a, blockIdx.x, C::TB, pr0, pr1);
+    if (pr1) {
+#pragma unroll
+      for (int k = 0; k < kPrefetch; ++k) {
+        const uint64_t o = pr0 + 16ull * (tid + k * kThreads);
+        pf[k] = (o < pr1) ? load_chunk(a, o) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+
+  for (uint32_t t = blockIdx.x; t < a.ntiles; t += G) {
     const uint32_t b0 = t * a.bpt;
     const uint32_t nb = min(a.bpt, a.nblk - b0);
 #ifdef MTBLX_STAMPS
@@ -523,54 +467,106 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
 #endif
     STAMP(7);
 
-    // ---- 1. stage: wave w stages blocks w, w+4, ... ----
-    for (uint32_t j = wv; j < nb; j += kThreads / kWave) {
-      const uint32_t L = a.blk_len[b0 + j];
-      const uint8_t* g = a.data + a.blk_off[b0 + j];
-      const uint32_t so = 16u + j * a.slot;
-      uint32_t bo = kNotStaged;
-      if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)C::TB) bo = so + stage_slot(S.stage + so, g, L, lo, hi, lane);
-      if (lane == 0) { S.boff[j] = bo; S.blen[j] = L; }
+    // ---- 1. stage ----
+    uint64_t r0 = pr0, r1 = pr1;
+    if (!C::PREFETCH) tile_range(a, t, C::TB, r0, r1);
+    if (r1) {
+      // contiguous layout: range byte x at stage offset 16 + x
+      const uint32_t nch = (uint32_t)((r1 - r0 + 15) >> 4);
+      if (C::PREFETCH) {
+#pragma unroll
+        for (int k = 0; k < kPrefetch; ++k) {
+          const uint32_t c = tid + k * kThreads;
+          if (c < nch) *reinterpret_cast<uint4*>(S.stage + 16 + 16 * c) = pf[k];
+        }
+        for (uint32_t c = tid + kPrefetch * kThreads; c < nch; c += kThreads)
+          *reinterpret_cast<uint4*>(S.stage + 16 + 16 * c) = load_chunk(a, r0 + 16ull * c);
+      } else {
+        constexpr int U = 4;
+        uint32_t c = tid;
+        for (; c + (U - 1) * kThreads < nch; c += U * kThreads) {
+          uint4 v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u] = load_chunk(a, r0 + 16ull * (c + u * kThreads));
+#pragma unroll
+          for (int u = 0; u < U; ++u) *reinterpret_cast<uint4*>(S.stage + 16 + 16 * (c + u * kThreads)) = v[u];
+        }
+        for (; c < nch; c += kThreads) *reinterpret_cast<uint4*>(S.stage + 16 + 16 * c) = load_chunk(a, r0 + 16ull * c);
+      }
+      if (tid < (int)nb) {
+        const uint64_t off = a.blk_off[b0 + tid];
+        const uint32_t L = a.blk_len[b0 + tid];
+        S.boff[tid] = (off >= r0 && off + L <= r1) ? (uint32_t)(16 + off - r0) : kNotStaged;
+        S.blen[tid] = L;
+      }
+    } else {
+      // fallback: one 16-aligned slot per block, wave w stages blocks w, w+4, ...
+      for (uint32_t j = wv; j < nb; j += kThreads / kWave) {
+        const uint32_t L = a.blk_len[b0 + j];
+        const uint64_t off = a.blk_off[b0 + j];
+        const uint32_t so = 16u + j * a.slot;
+        uint32_t bo = kNotStaged;
+        if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)C::TB) bo = so + stage_slot(a, S.stage + so, off, L, lane);
+        if (lane == 0) { S.boff[j] = bo; S.blen[j] = L; }
+      }
     }
     __syncthreads();
     STAMP(0);
 
-    // ---- 2. trailers (Block::init, src/block.rs:16-49) ----
-    if (tid < (int)nb) {
-      const uint32_t j = tid, L = S.blen[j], bo = S.boff[j];
-      uint32_t n = 0, R = 0, ok = 0;
-      if (bo != kNotStaged && L >= 8) {
-        n = lds_rd32(S.stage, bo + L - 4);
-        if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
+    // ---- 1b. prefetch the next tile of this workgroup into registers ----
+    if (C::PREFETCH) {
+      pr1 = 0;
+      if (t + G < a.ntiles) {
+        tile_range(a, t + G, C::TB, pr0, pr1);
+        if (pr1) {
+#pragma unroll
+          for (int k = 0; k < kPrefetch; ++k) {
+            const uint64_t o = pr0 + 16ull * (tid + k * kThreads);
+            pf[k] = (o < pr1) ? load_chunk(a, o) : make_uint4(0, 0, 0, 0);
+          }
+        }
       }
-      S.bn[j] = ok ? n : 0;
-      S.bR[j] = R;
-      S.bok[j] = ok;
-      S.bwr[j] = 1;
-      S.bst[j] = MTBLX_ST_OK;
     }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t f = 0;
-      for (uint32_t j = 0; j < nb; ++j) {
-        S.bint0[j] = f;
-        if (S.bok[j] && f + S.bn[j] <= (uint32_t)C::MAXINT) f += S.bn[j];
-        else S.bok[j] = 0;
+
+    // ---- 2. trailers (Block::init, src/block.rs:16-49) + interval numbering (wave 0) ----
+    if (wv == 0) {
+      uint32_t n = 0, R = 0, ok = 0;
+      if (lane < (int)nb) {
+        const uint32_t j = lane, L = S.blen[j], bo = S.boff[j];
+        if (bo != kNotStaged && L >= 8) {
+          n = lds_rd32(S.stage, bo + L - 4);
+          if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
+        }
+        if (!ok) n = 0;
       }
-      S.bint0[nb] = f;
+      uint32_t incl = wave_incl_scan(n, lane);
+      // blocks whose intervals overflow MAXINT become irregular
+      if (ok && incl > (uint32_t)C::MAXINT) { ok = 0; }
+      n = ok ? n : 0;
+      incl = wave_incl_scan(n, lane);
+      if (lane < (int)nb) {
+        S.bn[lane] = n;
+        S.bR[lane] = R;
+        S.bok[lane] = ok;
+        S.bwr[lane] = 1;
+        S.bst[lane] = MTBLX_ST_OK;
+        S.bint0[lane] = incl - n;
+      }
+      if (lane == (int)nb - 1) S.bint0[nb] = incl;
     }
     __syncthreads();
     const uint32_t nint = S.bint0[nb];
 
     // ---- 3. walk 1: one thread per restart interval across the tile ----
-    for (uint32_t f = tid; f < nint; f += kThreads) {
+    if (tid < (int)nint) {
+      const uint32_t f = tid;
       uint32_t j = 0;
       while (S.bint0[j + 1] <= f) ++j;
       const uint32_t i = f - S.bint0[j], bo = S.boff[j], L = S.blen[j], R = S.bR[j], n = S.bn[j];
       const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
       const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
       uint32_t cnt, kb, vb;
-      const bool ok = walk_interval<false, C>(S, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0, nullptr, nullptr, 0, 0) &&
+      const bool ok = walk_interval<false, C>(S, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0) &&
                       cnt <= (uint32_t)C::MAXREC;
       S.icnt[f] = cnt;
       S.ikb[f] = kb;
@@ -579,8 +575,8 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
       if (!ok) S.bok[j] = 0;
     }
     __syncthreads();
-
     STAMP(1);
+
     // ---- 4. irregular blocks: exact serial count (generic path, lane per block) ----
     if (tid < (int)nb && !S.bok[tid]) {
       const uint32_t j = tid, bo = S.boff[j], L = S.blen[j];
@@ -591,8 +587,7 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
       S.bvb[j] = (uint32_t)o.vb;
       S.bst[j] = o.st;
     }
-    // scan of interval counts (regular blocks only) -> tile-relative interval bases
-    // (MAXINT <= 256: one interval per thread)
+    // interval scan (regular blocks only) -> exclusive bases
     {
       uint32_t xc = 0, xk = 0, xv = 0;
       const uint32_t f = tid;
@@ -600,41 +595,145 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
       uint32_t tot[3];
       wg_excl_scan3(S, xc, xk, xv, tot);
       if (f < nint) { S.icnt[f] = xc; S.ikb[f] = xk; S.ivb[f] = xv; }
-      if (tid == 0) { S.icnt[nint] = tot[0]; S.ikb[nint] = tot[1]; S.ivb[nint] = tot[2]; }
+      if (tid == 0) { S.icnt[nint] = tot[0]; S.ikb[nint] = tot[1]; S.ivb[nint] = tot[2]; S.nfastrec = tot[0]; }
     }
     __syncthreads();
-    // block totals + tile-relative block bases (serial over <= MAXBLK blocks)
-    if (tid == 0) {
-      uint32_t rr = 0, rk = 0, rv = 0, fastrec = 0;
-      for (uint32_t j = 0; j < nb; ++j) {
+    // block totals + tile-relative block bases (wave 0, one lane per block)
+    if (wv == 0) {
+      uint32_t c = 0, k = 0, v = 0, rf = 0;
+      if (lane < (int)nb) {
+        const uint32_t j = lane;
+        const uint32_t fa = S.bint0[j], fb = S.bint0[j + 1];
+        rf = S.icnt[fa];
         if (S.bok[j]) {
-          const uint32_t fa = S.bint0[j], fb = S.bint0[j + 1];
-          S.bcnt[j] = S.icnt[fb] - S.icnt[fa];
-          S.bkb[j] = S.ikb[fb] - S.ikb[fa];
-          S.bvb[j] = S.ivb[fb] - S.ivb[fa];
-          fastrec += S.bcnt[j];
+          c = S.icnt[fb] - S.icnt[fa];
+          k = S.ikb[fb] - S.ikb[fa];
+          v = S.ivb[fb] - S.ivb[fa];
+        } else {
+          c = S.bcnt[j];
+          k = S.bkb[j];
+          v = S.bvb[j];
         }
-        S.brb[j] = rr; S.bkbb[j] = rk; S.bvbb[j] = rv;
-        rr += S.bcnt[j]; rk += S.bkb[j]; rv += S.bvb[j];
       }
-      S.ttot[0] = rr; S.ttot[1] = rk; S.ttot[2] = rv;
-      S.nfastrec = fastrec;
+      const uint32_t ic = wave_incl_scan(c, lane), ik = wave_incl_scan(k, lane), iv = wave_incl_scan(v, lane);
+      if (lane < (int)nb) {
+        S.bcnt[lane] = c; S.bkb[lane] = k; S.bvb[lane] = v;
+        S.brb[lane] = ic - c; S.bkbb[lane] = ik - k; S.bvbb[lane] = iv - v;
+        S.brf[lane] = rf;
+      }
+      if (lane == (int)nb - 1) { S.ttot[0] = ic; S.ttot[1] = ik; S.ttot[2] = iv; }
     }
     __syncthreads();
-
-    // ---- 5. publish aggregate + decoupled look-back (whole workgroup) ----
     STAMP(2);
-    tile_lookback<C>(S, a.lb, t, a.totals);
-    __syncthreads();
-    if (tid == 0 && t == a.ntiles - 1) {
-      a.totals[0] = S.tpre[0] + S.ttot[0];
-      a.totals[1] = S.tpre[1] + S.ttot[1];
-      a.totals[2] = S.tpre[2] + S.ttot[2];
+
+    // ---- 5. publish the tile aggregate, issue the look-back loads ----
+    const uint32_t agg_r = S.ttot[0], agg_k = S.ttot[1], agg_v = S.ttot[2];
+    if (tid == 0) {
+      if (agg_k >= kField) {
+        __hip_atomic_store(&a.lbx[t], (uint64_t)agg_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      }
+      __hip_atomic_store(&a.lb[t], pack_agg(agg_r, agg_k, agg_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t lo = (t >= G) ? t - G + 1 : 0;   // window of predecessors [lo, t)
+    uint64_t lw[kMaxLookbackLoads];
+#pragma unroll
+    for (int m = 0; m < kMaxLookbackLoads; ++m) {
+      const int64_t i = (int64_t)t - 1 - tid - (int64_t)m * kThreads;
+      lw[m] = kReady;  // outside the window: contributes 0
+      if (i >= (int64_t)lo) lw[m] = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     STAMP(3);
-    const uint64_t pr = S.tpre[0], pk = S.tpre[1], pv = S.tpre[2];
 
-    // ---- 6. per-block outputs + capacity check ----
+    // ---- 6. walk 2: per-record metadata (chunk 0) ----
+    const uint32_t nfr = S.nfastrec;
+    uint32_t fa = 0, fb = 0, rlo = 0, rhi = 0;
+    auto plan_chunk = [&](uint32_t from) {
+      fa = from;
+      const uint32_t lim = S.icnt[fa] + (uint32_t)C::MAXREC;
+      if (S.icnt[nint] <= lim) {
+        fb = nint;
+      } else {  // largest fb with icnt[fb] <= lim (walk 1 guarantees one interval fits)
+        uint32_t l = fa + 1, h = nint;
+        while (l < h) {
+          const uint32_t m = (l + h + 1) / 2;
+          if (S.icnt[m] <= lim) l = m; else h = m - 1;
+        }
+        fb = l;
+      }
+      rlo = S.icnt[fa];
+      rhi = S.icnt[fb];
+    };
+    auto walk2 = [&]() {
+      const uint32_t f = fa + tid;
+      if (f < fb) {
+        const uint32_t j = S.iblk[f];
+        if (S.bok[j]) {
+          const uint32_t fj = S.bint0[j];
+          const uint32_t i = f - fj, bo = S.boff[j], L = S.blen[j], R = S.bR[j], n = S.bn[j];
+          const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
+          const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
+          const uint32_t kin = S.ikb[f] - S.ikb[fj], vin = S.ivb[f] - S.ivb[fj];
+          uint32_t c, k, v;
+          walk_interval<true, C>(S, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi);
+        }
+      }
+    };
+    if (a.write && nfr) {
+      plan_chunk(0);
+      walk2();
+    }
+    STAMP(4);
+
+    // ---- 7. finish the look-back ----
+    {
+      uint64_t sr = 0, sk = 0, sv = 0;
+      bool timeout = false;
+#pragma unroll
+      for (int m = 0; m < kMaxLookbackLoads; ++m) {
+        const int64_t i = (int64_t)t - 1 - tid - (int64_t)m * kThreads;
+        uint64_t w = lw[m];
+        uint32_t spins = 0;
+        while (!(w & kReady)) {
+          __builtin_amdgcn_s_sleep(2);
+          w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (++spins > (1u << 22)) { timeout = true; w = kReady; }
+        }
+        if (i >= (int64_t)lo) {
+          sr += (w >> 42) & kField;
+          sv += (w >> 21) & kField;
+          uint64_t kk = w & kField;
+          if (kk == kField) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            kk = __hip_atomic_load(&a.lbx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          sk += kk;
+        }
+      }
+      if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 2ull);
+      sr = wave_sum64(sr);
+      sk = wave_sum64(sk);
+      sv = wave_sum64(sv);
+      if (lane == 0) { S.lbsum[wv][0] = sr; S.lbsum[wv][1] = sk; S.lbsum[wv][2] = sv; }
+      __syncthreads();
+      if (tid == 0) {
+        const uint64_t pre0 = S.tinc[0] + S.lbsum[0][0] + S.lbsum[1][0] + S.lbsum[2][0] + S.lbsum[3][0];
+        const uint64_t pre1 = S.tinc[1] + S.lbsum[0][1] + S.lbsum[1][1] + S.lbsum[2][1] + S.lbsum[3][1];
+        const uint64_t pre2 = S.tinc[2] + S.lbsum[0][2] + S.lbsum[1][2] + S.lbsum[2][2] + S.lbsum[3][2];
+        S.tpre[0] = pre0; S.tpre[1] = pre1; S.tpre[2] = pre2;
+        S.tinc[0] = pre0 + agg_r; S.tinc[1] = pre1 + agg_k; S.tinc[2] = pre2 + agg_v;
+        if (t == a.ntiles - 1) {
+          a.totals[0] = pre0 + agg_r;
+          a.totals[1] = pre1 + agg_k;
+          a.totals[2] = pre2 + agg_v;
+        }
+      }
+      __syncthreads();
+    }
+    const uint64_t pr = S.tpre[0], pk = S.tpre[1], pv = S.tpre[2];
+    STAMP(5);
+
+    // ---- 8. per-block outputs + capacity check ----
     if (tid < (int)nb) {
       const uint32_t j = tid, b = b0 + j;
       const uint64_t rb = pr + S.brb[j], kb = pk + S.bkbb[j], vb = pv + S.bvbb[j];
@@ -653,74 +752,46 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
     if (!a.write) { __syncthreads(); continue; }
     __syncthreads();
 
-    STAMP(4);
-    // ---- 7. walk 2 (metadata) + copy, in chunks of whole intervals of <= MAXREC records ----
-    // icnt[f] = regular records before interval f (irregular blocks contribute 0), so
-    // icnt is the metadata slot numbering and is monotone: chunks are found by search.
-    for (uint32_t fa = 0; fa < nint;) {
-      uint32_t fb;
-      {
-        const uint32_t lim = S.icnt[fa] + (uint32_t)C::MAXREC;
-        if (S.icnt[nint] <= lim) {
-          fb = nint;
-        } else {  // largest fb with icnt[fb] <= lim (walk 1 guarantees one interval fits)
-          uint32_t l = fa + 1, h = nint;
-          while (l < h) {
-            const uint32_t m = (l + h + 1) / 2;
-            if (S.icnt[m] <= lim) l = m; else h = m - 1;
-          }
-          fb = l;
-        }
-      }
-      const uint32_t rlo = S.icnt[fa], rhi = S.icnt[fb];
-      for (uint32_t f = fa + tid; f < fb; f += kThreads) {
-        const uint32_t j = S.iblk[f];
-        if (!S.bok[j]) continue;
-        const uint32_t fj = S.bint0[j];
-        const uint32_t i = f - fj, bo = S.boff[j], L = S.blen[j], R = S.bR[j], n = S.bn[j];
-        const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
-        const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
-        const uint32_t kin = S.ikb[f] - S.ikb[fj], vin = S.ivb[f] - S.ivb[fj];  // bytes before f in block
-        const uint32_t rin = S.icnt[f] - S.icnt[fj];                             // records before f in block
-        uint32_t* ke = S.bwr[j] ? a.key_end + pr + S.brb[j] + rin : nullptr;
-        uint32_t* ve = S.bwr[j] ? a.val_end + pr + S.brb[j] + rin : nullptr;
-        uint32_t c, k, v;
-        walk_interval<true, C>(S, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi,
-                               ke, ve, kin, vin);
-      }
-      __syncthreads();
-      STAMP(5);
-      // copy: one thread per record
+    // ---- 9. copy (one thread per record), chunk by chunk ----
+    while (nfr) {
       for (uint32_t q = tid; q < rhi - rlo; q += kThreads) {
-        const uint32_t j = S.rblk[q];
+        const uint4 rr = *reinterpret_cast<const uint4*>(&S.rec[q]);
+        const uint32_t j = rr.w >> 24;
         if (!S.bwr[j]) continue;
         const uint32_t bo = S.boff[j];
-        const uint32_t vl = S.rvl[q];
-        const uint32_t vsrc = bo + S.rpos[q] + S.rns[q];
-        uint8_t* vd = a.vals + pv + S.rvs[q];
+        const uint32_t pos = rr.x & 0xFFFFu, shr = rr.x >> 16, ns = rr.y & 0xFFFFu, vl = rr.y >> 16;
+        const uint32_t ks = rr.z, vs = rr.w & 0xFFFFFFu;
+        const uint32_t klen = shr + ns;
+        // key_end / val_end: END offsets relative to the block's bases
+        const uint64_t gr = pr + S.brb[j] + (q + rlo - S.brf[j]);
+        a.key_end[gr] = ks + klen - S.bkbb[j];
+        a.val_end[gr] = vs + vl - S.bvbb[j];
+        // value bytes: LDS window -> unaligned 16-byte stores
+        const uint32_t vsrc = bo + pos + ns;
+        uint8_t* vd = a.vals + pv + vs;
         for (uint32_t o = 0; o < vl; o += 16) {
-          uint4 wv4 = lds_win16(S.stage, vsrc + o);
+          uint4 w4 = lds_win16(S.stage, vsrc + o);
           const uint32_t m = vl - o;
-          store_bytes(vd + o, wv4, m < 16 ? m : 16);
+          store_bytes(vd + o, w4, m < 16 ? m : 16);
         }
-        const uint32_t shr = S.rsh[q];
-        const uint32_t klen = shr + S.rns[q];
-        uint8_t* kd = a.keys + pk + S.rks[q];
+        // key bytes: each byte comes from the suffix of the latest record s <= q (same
+        // interval) with shared_s <= byte index
+        uint8_t* kd = a.keys + pk + ks;
         for (uint32_t j0 = 0; j0 < klen; j0 += 16) {
           const uint32_t jend = (j0 + 16 < klen) ? j0 + 16 : klen;
           uint4 outw = make_uint4(0, 0, 0, 0);
           uint32_t jj = j0;
           while (jj < jend) {
-            // source of key byte jj: the latest record s <= q with shared_s <= jj (same interval;
-            // the interval's first record has shared 0 and lies in this chunk)
-            uint32_t sidx = q, m = klen, shs = shr;
+            uint32_t sidx = q, m = klen, shs = shr, ps = pos;
             while (shs > jj) {
               m = shs < m ? shs : m;
               --sidx;
-              shs = S.rsh[sidx];
+              const uint32_t x = S.rec[sidx].pos_sh;
+              shs = x >> 16;
+              ps = x & 0xFFFFu;
             }
             const uint32_t seg = m < jend ? m : jend;
-            const uint32_t src = bo + S.rpos[sidx] + (jj - shs);
+            const uint32_t src = bo + ps + (jj - shs);
             uint4 w4 = lds_win16(S.stage, src - (jj - j0));
             merge_bytes(outw, w4, (int)(jj - j0), (int)(seg - j0));
             jj = seg;
@@ -729,11 +800,14 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
         }
       }
       __syncthreads();
-      STAMP(6);
-      fa = fb;
+      if (fb >= nint) break;
+      plan_chunk(fb);
+      walk2();
+      __syncthreads();
     }
+    STAMP(6);
 
-    // ---- 8. irregular blocks: exact serial write (lane per block) ----
+    // ---- 10. irregular blocks: exact serial write (lane per block) ----
     if (tid < (int)nb && !S.bok[tid] && S.bwr[tid]) {
       const uint32_t j = tid, bo = S.boff[j], L = S.blen[j];
       const uint8_t* d = (bo != kNotStaged) ? (S.stage + bo) : (a.data + a.blk_off[b0 + j]);
@@ -750,8 +824,8 @@ __global__ void __launch_bounds__(kThreads) k_decode_tiles(TileArgs a) {
 #endif
 }
 
-using CfgSmall = TileCfg<32768, 512, 128, 16>;
-using CfgLarge = TileCfg<67584, 1024, 256, 4>;
+using CfgSmall = TileCfg<32768, 640, 256, 64, true, 3>;
+using CfgLarge = TileCfg<67584, 1024, 256, 16, false, 1>;
 
 }  // namespace mtblx
 
@@ -768,17 +842,19 @@ struct Plan {
 
 Plan make_plan(uint32_t nblk, uint32_t max_len) {
   Plan p{};
-  const uint32_t slot = ((max_len + 15u + 15u) / 16u) * 16u;
+  const uint32_t slot = ((max_len + 30u) / 16u) * 16u;
+  // contiguous staging: blocks + framing (<= 14 B each) + 16 B alignment + 32 B tail
+  const uint32_t per = max_len + 16u;
   uint32_t usable = CfgSmall::TB - 48;
   if (max_len != 0 && slot <= usable) {
     p.large = false;
     p.slot = slot;
-    p.bpt = std::min<uint32_t>(usable / slot, CfgSmall::MAXBLK);
+    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, slot), CfgSmall::MAXBLK));
   } else {
     usable = CfgLarge::TB - 48;
     p.large = true;
     p.slot = (max_len != 0 && slot <= usable) ? slot : usable;
-    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / p.slot, CfgLarge::MAXBLK));
+    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, p.slot), CfgLarge::MAXBLK));
   }
   p.ntiles = (nblk + p.bpt - 1) / p.bpt;
   return p;
@@ -789,20 +865,21 @@ int resident_grid(uint32_t ntiles) {
   static int cached = 0;
   if (!cached) {
     int dev = 0, ncu = 0, occ = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_decode_tiles<C>, kThreads, 0) != hipSuccess || occ < 1)
       occ = 1;
     int lds_lim = (int)((160u * 1024u) / sizeof(TileLds<C>));
     if (lds_lim < 1) lds_lim = 1;
     cached = std::max(1, ncu * std::min(occ, lds_lim));
+    cached = std::min(cached, kMaxLookbackLoads * kThreads + 1);  // look-back window = G - 1
   }
   return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
 }
 }  // namespace
 
-// workspace: [0, 256) diagnostic stamps | look-back words (worst case one block per tile)
-extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
+// workspace: [0, 256) diagnostic stamps | lb[nblk] | lbx[nblk]
+extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 16u + 64u; }
 
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
                               hipStream_t s) {
@@ -810,12 +887,13 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
   const Plan p = make_plan(nblk, in->max_blk_len);
   uint64_t* dbg = reinterpret_cast<uint64_t*>(ws);
   uint64_t* lb = dbg + 32;
-  if (hipMemsetAsync(ws, 0, 256u + (size_t)p.ntiles * 24u, s) != hipSuccess) return MTBLX_E_HIP;
+  uint64_t* lbx = lb + nblk;
+  if (hipMemsetAsync(ws, 0, 256u + (size_t)p.ntiles * 8u, s) != hipSuccess) return MTBLX_E_HIP;
   if (hipMemsetAsync(out->totals, 0, 32, s) != hipSuccess) return MTBLX_E_HIP;
   TileArgs a{in->data,     in->data_len,  in->blk_off,  in->blk_len,   nblk,         p.bpt,         p.slot,
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
-             lb,           dbg,           write ? 1 : 0};
+             lb,           lbx,           dbg,          write ? 1 : 0};
   if (p.large) {
     hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
   } else {

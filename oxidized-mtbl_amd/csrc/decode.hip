@@ -81,13 +81,21 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, uint4 w, uint32_t m) {
   if (m & 1) { *p = (uint8_t)w.x; }
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t t = __shfl_up(v, d, kWave);
-    if (lane >= d) v += t;
-  }
-  return v;
+// Inclusive scan over the 64 lanes with DPP (row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast:15 / row_bcast:31 across rows): 6 VALU ops, no LDS permutes.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int /*lane*/ = 0) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
+// sum over the 64 lanes, broadcast (uniform)
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -402,6 +410,45 @@ __device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32
   return p == e && (prevlen <= 0xFFFFu);
 }
 
+// Tight walk for the common case: every header is three 1-byte varints.  All checks are
+// accumulated into `bad` off the loop-carried chain (p -> LDS read -> p'); any multi-byte
+// header, shared > previous length, or overrun ends it and the caller falls back to the
+// exact walk_interval above.  Same preconditions, same results when it returns true.
+template <bool WRITE, class C>
+__device__ __forceinline__ bool walk_fast(TileLds<C>& S, uint32_t bo, uint32_t R, uint32_t s, uint32_t e,
+                                          uint32_t& cnt, uint32_t& kb, uint32_t& vb, uint32_t slot0, uint32_t kbase,
+                                          uint32_t vbase, uint32_t blk, uint32_t rlo, uint32_t rhi) {
+  cnt = kb = vb = 0;
+  if (!(s < e && e <= R)) return false;
+  uint32_t p = s, prevlen = 0, bad = 0;
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(S.stage);
+  do {
+    const uint32_t ad = bo + p;
+    const uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
+    const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
+    const uint32_t np = p + 3u + ns + vl;
+    bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R);
+    if (WRITE) {
+      const uint32_t r = slot0 + cnt;
+      if (r >= rlo && r < rhi) {
+        Rec x;
+        x.pos_sh = (p + 3u) | (sh << 16);
+        x.ns_vl = ns | (vl << 16);
+        x.ks = kbase + kb;
+        x.vs_blk = (vbase + vb) | (blk << 24);
+        S.rec[r - rlo] = x;
+      }
+    }
+    const uint32_t klen = sh + ns;
+    cnt += 1;
+    kb += klen;
+    vb += vl;
+    prevlen = klen;
+    p = np;
+  } while (p < e && !bad);
+  return !bad && p == e;
+}
+
 // exclusive scan of 3 u32 per thread over the workgroup; returns the workgroup totals
 template <class C>
 __device__ __forceinline__ void wg_excl_scan3(TileLds<C>& S, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t tot[3]) {
@@ -566,8 +613,9 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
       const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
       const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
       uint32_t cnt, kb, vb;
-      const bool ok = walk_interval<false, C>(S, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0) &&
-                      cnt <= (uint32_t)C::MAXREC;
+      bool ok = walk_fast<false, C>(S, bo, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
+      if (!ok) ok = walk_interval<false, C>(S, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
+      ok = ok && cnt <= (uint32_t)C::MAXREC;
       S.icnt[f] = cnt;
       S.ikb[f] = kb;
       S.ivb[f] = vb;
@@ -675,7 +723,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
           const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
           const uint32_t kin = S.ikb[f] - S.ikb[fj], vin = S.ivb[f] - S.ivb[fj];
           uint32_t c, k, v;
-          walk_interval<true, C>(S, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi);
+          if (!walk_fast<true, C>(S, bo, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi))
+            walk_interval<true, C>(S, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi);
         }
       }
     };
@@ -711,9 +760,11 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         }
       }
       if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 2ull);
-      sr = wave_sum64(sr);
-      sk = wave_sum64(sk);
-      sv = wave_sum64(sv);
+      // per-thread sums are < 2^23 (4 tiles x 21-bit fields) unless a key field saturated
+      sr = wave_sum32((uint32_t)sr);
+      sv = wave_sum32((uint32_t)sv);
+      if (__ballot(sk >= (1ull << 24)) == 0ull) sk = wave_sum32((uint32_t)sk);
+      else sk = wave_sum64(sk);
       if (lane == 0) { S.lbsum[wv][0] = sr; S.lbsum[wv][1] = sk; S.lbsum[wv][2] = sv; }
       __syncthreads();
       if (tid == 0) {
@@ -766,6 +817,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         const uint64_t gr = pr + S.brb[j] + (q + rlo - S.brf[j]);
         a.key_end[gr] = ks + klen - S.bkbb[j];
         a.val_end[gr] = vs + vl - S.bvbb[j];
+#ifndef MTBLX_ABL_NOVAL
         // value bytes: LDS window -> unaligned 16-byte stores
         const uint32_t vsrc = bo + pos + ns;
         uint8_t* vd = a.vals + pv + vs;
@@ -774,6 +826,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
           const uint32_t m = vl - o;
           store_bytes(vd + o, w4, m < 16 ? m : 16);
         }
+#endif
+#ifndef MTBLX_ABL_NOKEY
         // key bytes: each byte comes from the suffix of the latest record s <= q (same
         // interval) with shared_s <= byte index
         uint8_t* kd = a.keys + pk + ks;
@@ -798,6 +852,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
           }
           store_bytes(kd + j0, outw, jend - j0);
         }
+#endif
       }
       __syncthreads();
       if (fb >= nint) break;

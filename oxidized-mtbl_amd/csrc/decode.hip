@@ -360,22 +360,22 @@ __device__ __forceinline__ uint32_t stage_slot(const TileArgs& a, uint8_t* slot,
 // ones shared <= previous key length (so Vec capacity never matters); fields fit 16
 // bits; the walk lands exactly on e.  Under these the reference's linear chain
 // (src/block.rs:119-143) visits exactly these entries and rebuilds exactly these keys.
-template <bool WRITE, class C>
-__device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32_t L, uint32_t R, uint32_t s,
+template <bool WRITE>
+__device__ __forceinline__ bool walk_interval(const uint8_t* stage, Rec* recs, uint32_t bo, uint32_t L, uint32_t R, uint32_t s,
                                               uint32_t e, uint32_t& cnt, uint32_t& kb, uint32_t& vb, uint32_t slot0,
                                               uint32_t kbase, uint32_t vbase, uint32_t blk, uint32_t rlo,
                                               uint32_t rhi) {
   cnt = kb = vb = 0;
   if (!(s < e && e <= R)) return false;
   uint32_t p = s, prevlen = 0;
-  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(S.stage);
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   while (p < e) {
     const uint32_t ad = bo + p;
     uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
     uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu, h = 3;
     if (__builtin_expect((hw & 0x808080u) != 0u, 0)) {  // multi-byte varint header (slow path)
       if (R - p < 3u) return false;
-      uint4 W = lds_win16(S.stage, ad);
+      uint4 W = lds_win16(stage, ad);
       uint32_t l0 = dec32(W, 0, L - p, sh);
       if (l0 == 0) return false;
       uint32_t l1 = dec32(W, l0, L - p - l0, ns);
@@ -398,7 +398,7 @@ __device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32
         x.ns_vl = ns | (vl << 16);
         x.ks = kbase + kb;
         x.vs_blk = (vbase + vb) | (blk << 24);
-        S.rec[r - rlo] = x;
+        recs[r - rlo] = x;
       }
     }
     cnt += 1;
@@ -414,14 +414,14 @@ __device__ __forceinline__ bool walk_interval(TileLds<C>& S, uint32_t bo, uint32
 // accumulated into `bad` off the loop-carried chain (p -> LDS read -> p'); any multi-byte
 // header, shared > previous length, or overrun ends it and the caller falls back to the
 // exact walk_interval above.  Same preconditions, same results when it returns true.
-template <bool WRITE, class C>
-__device__ __forceinline__ bool walk_fast(TileLds<C>& S, uint32_t bo, uint32_t R, uint32_t s, uint32_t e,
+template <bool WRITE>
+__device__ __forceinline__ bool walk_fast(const uint8_t* stage, Rec* recs, uint32_t bo, uint32_t R, uint32_t s, uint32_t e,
                                           uint32_t& cnt, uint32_t& kb, uint32_t& vb, uint32_t slot0, uint32_t kbase,
                                           uint32_t vbase, uint32_t blk, uint32_t rlo, uint32_t rhi) {
   cnt = kb = vb = 0;
   if (!(s < e && e <= R)) return false;
   uint32_t p = s, prevlen = 0, bad = 0;
-  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(S.stage);
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   do {
     const uint32_t ad = bo + p;
     const uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
@@ -436,7 +436,7 @@ __device__ __forceinline__ bool walk_fast(TileLds<C>& S, uint32_t bo, uint32_t R
         x.ns_vl = ns | (vl << 16);
         x.ks = kbase + kb;
         x.vs_blk = (vbase + vb) | (blk << 24);
-        S.rec[r - rlo] = x;
+        recs[r - rlo] = x;
       }
     }
     const uint32_t klen = sh + ns;
@@ -613,8 +613,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
       const uint32_t s = lds_rd32(S.stage, bo + R + 4u * i);
       const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
       uint32_t cnt, kb, vb;
-      bool ok = walk_fast<false, C>(S, bo, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
-      if (!ok) ok = walk_interval<false, C>(S, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
+      bool ok = walk_fast<false>(S.stage, S.rec, bo, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
+      if (!ok) ok = walk_interval<false>(S.stage, S.rec, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
       ok = ok && cnt <= (uint32_t)C::MAXREC;
       S.icnt[f] = cnt;
       S.ikb[f] = kb;
@@ -723,8 +723,9 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
           const uint32_t e = (i + 1 < n) ? lds_rd32(S.stage, bo + R + 4u * (i + 1)) : R;
           const uint32_t kin = S.ikb[f] - S.ikb[fj], vin = S.ivb[f] - S.ivb[fj];
           uint32_t c, k, v;
-          if (!walk_fast<true, C>(S, bo, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi))
-            walk_interval<true, C>(S, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi);
+          if (!walk_fast<true>(S.stage, S.rec, bo, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo, rhi))
+            walk_interval<true>(S.stage, S.rec, bo, L, R, s, e, c, k, v, S.icnt[f], S.bkbb[j] + kin, S.bvbb[j] + vin, j, rlo,
+                                rhi);
         }
       }
     };
@@ -879,6 +880,455 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 #endif
 }
 
+// ----------------------------------------------------------------------------------
+// software-pipelined decoder for small blocks (k_decode_pipe)
+// ----------------------------------------------------------------------------------
+// One 512-thread workgroup per CU, persistent, static round-robin over tiles (t = g + kG).
+// A ring of three tile buffers in LDS holds three tiles in flight.  In iteration i:
+//   wave 0      : walk 1 of tile i+2 (counts), interval scan, block totals, publish A
+//   wave 1      : walk 2 of tile i+1 (per-record metadata), look-back -> prefix,
+//                 per-block outputs (nrec, bases, status)
+//   waves 2..7  : stage tile i+2 (from registers loaded during the previous iteration),
+//                 prefetch tile i+3 into registers, copy tile i (keys, values, ends)
+//   __syncthreads
+// The serial, latency-bound walks run beside the bandwidth-bound copy instead of in
+// front of it, and the look-back of tile i+1 reads aggregates that the other
+// workgroups published an iteration earlier, so in steady state nothing waits.
+// Wave 0 starts walk 1 only after waves 2..7 signal (LDS counter) that the tile is
+// staged.
+constexpr int kPipeThreads = 512;
+constexpr int kPipeCopyThreads = kPipeThreads - 2 * kWave;  // waves 2..7
+constexpr int kPipeCopyWaves = kPipeCopyThreads / kWave;
+constexpr int kPipeTB = 32768;
+constexpr int kPipeMaxRec = 640;
+constexpr int kPipeMaxInt = 256;
+constexpr int kPipeMaxBlk = 16;
+constexpr int kPipePf = (kPipeTB + 16 * kPipeCopyThreads - 1) / (16 * kPipeCopyThreads);  // uint4 per copy thread
+
+struct alignas(16) PipeBuf {
+  uint8_t stage[kPipeTB];
+  Rec rec[kPipeMaxRec];
+  uint32_t boff[kPipeMaxBlk], blen[kPipeMaxBlk], bR[kPipeMaxBlk], bn[kPipeMaxBlk];
+  uint32_t bok[kPipeMaxBlk], bwr[kPipeMaxBlk];
+  int32_t bst[kPipeMaxBlk];
+  uint32_t bcnt[kPipeMaxBlk], bkb[kPipeMaxBlk], bvb[kPipeMaxBlk];
+  uint32_t brb[kPipeMaxBlk], bkbb[kPipeMaxBlk], bvbb[kPipeMaxBlk], brf[kPipeMaxBlk];
+  uint32_t bint0[kPipeMaxBlk + 1];
+  uint32_t icnt[kPipeMaxInt + 1], ikb[kPipeMaxInt + 1], ivb[kPipeMaxInt + 1];
+  uint8_t iblk[kPipeMaxInt];
+  uint64_t tpre[3];
+  uint32_t ttot[3];
+  uint32_t nfastrec, nb, b0;
+};
+
+struct alignas(16) PipeLds {
+  PipeBuf buf[3];
+  uint32_t staged;  // waves 2..7 increment after staging a tile (wave 0 waits on it)
+};
+
+// interval -> block of the tile (<= kPipeMaxBlk blocks, linear search)
+__device__ __forceinline__ uint32_t pipe_block_of(const PipeBuf& B, uint32_t f) {
+  uint32_t j = 0;
+  while (B.bint0[j + 1] <= f) ++j;
+  return j;
+}
+
+// wave 0: trailers, walk 1, irregular counts, interval scan, block totals, publish A(t)
+__device__ __forceinline__ void pipe_walk1(PipeBuf& B, const TileArgs& a, uint32_t t, int lane) {
+  const uint32_t nb = B.nb, b0 = B.b0;
+  // trailers (Block::init, src/block.rs:16-49)
+  {
+    uint32_t n = 0, R = 0, ok = 0;
+    if (lane < (int)nb) {
+      const uint32_t L = B.blen[lane], bo = B.boff[lane];
+      if (bo != kNotStaged && L >= 8) {
+        n = lds_rd32(B.stage, bo + L - 4);
+        if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
+      }
+    }
+    uint32_t incl = wave_incl_scan(ok ? n : 0u);
+    if (ok && incl > (uint32_t)kPipeMaxInt) ok = 0;
+    n = ok ? n : 0;
+    incl = wave_incl_scan(n);
+    if (lane < (int)nb) {
+      B.bn[lane] = n; B.bR[lane] = R; B.bok[lane] = ok; B.bwr[lane] = 1; B.bst[lane] = MTBLX_ST_OK;
+      B.bint0[lane] = incl - n;
+    }
+    if (lane == (int)nb - 1) B.bint0[nb] = incl;
+  }
+  wave_sync();
+  const uint32_t nint = B.bint0[nb];
+  // walk 1: one lane per restart interval
+  for (uint32_t f = lane; f < nint; f += kWave) {
+    const uint32_t j = pipe_block_of(B, f);
+    const uint32_t i = f - B.bint0[j], bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
+    const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
+    const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
+    uint32_t cnt, kb, vb;
+    bool ok = walk_fast<false>(B.stage, B.rec, bo, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
+    if (!ok) ok = walk_interval<false>(B.stage, B.rec, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
+    B.icnt[f] = cnt; B.ikb[f] = kb; B.ivb[f] = vb; B.iblk[f] = (uint8_t)j;
+    if (!ok) B.bok[j] = 0;
+  }
+  wave_sync();
+  for (int pass = 0; pass < 2; ++pass) {
+    // irregular blocks: exact serial count (generic path, lane per block)
+    if (lane < (int)nb && !B.bok[lane] && (pass == 0 || B.bst[lane] == -1)) {
+      const uint32_t j = lane, bo = B.boff[j], L = B.blen[j];
+      const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + j]);
+      GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
+      B.bcnt[j] = o.nrec; B.bkb[j] = (uint32_t)o.kb; B.bvb[j] = (uint32_t)o.vb; B.bst[j] = o.st;
+    }
+    wave_sync();
+    // interval scan over regular blocks: lane l owns intervals [l*k, (l+1)*k)
+    const uint32_t k = (nint + kWave - 1) / kWave;
+    uint32_t c = 0, kk = 0, v = 0;
+    for (uint32_t q = 0; q < k; ++q) {
+      const uint32_t f = lane * k + q;
+      if (f < nint && B.bok[B.iblk[f]]) { c += B.icnt[f]; kk += B.ikb[f]; v += B.ivb[f]; }
+    }
+    const uint32_t ic = wave_incl_scan(c), ik = wave_incl_scan(kk), iv = wave_incl_scan(v);
+    uint32_t rc = ic - c, rk = ik - kk, rv = iv - v;
+    for (uint32_t q = 0; q < k; ++q) {
+      const uint32_t f = lane * k + q;
+      if (f < nint) {
+        const bool reg = B.bok[B.iblk[f]] != 0;
+        const uint32_t x = reg ? B.icnt[f] : 0u, y = reg ? B.ikb[f] : 0u, z = reg ? B.ivb[f] : 0u;
+        B.icnt[f] = rc; B.ikb[f] = rk; B.ivb[f] = rv;
+        rc += x; rk += y; rv += z;
+      }
+    }
+    const uint32_t totr = (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
+    if (lane == 0) {
+      B.icnt[nint] = totr;
+      B.ikb[nint] = (uint32_t)__builtin_amdgcn_readlane((int)ik, 63);
+      B.ivb[nint] = (uint32_t)__builtin_amdgcn_readlane((int)iv, 63);
+      B.nfastrec = totr;
+    }
+    wave_sync();
+    if (totr <= (uint32_t)kPipeMaxRec || pass == 1) break;
+    // too many regular records for the metadata array: demote trailing blocks to the
+    // generic path (rare: tiny records), restore their interval counts for the re-scan
+    // is unnecessary (demoted intervals are skipped), then count them serially
+    uint32_t keep = 0;
+    if (lane < (int)nb && B.bok[lane]) {
+      const uint32_t end = B.icnt[B.bint0[lane + 1]];
+      keep = end <= (uint32_t)kPipeMaxRec;
+    } else if (lane < (int)nb) {
+      keep = 1;
+    }
+    // a block is kept only if every earlier regular block is kept too (prefix property)
+    const uint64_t drop = __ballot(lane < (int)nb && !keep);
+    if (lane < (int)nb && drop) {
+      const int first = __builtin_ctzll(drop);
+      if (lane >= first && B.bok[lane]) { B.bok[lane] = 0; B.bst[lane] = -1; }
+    }
+    // restore raw interval counts for the re-scan: re-walk (counts only) is simplest
+    wave_sync();
+    for (uint32_t f = lane; f < nint; f += kWave) {
+      const uint32_t j = B.iblk[f];
+      if (!B.bok[j]) continue;
+      const uint32_t i = f - B.bint0[j], bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
+      const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
+      const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
+      uint32_t cnt, kb2, vb2;
+      if (!walk_fast<false>(B.stage, B.rec, bo, R, s, e, cnt, kb2, vb2, 0, 0, 0, 0, 0, 0))
+        walk_interval<false>(B.stage, B.rec, bo, L, R, s, e, cnt, kb2, vb2, 0, 0, 0, 0, 0, 0);
+      B.icnt[f] = cnt; B.ikb[f] = kb2; B.ivb[f] = vb2;
+    }
+    wave_sync();
+  }
+  // block totals + tile-relative block bases
+  {
+    uint32_t c = 0, k = 0, v = 0, rf = 0;
+    if (lane < (int)nb) {
+      const uint32_t fa = B.bint0[lane], fb = B.bint0[lane + 1];
+      rf = B.icnt[fa];
+      if (B.bok[lane]) {
+        c = B.icnt[fb] - B.icnt[fa]; k = B.ikb[fb] - B.ikb[fa]; v = B.ivb[fb] - B.ivb[fa];
+      } else {
+        c = B.bcnt[lane]; k = B.bkb[lane]; v = B.bvb[lane];
+      }
+    }
+    const uint32_t ic = wave_incl_scan(c), ik = wave_incl_scan(k), iv = wave_incl_scan(v);
+    if (lane < (int)nb) {
+      B.bcnt[lane] = c; B.bkb[lane] = k; B.bvb[lane] = v;
+      B.brb[lane] = ic - c; B.bkbb[lane] = ik - k; B.bvbb[lane] = iv - v; B.brf[lane] = rf;
+    }
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane((int)ic, (int)nb - 1);
+    const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)ik, (int)nb - 1);
+    const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)iv, (int)nb - 1);
+    if (lane == 0) {
+      B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
+      if (tk >= kField) {
+        __hip_atomic_store(&a.lbx[t], (uint64_t)tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      }
+      __hip_atomic_store(&a.lb[t], pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// wave 1: walk 2 (metadata), look-back, per-block outputs.  tinc = inclusive prefix of
+// this workgroup's previous tile (kept in wave 1's registers across iterations).
+__device__ __forceinline__ void pipe_walk2(PipeBuf& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3], int lane) {
+  const uint32_t nb = B.nb, b0 = B.b0, nint = B.bint0[nb];
+  // issue the look-back loads first (window [lo, t) of other workgroups' aggregates)
+  const uint32_t lo = (t >= G) ? t - G + 1 : 0;
+  uint64_t lw[kMaxLookbackLoads];
+#pragma unroll
+  for (int m = 0; m < kMaxLookbackLoads; ++m) {
+    const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
+    lw[m] = kReady;
+    if (i >= (int64_t)lo) lw[m] = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (a.write) {
+    for (uint32_t f = lane; f < nint; f += kWave) {
+      const uint32_t j = B.iblk[f];
+      if (!B.bok[j]) continue;
+      const uint32_t fj = B.bint0[j];
+      const uint32_t i = f - fj, bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
+      const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
+      const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
+      const uint32_t kin = B.ikb[f] - B.ikb[fj], vin = B.ivb[f] - B.ivb[fj];
+      uint32_t c, k, v;
+      if (!walk_fast<true>(B.stage, B.rec, bo, R, s, e, c, k, v, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j, 0,
+                           kPipeMaxRec))
+        walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, c, k, v, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j, 0,
+                            kPipeMaxRec);
+    }
+  }
+  // finish the look-back
+  uint64_t sr = 0, sk = 0, sv = 0;
+  bool timeout = false;
+#pragma unroll
+  for (int m = 0; m < kMaxLookbackLoads; ++m) {
+    const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
+    uint64_t w = lw[m];
+    uint32_t spins = 0;
+    while (!(w & kReady)) {
+      __builtin_amdgcn_s_sleep(2);
+      w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > (1u << 22)) { timeout = true; w = kReady; }
+    }
+    if (i >= (int64_t)lo) {
+      sr += (w >> 42) & kField;
+      sv += (w >> 21) & kField;
+      uint64_t kk = w & kField;
+      if (kk == kField) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        kk = __hip_atomic_load(&a.lbx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      sk += kk;
+    }
+  }
+  if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 2ull);
+  sr = wave_sum32((uint32_t)sr);
+  sv = wave_sum32((uint32_t)sv);
+  if (__ballot(sk >= (1ull << 24)) == 0ull) sk = wave_sum32((uint32_t)sk);
+  else sk = wave_sum64(sk);
+  const uint64_t pr = tinc[0] + sr, pk = tinc[1] + sk, pv = tinc[2] + sv;
+  tinc[0] = pr + B.ttot[0];
+  tinc[1] = pk + B.ttot[1];
+  tinc[2] = pv + B.ttot[2];
+  if (lane == 0) {
+    B.tpre[0] = pr; B.tpre[1] = pk; B.tpre[2] = pv;
+    if (t == a.ntiles - 1) { a.totals[0] = tinc[0]; a.totals[1] = tinc[1]; a.totals[2] = tinc[2]; }
+  }
+  // per-block outputs + capacity check
+  if (lane < (int)nb) {
+    const uint32_t j = lane, b = b0 + j;
+    const uint64_t rb = pr + B.brb[j], kb = pk + B.bkbb[j], vb = pv + B.bvbb[j];
+    a.nrec[b] = B.bcnt[j];
+    a.rec_base[b] = rb;
+    a.key_base[b] = kb;
+    a.val_base[b] = vb;
+    int32_t st = B.bst[j];
+    if (a.write && (rb + B.bcnt[j] > a.rec_cap || kb + B.bkb[j] > a.keys_cap || vb + B.bvb[j] > a.vals_cap)) {
+      st = MTBLX_ST_OVERFLOW;
+      B.bwr[j] = 0;
+      atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 1ull);
+    }
+    a.status[b] = st;
+  }
+}
+
+// waves 2..7: copy one tile's records (thread per record) + irregular blocks
+__device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int ct) {
+  const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
+  const uint32_t nfr = B.nfastrec, nb = B.nb;
+  for (uint32_t q = ct; q < nfr; q += kPipeCopyThreads) {
+    const uint4 rr = *reinterpret_cast<const uint4*>(&B.rec[q]);
+    const uint32_t j = rr.w >> 24;
+    if (!B.bwr[j]) continue;
+    const uint32_t bo = B.boff[j];
+    const uint32_t pos = rr.x & 0xFFFFu, shr = rr.x >> 16, ns = rr.y & 0xFFFFu, vl = rr.y >> 16;
+    const uint32_t ks = rr.z, vs = rr.w & 0xFFFFFFu;
+    const uint32_t klen = shr + ns;
+    const uint64_t gr = pr + B.brb[j] + (q - B.brf[j]);
+    a.key_end[gr] = ks + klen - B.bkbb[j];
+    a.val_end[gr] = vs + vl - B.bvbb[j];
+#ifndef MTBLX_ABL_NOVAL
+    const uint32_t vsrc = bo + pos + ns;
+    uint8_t* vd = a.vals + pv + vs;
+    for (uint32_t o = 0; o < vl; o += 16) {
+      uint4 w4 = lds_win16(B.stage, vsrc + o);
+      const uint32_t m = vl - o;
+      store_bytes(vd + o, w4, m < 16 ? m : 16);
+    }
+#endif
+#ifndef MTBLX_ABL_NOKEY
+    uint8_t* kd = a.keys + pk + ks;
+    for (uint32_t j0 = 0; j0 < klen; j0 += 16) {
+      const uint32_t jend = (j0 + 16 < klen) ? j0 + 16 : klen;
+      uint4 outw = make_uint4(0, 0, 0, 0);
+      uint32_t jj = j0;
+      while (jj < jend) {
+        // key byte jj comes from the suffix of the latest record s <= q (same interval)
+        // with shared_s <= jj
+        uint32_t sidx = q, m = klen, shs = shr, ps = pos;
+        while (shs > jj) {
+          m = shs < m ? shs : m;
+          --sidx;
+          const uint32_t x = B.rec[sidx].pos_sh;
+          shs = x >> 16;
+          ps = x & 0xFFFFu;
+        }
+        const uint32_t seg = m < jend ? m : jend;
+        const uint32_t src = bo + ps + (jj - shs);
+        uint4 w4 = lds_win16(B.stage, src - (jj - j0));
+        merge_bytes(outw, w4, (int)(jj - j0), (int)(seg - j0));
+        jj = seg;
+      }
+      store_bytes(kd + j0, outw, jend - j0);
+    }
+#endif
+  }
+  // irregular blocks: exact serial write (thread per block)
+  if (ct < (int)nb && !B.bok[ct] && B.bwr[ct]) {
+    const uint32_t j = ct, bo = B.boff[j], L = B.blen[j];
+    const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[B.b0 + j]);
+    generic_block<true>(d, L, a.keys + pk + B.bkbb[j], a.vals + pv + B.bvbb[j], a.key_end + pr + B.brb[j],
+                        a.val_end + pr + B.brb[j]);
+  }
+}
+
+__global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
+  __shared__ PipeLds S;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t g = blockIdx.x, G = gridDim.x;
+  const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
+  const int ct = tid - 2 * kWave;                                          // copy-thread index
+#ifdef MTBLX_STAMPS
+  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime(), ntl = 0;
+#define PSTAMP(k) do { if (lane == 0) { const uint64_t _t = __builtin_amdgcn_s_memtime(); tacc[k] += _t - tprev; tprev = _t; } } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#endif
+  if (tid == 0) S.staged = 0;
+  __syncthreads();
+
+  uint64_t tinc[3] = {0, 0, 0};   // wave 1 only
+  uint4 pf[kPipePf];              // copy waves: prefetched bytes of the next tile to stage
+  uint64_t pr0 = 0, pr1 = 0;
+  auto prefetch = [&](uint32_t k) {   // copy waves: load tile g + kG's range into registers
+    pr1 = 0;
+    if (k >= nloc) return;
+    tile_range(a, g + k * G, kPipeTB, pr0, pr1);
+    if (!pr1) return;
+#pragma unroll
+    for (int m = 0; m < kPipePf; ++m) {
+      const uint64_t o = pr0 + 16ull * (uint32_t)(ct + m * kPipeCopyThreads);
+      pf[m] = (o < pr1) ? load_chunk(a, o) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (wv >= 2) prefetch(0);
+
+  for (int it = -2; it < (int)nloc; ++it) {
+    // tiles of this iteration (local indices): walk 1 -> it+2, walk 2 -> it+1, copy -> it
+    if (wv >= 2) {
+      // ---- stage local tile it+2 into buf[(it+2)%3], prefetch it+3, copy tile it ----
+      const uint32_t k2 = (uint32_t)(it + 2);
+      if (k2 < nloc) {
+        PipeBuf& B = S.buf[k2 % 3];
+        const uint32_t t2 = g + k2 * G;
+        const uint32_t b0 = t2 * a.bpt, nb = min(a.bpt, a.nblk - b0);
+        if (pr1) {
+          const uint32_t nch = (uint32_t)((pr1 - pr0 + 15) >> 4);
+#pragma unroll
+          for (int m = 0; m < kPipePf; ++m) {
+            const uint32_t c = ct + m * kPipeCopyThreads;
+            if (c < nch) *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = pf[m];
+          }
+          if (ct < (int)nb) {
+            const uint64_t off = a.blk_off[b0 + ct];
+            const uint32_t L = a.blk_len[b0 + ct];
+            B.boff[ct] = (off >= pr0 && off + L <= pr1) ? (uint32_t)(16 + off - pr0) : kNotStaged;
+            B.blen[ct] = L;
+          }
+        } else {
+          for (uint32_t j = wv - 2; j < nb; j += kPipeCopyWaves) {
+            const uint32_t L = a.blk_len[b0 + j];
+            const uint64_t off = a.blk_off[b0 + j];
+            const uint32_t so = 16u + j * a.slot;
+            uint32_t bo = kNotStaged;
+            if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)kPipeTB) bo = so + stage_slot(a, B.stage + so, off, L, lane);
+            if (lane == 0) { B.boff[j] = bo; B.blen[j] = L; }
+          }
+        }
+        if (ct == 0) { B.nb = nb; B.b0 = b0; }
+        // signal wave 0: this wave's part of the tile is in LDS
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&S.staged, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prefetch(k2 + 1);
+      }
+      PSTAMP(0);
+      if (it >= 0 && a.write) pipe_copy(S.buf[it % 3], a, ct);
+      PSTAMP(1);
+    } else if (wv == 0) {
+      const uint32_t k2 = (uint32_t)(it + 2);
+      if (k2 < nloc) {
+        // wait until all copy waves staged the tile
+        const uint32_t want = (uint32_t)kPipeCopyWaves * (k2 + 1);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(&S.staged, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 24)) break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        PSTAMP(2);
+        pipe_walk1(S.buf[k2 % 3], a, g + k2 * G, lane);
+        PSTAMP(3);
+      }
+    } else {  // wave 1
+      const int k1 = it + 1;
+      if (k1 >= 0 && k1 < (int)nloc) {
+        PSTAMP(4);
+        pipe_walk2(S.buf[k1 % 3], a, g + (uint32_t)k1 * G, G, tinc, lane);
+        PSTAMP(5);
+      }
+    }
+    __syncthreads();
+#ifdef MTBLX_STAMPS
+    if (wv == 0) { PSTAMP(6); ++ntl; }
+    if (wv == 1) PSTAMP(6);
+    if (wv >= 2) PSTAMP(7);
+#endif
+  }
+#ifdef MTBLX_STAMPS
+  // per role: wave 0 -> [2]=wait staged, [3]=walk1, [6]=barrier; wave 1 -> [4] idle,[5]=walk2+lookback;
+  // wave 2 -> [0]=stage, [1]=copy, [7]=barrier.  Summed over workgroups, lane 0 of waves 0..2.
+  if (lane == 0 && a.dbg && wv <= 2) {
+    for (int k = 0; k < 8; ++k) {
+      const bool mine = (wv == 0 && (k == 2 || k == 3 || k == 6)) || (wv == 1 && (k == 4 || k == 5)) ||
+                        (wv == 2 && (k == 0 || k == 1 || k == 7));
+      if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)tacc[k]);
+    }
+    if (wv == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 8), (unsigned long long)ntl);
+  }
+#endif
+}
+
 using CfgSmall = TileCfg<32768, 640, 256, 64, true, 3>;
 using CfgLarge = TileCfg<67584, 1024, 256, 16, false, 1>;
 
@@ -900,11 +1350,11 @@ Plan make_plan(uint32_t nblk, uint32_t max_len) {
   const uint32_t slot = ((max_len + 30u) / 16u) * 16u;
   // contiguous staging: blocks + framing (<= 14 B each) + 16 B alignment + 32 B tail
   const uint32_t per = max_len + 16u;
-  uint32_t usable = CfgSmall::TB - 48;
+  uint32_t usable = kPipeTB - 48;
   if (max_len != 0 && slot <= usable) {
     p.large = false;
     p.slot = slot;
-    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, slot), CfgSmall::MAXBLK));
+    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, slot), kPipeMaxBlk));
   } else {
     usable = CfgLarge::TB - 48;
     p.large = true;
@@ -913,6 +1363,17 @@ Plan make_plan(uint32_t nblk, uint32_t max_len) {
   }
   p.ntiles = (nblk + p.bpt - 1) / p.bpt;
   return p;
+}
+
+int pipe_grid(uint32_t ntiles) {
+  static int cached = 0;
+  if (!cached) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    cached = std::max(1, std::min(ncu, kMaxLookbackLoads * kWave + 1));  // 1 workgroup per CU
+  }
+  return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
 }
 
 template <class C>
@@ -952,7 +1413,7 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
   if (p.large) {
     hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
   } else {
-    hipLaunchKernelGGL(k_decode_tiles<CfgSmall>, dim3(resident_grid<CfgSmall>(p.ntiles)), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(k_decode_pipe, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   }
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

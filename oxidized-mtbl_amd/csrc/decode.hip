@@ -900,7 +900,8 @@ constexpr int kPipeThreads = 512;
 constexpr int kPipeCopyThreads = kPipeThreads - 2 * kWave;  // waves 2..7
 constexpr int kPipeCopyWaves = kPipeCopyThreads / kWave;
 constexpr int kPipeTB = 32768;
-constexpr int kPipeMaxRec = 640;
+constexpr int kPipeMaxRec = 512;
+constexpr uint32_t kKeyInImg = 1u << 20;   // Rec.vs_blk flag: the record's key is in kimg
 constexpr int kPipeMaxInt = 256;
 constexpr int kPipeMaxBlk = 16;
 constexpr int kPipePf = (kPipeTB + 16 * kPipeCopyThreads - 1) / (16 * kPipeCopyThreads);  // uint4 per copy thread
@@ -908,6 +909,7 @@ constexpr int kPipePf = (kPipeTB + 16 * kPipeCopyThreads - 1) / (16 * kPipeCopyT
 struct alignas(16) PipeBuf {
   uint8_t stage[kPipeTB];
   Rec rec[kPipeMaxRec];
+  uint4 kimg[kPipeMaxRec];    // full key of records with key length <= 16 (walk 2)
   uint32_t boff[kPipeMaxBlk], blen[kPipeMaxBlk], bR[kPipeMaxBlk], bn[kPipeMaxBlk];
   uint32_t bok[kPipeMaxBlk], bwr[kPipeMaxBlk];
   int32_t bst[kPipeMaxBlk];
@@ -1069,6 +1071,52 @@ __device__ __forceinline__ void pipe_walk1(PipeBuf& B, const TileArgs& a, uint32
   }
 }
 
+// Walk 2 of one restart interval (regular block, 1-byte varint headers) that also
+// rebuilds keys in registers: the first 16 key bytes are kept in `key`; the suffix of
+// record r is read as a 16-byte LDS window starting sh_r bytes before the suffix, so
+// window byte j IS key byte j for j in [sh_r, klen_r) and a byte-mask merge rebuilds
+// the key (src/block.rs:134-135: key.truncate(shared); key.extend(suffix)).  Keys of
+// <= 16 bytes are written whole into kimg.  Returns false on any irregularity (then the
+// caller runs the exact walk_interval<true>, which leaves keys to the copy's walk-back).
+__device__ __forceinline__ bool walk2_keys(const uint8_t* stage, Rec* recs, uint4* kimg, uint32_t bo, uint32_t R,
+                                           uint32_t s, uint32_t e, uint32_t slot0, uint32_t kbase, uint32_t vbase,
+                                           uint32_t blk) {
+  if (!(s < e && e <= R)) return false;
+  uint32_t p = s, prevlen = 0, bad = 0, cnt = 0, kb = 0, vb = 0;
+  uint4 key = make_uint4(0, 0, 0, 0);
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
+  do {
+    const uint32_t ad = bo + p;
+    const uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
+    const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
+    const uint32_t np = p + 3u + ns + vl;
+    bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R);
+    const uint32_t klen = sh + ns;
+    // window aligned to key positions; only bytes [sh, 16) are merged, so the window is
+    // needed only when sh < 16 (then ad + 3 - sh >= bo - 12 >= 4: inside the stage)
+    if (sh < 16u) {
+      const uint4 w = lds_win16(stage, ad + 3u - sh);
+      merge_bytes(key, w, (int)sh, (int)(klen < 16u ? klen : 16u));
+    }
+    const uint32_t r = slot0 + cnt;
+    if (r < (uint32_t)kPipeMaxRec) {
+      Rec x;
+      x.pos_sh = (p + 3u) | (sh << 16);
+      x.ns_vl = ns | (vl << 16);
+      x.ks = kbase + kb;
+      x.vs_blk = (vbase + vb) | (klen <= 16u ? kKeyInImg : 0u) | (blk << 24);
+      recs[r] = x;
+      kimg[r] = key;
+    }
+    cnt += 1;
+    kb += klen;
+    vb += vl;
+    prevlen = klen;
+    p = np;
+  } while (p < e && !bad);
+  return !bad && p == e;
+}
+
 // wave 1: walk 2 (metadata), look-back, per-block outputs.  tinc = inclusive prefix of
 // this workgroup's previous tile (kept in wave 1's registers across iterations).
 __device__ __forceinline__ void pipe_walk2(PipeBuf& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3], int lane) {
@@ -1092,8 +1140,7 @@ __device__ __forceinline__ void pipe_walk2(PipeBuf& B, const TileArgs& a, uint32
       const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
       const uint32_t kin = B.ikb[f] - B.ikb[fj], vin = B.ivb[f] - B.ivb[fj];
       uint32_t c, k, v;
-      if (!walk_fast<true>(B.stage, B.rec, bo, R, s, e, c, k, v, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j, 0,
-                           kPipeMaxRec))
+      if (!walk2_keys(B.stage, B.rec, B.kimg, bo, R, s, e, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j))
         walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, c, k, v, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j, 0,
                             kPipeMaxRec);
     }
@@ -1163,7 +1210,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, i
     if (!B.bwr[j]) continue;
     const uint32_t bo = B.boff[j];
     const uint32_t pos = rr.x & 0xFFFFu, shr = rr.x >> 16, ns = rr.y & 0xFFFFu, vl = rr.y >> 16;
-    const uint32_t ks = rr.z, vs = rr.w & 0xFFFFFFu;
+    const uint32_t ks = rr.z, vs = rr.w & 0xFFFFFu;
     const uint32_t klen = shr + ns;
     const uint64_t gr = pr + B.brb[j] + (q - B.brf[j]);
     a.key_end[gr] = ks + klen - B.bkbb[j];
@@ -1179,6 +1226,10 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, i
 #endif
 #ifndef MTBLX_ABL_NOKEY
     uint8_t* kd = a.keys + pk + ks;
+    if (rr.w & kKeyInImg) {  // whole key rebuilt by walk 2
+      store_bytes(kd, B.kimg[q], klen);
+      continue;
+    }
     for (uint32_t j0 = 0; j0 < klen; j0 += 16) {
       const uint32_t jend = (j0 + 16 < klen) ? j0 + 16 : klen;
       uint4 outw = make_uint4(0, 0, 0, 0);
@@ -1227,6 +1278,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
 #endif
   if (tid == 0) S.staged = 0;
   __syncthreads();
+  // the walks are serial latency chains: let them issue ahead of the copy waves
+  if (wv < 2) __builtin_amdgcn_s_setprio(2);
 
   uint64_t tinc[3] = {0, 0, 0};   // wave 1 only
   uint4 pf[kPipePf];              // copy waves: prefetched bytes of the next tile to stage

@@ -193,8 +193,8 @@ def main():
     }
     if args.stamps:
         d = ws.buf[:72].cpu().numpy().view(np.uint64).astype(np.float64)
-        names = ["w2-7:stage", "w2-7:copy", "w0:wait-staged", "w0:walk1", "w1:-", "w1:walk2+lookback",
-                 "w0:barrier", "w2-7:barrier"]
+        names = ["w1:stage", "w1:lookback", "w0:wait-staged", "w0:walk", "-", "w1:barrier", "w0:barrier",
+                 "w1:copy"]
         ntl = max(d[8], 1)
         res["phase_cycles_per_tile"] = {n: round(d[k] / ntl, 1) for k, n in enumerate(names)}
         res["stamps_note"] = "diagnostic build (s_memtime, thread 0 of each workgroup), last step only; shares, not time"

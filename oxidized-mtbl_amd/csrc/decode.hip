@@ -883,63 +883,114 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 // ----------------------------------------------------------------------------------
 // software-pipelined decoder for small blocks (k_decode_pipe)
 // ----------------------------------------------------------------------------------
-// One 512-thread workgroup per CU, persistent, static round-robin over tiles (t = g + kG).
-// A ring of three tile buffers in LDS holds three tiles in flight.  In iteration i:
-//   wave 0      : walk 1 of tile i+2 (counts), interval scan, block totals, publish A
-//   wave 1      : walk 2 of tile i+1 (per-record metadata), look-back -> prefix,
-//                 per-block outputs (nrec, bases, status)
-//   waves 2..7  : stage tile i+2 (from registers loaded during the previous iteration),
-//                 prefetch tile i+3 into registers, copy tile i (keys, values, ends)
+// One 512-thread workgroup per CU, persistent, static round-robin over tiles
+// (t = g + kG).  Two tile buffers in LDS.  Iteration i:
+//   wave 0      : walk of tile i+1 -- ONE pass per restart interval that counts AND
+//                 writes per-record metadata + rebuilt keys (<= 16 B) into
+//                 provisional slots (interval f, entry k -> slot 16 f + k); interval
+//                 scan; block totals; publish the tile aggregate A
+//   waves 1..7  : stage tile i+1 (registers prefetched during iteration i-1), signal
+//                 wave 0, prefetch tile i+2; wave 1 computes the look-back of tile i
+//                 (aggregates other workgroups published one iteration earlier) and the
+//                 per-block outputs; then all seven waves copy tile i
 //   __syncthreads
-// The serial, latency-bound walks run beside the bandwidth-bound copy instead of in
-// front of it, and the look-back of tile i+1 reads aggregates that the other
-// workgroups published an iteration earlier, so in steady state nothing waits.
-// Wave 0 starts walk 1 only after waves 2..7 signal (LDS counter) that the tile is
-// staged.
+// Restart intervals of more than 16 entries (the reference default is 16,
+// src/lib.rs:4) or tiles of more than kP2MaxInt intervals take the exact generic
+// path for the affected blocks.
 constexpr int kPipeThreads = 512;
-constexpr int kPipeCopyThreads = kPipeThreads - 2 * kWave;  // waves 2..7
+constexpr int kPipeCopyThreads = kPipeThreads - kWave;   // waves 1..7
 constexpr int kPipeCopyWaves = kPipeCopyThreads / kWave;
-constexpr int kPipeTB = 32768;
-constexpr int kPipeMaxRec = 512;
-constexpr uint32_t kKeyInImg = 1u << 20;   // Rec.vs_blk flag: the record's key is in kimg
-constexpr int kPipeMaxInt = 256;
+constexpr int kPipeTB = 49152;
+constexpr int kP2Spi = 16;                                // slots per interval
+constexpr int kP2MaxInt = 56;
+constexpr int kP2Slots = kP2MaxInt * kP2Spi;
 constexpr int kPipeMaxBlk = 16;
-constexpr int kPipePf = (kPipeTB + 16 * kPipeCopyThreads - 1) / (16 * kPipeCopyThreads);  // uint4 per copy thread
+constexpr int kPipePf = (kPipeTB + 16 * kPipeCopyThreads - 1) / (16 * kPipeCopyThreads);  // uint4 per thread
+constexpr uint32_t kKeyInImg = 1u << 20;   // Rec.vs_blk flag: the record's key is in kimg
 
 struct alignas(16) PipeBuf {
   uint8_t stage[kPipeTB];
-  Rec rec[kPipeMaxRec];
-  uint4 kimg[kPipeMaxRec];    // full key of records with key length <= 16 (walk 2)
+  Rec rec[kP2Slots];          // ks / vs interval-relative
+  uint4 kimg[kP2Slots];       // full key of entries with key length <= 16
   uint32_t boff[kPipeMaxBlk], blen[kPipeMaxBlk], bR[kPipeMaxBlk], bn[kPipeMaxBlk];
   uint32_t bok[kPipeMaxBlk], bwr[kPipeMaxBlk];
   int32_t bst[kPipeMaxBlk];
   uint32_t bcnt[kPipeMaxBlk], bkb[kPipeMaxBlk], bvb[kPipeMaxBlk];
-  uint32_t brb[kPipeMaxBlk], bkbb[kPipeMaxBlk], bvbb[kPipeMaxBlk], brf[kPipeMaxBlk];
+  uint32_t brb[kPipeMaxBlk], bkbb[kPipeMaxBlk], bvbb[kPipeMaxBlk];
   uint32_t bint0[kPipeMaxBlk + 1];
-  uint32_t icnt[kPipeMaxInt + 1], ikb[kPipeMaxInt + 1], ivb[kPipeMaxInt + 1];
-  uint8_t iblk[kPipeMaxInt];
+  // per interval: raw counts after the walk; after the scan, tile-relative bases
+  uint32_t icnt[kP2MaxInt + 1], ikb[kP2MaxInt + 1], ivb[kP2MaxInt + 1];
+  uint8_t iraw[kP2MaxInt];    // entries of the interval (<= 16)
+  uint8_t iblk[kP2MaxInt];
   uint64_t tpre[3];
   uint32_t ttot[3];
-  uint32_t nfastrec, nb, b0;
+  uint32_t nb, b0, nint;
 };
 
 struct alignas(16) PipeLds {
-  PipeBuf buf[3];
-  uint32_t staged;  // waves 2..7 increment after staging a tile (wave 0 waits on it)
+  PipeBuf buf[2];
+  uint32_t staged;   // copy waves increment after staging a tile (wave 0 waits on it)
+  uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
 };
 
-// interval -> block of the tile (<= kPipeMaxBlk blocks, linear search)
-__device__ __forceinline__ uint32_t pipe_block_of(const PipeBuf& B, uint32_t f) {
-  uint32_t j = 0;
-  while (B.bint0[j + 1] <= f) ++j;
-  return j;
+// One pass over restart interval [s, e): counts, per-entry metadata into slots
+// slot0 + k (k < 16), and keys rebuilt in registers (first 16 bytes; src/block.rs:134-135
+// key.truncate(shared) + key.extend(suffix): the 16-byte LDS window starting sh bytes
+// before the suffix has key byte j at window byte j).  The next header's LDS read is
+// issued before this entry's window/merge/stores, so the loop-carried chain is one LDS
+// round trip.  1-byte-varint headers only; false on anything else (the caller then runs
+// the exact walk_interval).
+__device__ __forceinline__ bool walk_slots(const uint8_t* stage, Rec* recs, uint4* kimg, uint32_t bo, uint32_t R,
+                                           uint32_t s, uint32_t e, uint32_t slot0, uint32_t& cnt, uint32_t& kb,
+                                           uint32_t& vb) {
+  cnt = kb = vb = 0;
+  if (!(s < e && e <= R)) return false;
+  uint32_t p = s, prevlen = 0, bad = 0;
+  uint4 key = make_uint4(0, 0, 0, 0);
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
+  uint32_t ad = bo + p;
+  uint32_t w0 = st32[ad >> 2], w1 = st32[(ad >> 2) + 1];
+  do {
+    const uint32_t hw = __builtin_amdgcn_alignbit(w1, w0, (ad & 3u) * 8u);
+    const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
+    const uint32_t np = p + 3u + ns + vl;
+    bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R) | (uint32_t)(cnt >= (uint32_t)kP2Spi);
+    // issue the next header read now (np <= R + 3 + 254 stays inside the stage buffer:
+    // bo + R <= TB - 48 and the read is only consumed if np < e <= R)
+    const uint32_t nad = bo + (np < e ? np : p);
+    const uint32_t n0 = st32[nad >> 2], n1 = st32[(nad >> 2) + 1];
+    const uint32_t klen = sh + ns;
+    if (sh < 16u) {
+      const uint4 w = lds_win16(stage, ad + 3u - sh);
+      merge_bytes(key, w, (int)sh, (int)(klen < 16u ? klen : 16u));
+    }
+    if (!bad) {
+      const uint32_t r = slot0 + cnt;
+      Rec x;
+      x.pos_sh = (p + 3u) | (sh << 16);
+      x.ns_vl = ns | (vl << 16);
+      x.ks = kb;
+      x.vs_blk = vb | (klen <= 16u ? kKeyInImg : 0u);
+      recs[r] = x;
+      kimg[r] = key;
+    }
+    cnt += 1;
+    kb += klen;
+    vb += vl;
+    prevlen = klen;
+    p = np;
+    ad = nad;
+    w0 = n0;
+    w1 = n1;
+  } while (p < e && !bad);
+  return !bad && p == e;
 }
 
-// wave 0: trailers, walk 1, irregular counts, interval scan, block totals, publish A(t)
-__device__ __forceinline__ void pipe_walk1(PipeBuf& B, const TileArgs& a, uint32_t t, int lane) {
+// wave 0: trailers, walk (metadata + keys into slots), irregular counts, interval scan,
+// block totals, publish A(t)
+__device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_t t, int lane) {
   const uint32_t nb = B.nb, b0 = B.b0;
-  // trailers (Block::init, src/block.rs:16-49)
-  {
+  {  // trailers (Block::init, src/block.rs:16-49) + interval numbering
     uint32_t n = 0, R = 0, ok = 0;
     if (lane < (int)nb) {
       const uint32_t L = B.blen[lane], bo = B.boff[lane];
@@ -949,117 +1000,75 @@ __device__ __forceinline__ void pipe_walk1(PipeBuf& B, const TileArgs& a, uint32
       }
     }
     uint32_t incl = wave_incl_scan(ok ? n : 0u);
-    if (ok && incl > (uint32_t)kPipeMaxInt) ok = 0;
+    if (ok && incl > (uint32_t)kP2MaxInt) ok = 0;
     n = ok ? n : 0;
     incl = wave_incl_scan(n);
     if (lane < (int)nb) {
       B.bn[lane] = n; B.bR[lane] = R; B.bok[lane] = ok; B.bwr[lane] = 1; B.bst[lane] = MTBLX_ST_OK;
       B.bint0[lane] = incl - n;
     }
-    if (lane == (int)nb - 1) B.bint0[nb] = incl;
+    if (lane == (int)nb - 1) { B.bint0[nb] = incl; B.nint = incl; }
   }
   wave_sync();
-  const uint32_t nint = B.bint0[nb];
-  // walk 1: one lane per restart interval
-  for (uint32_t f = lane; f < nint; f += kWave) {
-    const uint32_t j = pipe_block_of(B, f);
+  const uint32_t nint = B.nint;
+  // walk: one lane per restart interval (nint <= kP2MaxInt <= 64)
+  uint32_t cnt = 0, kb = 0, vb = 0, jf = 0;
+  if (lane < (int)nint) {
+    const uint32_t f = lane;
+    uint32_t j = 0;
+    while (B.bint0[j + 1] <= f) ++j;
+    jf = j;
     const uint32_t i = f - B.bint0[j], bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
     const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
     const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
-    uint32_t cnt, kb, vb;
-    bool ok = walk_fast<false>(B.stage, B.rec, bo, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
-    if (!ok) ok = walk_interval<false>(B.stage, B.rec, bo, L, R, s, e, cnt, kb, vb, 0, 0, 0, 0, 0, 0);
-    B.icnt[f] = cnt; B.ikb[f] = kb; B.ivb[f] = vb; B.iblk[f] = (uint8_t)j;
+    const uint32_t slot0 = f * kP2Spi;
+    bool ok = walk_slots(B.stage, B.rec, B.kimg, bo, R, s, e, slot0, cnt, kb, vb);
+    if (!ok) {
+      ok = walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, cnt, kb, vb, slot0, 0, 0, 0, slot0, slot0 + kP2Spi);
+      ok = ok && cnt <= (uint32_t)kP2Spi;
+    }
+    B.iraw[f] = (uint8_t)(cnt < 255u ? cnt : 255u);
+    B.iblk[f] = (uint8_t)j;
     if (!ok) B.bok[j] = 0;
   }
   wave_sync();
-  for (int pass = 0; pass < 2; ++pass) {
-    // irregular blocks: exact serial count (generic path, lane per block)
-    if (lane < (int)nb && !B.bok[lane] && (pass == 0 || B.bst[lane] == -1)) {
-      const uint32_t j = lane, bo = B.boff[j], L = B.blen[j];
-      const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + j]);
-      GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
-      B.bcnt[j] = o.nrec; B.bkb[j] = (uint32_t)o.kb; B.bvb[j] = (uint32_t)o.vb; B.bst[j] = o.st;
-    }
-    wave_sync();
-    // interval scan over regular blocks: lane l owns intervals [l*k, (l+1)*k)
-    const uint32_t k = (nint + kWave - 1) / kWave;
-    uint32_t c = 0, kk = 0, v = 0;
-    for (uint32_t q = 0; q < k; ++q) {
-      const uint32_t f = lane * k + q;
-      if (f < nint && B.bok[B.iblk[f]]) { c += B.icnt[f]; kk += B.ikb[f]; v += B.ivb[f]; }
-    }
-    const uint32_t ic = wave_incl_scan(c), ik = wave_incl_scan(kk), iv = wave_incl_scan(v);
-    uint32_t rc = ic - c, rk = ik - kk, rv = iv - v;
-    for (uint32_t q = 0; q < k; ++q) {
-      const uint32_t f = lane * k + q;
-      if (f < nint) {
-        const bool reg = B.bok[B.iblk[f]] != 0;
-        const uint32_t x = reg ? B.icnt[f] : 0u, y = reg ? B.ikb[f] : 0u, z = reg ? B.ivb[f] : 0u;
-        B.icnt[f] = rc; B.ikb[f] = rk; B.ivb[f] = rv;
-        rc += x; rk += y; rv += z;
-      }
-    }
-    const uint32_t totr = (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
-    if (lane == 0) {
-      B.icnt[nint] = totr;
-      B.ikb[nint] = (uint32_t)__builtin_amdgcn_readlane((int)ik, 63);
-      B.ivb[nint] = (uint32_t)__builtin_amdgcn_readlane((int)iv, 63);
-      B.nfastrec = totr;
-    }
-    wave_sync();
-    if (totr <= (uint32_t)kPipeMaxRec || pass == 1) break;
-    // too many regular records for the metadata array: demote trailing blocks to the
-    // generic path (rare: tiny records), restore their interval counts for the re-scan
-    // is unnecessary (demoted intervals are skipped), then count them serially
-    uint32_t keep = 0;
-    if (lane < (int)nb && B.bok[lane]) {
-      const uint32_t end = B.icnt[B.bint0[lane + 1]];
-      keep = end <= (uint32_t)kPipeMaxRec;
-    } else if (lane < (int)nb) {
-      keep = 1;
-    }
-    // a block is kept only if every earlier regular block is kept too (prefix property)
-    const uint64_t drop = __ballot(lane < (int)nb && !keep);
-    if (lane < (int)nb && drop) {
-      const int first = __builtin_ctzll(drop);
-      if (lane >= first && B.bok[lane]) { B.bok[lane] = 0; B.bst[lane] = -1; }
-    }
-    // restore raw interval counts for the re-scan: re-walk (counts only) is simplest
-    wave_sync();
-    for (uint32_t f = lane; f < nint; f += kWave) {
-      const uint32_t j = B.iblk[f];
-      if (!B.bok[j]) continue;
-      const uint32_t i = f - B.bint0[j], bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
-      const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
-      const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
-      uint32_t cnt, kb2, vb2;
-      if (!walk_fast<false>(B.stage, B.rec, bo, R, s, e, cnt, kb2, vb2, 0, 0, 0, 0, 0, 0))
-        walk_interval<false>(B.stage, B.rec, bo, L, R, s, e, cnt, kb2, vb2, 0, 0, 0, 0, 0, 0);
-      B.icnt[f] = cnt; B.ikb[f] = kb2; B.ivb[f] = vb2;
-    }
-    wave_sync();
+  // irregular blocks: exact serial count (generic path, lane per block)
+  if (lane < (int)nb && !B.bok[lane]) {
+    const uint32_t j = lane, bo = B.boff[j], L = B.blen[j];
+    const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + j]);
+    GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
+    B.bcnt[j] = o.nrec; B.bkb[j] = (uint32_t)o.kb; B.bvb[j] = (uint32_t)o.vb; B.bst[j] = o.st;
   }
-  // block totals + tile-relative block bases
+  wave_sync();
+  // interval scan over regular blocks (one interval per lane)
+  const bool reg = lane < (int)nint && B.bok[jf];
+  const uint32_t c = reg ? cnt : 0u, k = reg ? kb : 0u, v = reg ? vb : 0u;
+  const uint32_t ic = wave_incl_scan(c), ik = wave_incl_scan(k), iv = wave_incl_scan(v);
+  // block totals (regular: differences of the interval scan) -> block bases.
+  // Cross-lane reads are done by every lane (uniform control flow), results used after.
   {
-    uint32_t c = 0, k = 0, v = 0, rf = 0;
+    const uint32_t fa = lane < (int)nb ? B.bint0[lane] : 0u, fb = lane < (int)nb ? B.bint0[lane + 1] : 0u;
+    const int sa = fa ? (int)fa - 1 : 0, sb = fb ? (int)fb - 1 : 0;
+    const uint32_t ea = fa ? (uint32_t)__shfl(ic, sa, kWave) : 0u, eb0 = (uint32_t)__shfl(ic, sb, kWave);
+    const uint32_t ka = fa ? (uint32_t)__shfl(ik, sa, kWave) : 0u, kb0 = (uint32_t)__shfl(ik, sb, kWave);
+    const uint32_t va = fa ? (uint32_t)__shfl(iv, sa, kWave) : 0u, vb0 = (uint32_t)__shfl(iv, sb, kWave);
+    const uint32_t eb = fb ? eb0 : 0u, kb2 = fb ? kb0 : 0u, vb2 = fb ? vb0 : 0u;
+    uint32_t bc = 0, bk = 0, bv = 0;
     if (lane < (int)nb) {
-      const uint32_t fa = B.bint0[lane], fb = B.bint0[lane + 1];
-      rf = B.icnt[fa];
       if (B.bok[lane]) {
-        c = B.icnt[fb] - B.icnt[fa]; k = B.ikb[fb] - B.ikb[fa]; v = B.ivb[fb] - B.ivb[fa];
+        bc = eb - ea; bk = kb2 - ka; bv = vb2 - va;
       } else {
-        c = B.bcnt[lane]; k = B.bkb[lane]; v = B.bvb[lane];
+        bc = B.bcnt[lane]; bk = B.bkb[lane]; bv = B.bvb[lane];
       }
     }
-    const uint32_t ic = wave_incl_scan(c), ik = wave_incl_scan(k), iv = wave_incl_scan(v);
+    const uint32_t jc = wave_incl_scan(bc), jk = wave_incl_scan(bk), jv = wave_incl_scan(bv);
     if (lane < (int)nb) {
-      B.bcnt[lane] = c; B.bkb[lane] = k; B.bvb[lane] = v;
-      B.brb[lane] = ic - c; B.bkbb[lane] = ik - k; B.bvbb[lane] = iv - v; B.brf[lane] = rf;
+      B.bcnt[lane] = bc; B.bkb[lane] = bk; B.bvb[lane] = bv;
+      B.brb[lane] = jc - bc; B.bkbb[lane] = jk - bk; B.bvbb[lane] = jv - bv;
     }
-    const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane((int)ic, (int)nb - 1);
-    const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)ik, (int)nb - 1);
-    const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)iv, (int)nb - 1);
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane((int)jc, (int)nb - 1);
+    const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)jk, (int)nb - 1);
+    const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)jv, (int)nb - 1);
     if (lane == 0) {
       B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
       if (tk >= kField) {
@@ -1069,105 +1078,51 @@ __device__ __forceinline__ void pipe_walk1(PipeBuf& B, const TileArgs& a, uint32
       __hip_atomic_store(&a.lb[t], pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  wave_sync();
+  // tile-relative interval bases (record index, key byte, value byte)
+  {
+    const uint32_t fa = lane < (int)nint ? B.bint0[jf] : 0u;
+    const int sa = fa ? (int)fa - 1 : 0;
+    const uint32_t e0r = (uint32_t)__shfl(ic, sa, kWave), k0r = (uint32_t)__shfl(ik, sa, kWave),
+                   v0r = (uint32_t)__shfl(iv, sa, kWave);
+    if (lane < (int)nint) {
+      const uint32_t j = jf;
+      const uint32_t e0 = fa ? e0r : 0u, k0 = fa ? k0r : 0u, v0 = fa ? v0r : 0u;
+      B.icnt[lane] = B.brb[j] + (ic - c) - e0;
+      B.ikb[lane] = B.bkbb[j] + (ik - k) - k0;
+      B.ivb[lane] = B.bvbb[j] + (iv - v) - v0;
+    }
+  }
 }
 
-// Walk 2 of one restart interval (regular block, 1-byte varint headers) that also
-// rebuilds keys in registers: the first 16 key bytes are kept in `key`; the suffix of
-// record r is read as a 16-byte LDS window starting sh_r bytes before the suffix, so
-// window byte j IS key byte j for j in [sh_r, klen_r) and a byte-mask merge rebuilds
-// the key (src/block.rs:134-135: key.truncate(shared); key.extend(suffix)).  Keys of
-// <= 16 bytes are written whole into kimg.  Returns false on any irregularity (then the
-// caller runs the exact walk_interval<true>, which leaves keys to the copy's walk-back).
-__device__ __forceinline__ bool walk2_keys(const uint8_t* stage, Rec* recs, uint4* kimg, uint32_t bo, uint32_t R,
-                                           uint32_t s, uint32_t e, uint32_t slot0, uint32_t kbase, uint32_t vbase,
-                                           uint32_t blk) {
-  if (!(s < e && e <= R)) return false;
-  uint32_t p = s, prevlen = 0, bad = 0, cnt = 0, kb = 0, vb = 0;
-  uint4 key = make_uint4(0, 0, 0, 0);
-  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
-  do {
-    const uint32_t ad = bo + p;
-    const uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
-    const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
-    const uint32_t np = p + 3u + ns + vl;
-    bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R);
-    const uint32_t klen = sh + ns;
-    // window aligned to key positions; only bytes [sh, 16) are merged, so the window is
-    // needed only when sh < 16 (then ad + 3 - sh >= bo - 12 >= 4: inside the stage)
-    if (sh < 16u) {
-      const uint4 w = lds_win16(stage, ad + 3u - sh);
-      merge_bytes(key, w, (int)sh, (int)(klen < 16u ? klen : 16u));
-    }
-    const uint32_t r = slot0 + cnt;
-    if (r < (uint32_t)kPipeMaxRec) {
-      Rec x;
-      x.pos_sh = (p + 3u) | (sh << 16);
-      x.ns_vl = ns | (vl << 16);
-      x.ks = kbase + kb;
-      x.vs_blk = (vbase + vb) | (klen <= 16u ? kKeyInImg : 0u) | (blk << 24);
-      recs[r] = x;
-      kimg[r] = key;
-    }
-    cnt += 1;
-    kb += klen;
-    vb += vl;
-    prevlen = klen;
-    p = np;
-  } while (p < e && !bad);
-  return !bad && p == e;
-}
-
-// wave 1: walk 2 (metadata), look-back, per-block outputs.  tinc = inclusive prefix of
-// this workgroup's previous tile (kept in wave 1's registers across iterations).
-__device__ __forceinline__ void pipe_walk2(PipeBuf& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3], int lane) {
-  const uint32_t nb = B.nb, b0 = B.b0, nint = B.bint0[nb];
-  // issue the look-back loads first (window [lo, t) of other workgroups' aggregates)
+// wave 1: look-back of tile t (aggregates published by the other workgroups one
+// iteration earlier) + per-block outputs.  tinc = inclusive prefix of this workgroup's
+// previous tile (wave 1 registers).
+__device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3],
+                                              int lane) {
+  const uint32_t nb = B.nb, b0 = B.b0;
   const uint32_t lo = (t >= G) ? t - G + 1 : 0;
-  uint64_t lw[kMaxLookbackLoads];
-#pragma unroll
-  for (int m = 0; m < kMaxLookbackLoads; ++m) {
-    const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
-    lw[m] = kReady;
-    if (i >= (int64_t)lo) lw[m] = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (a.write) {
-    for (uint32_t f = lane; f < nint; f += kWave) {
-      const uint32_t j = B.iblk[f];
-      if (!B.bok[j]) continue;
-      const uint32_t fj = B.bint0[j];
-      const uint32_t i = f - fj, bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
-      const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
-      const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
-      const uint32_t kin = B.ikb[f] - B.ikb[fj], vin = B.ivb[f] - B.ivb[fj];
-      uint32_t c, k, v;
-      if (!walk2_keys(B.stage, B.rec, B.kimg, bo, R, s, e, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j))
-        walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, c, k, v, B.icnt[f], B.bkbb[j] + kin, B.bvbb[j] + vin, j, 0,
-                            kPipeMaxRec);
-    }
-  }
-  // finish the look-back
   uint64_t sr = 0, sk = 0, sv = 0;
   bool timeout = false;
 #pragma unroll
   for (int m = 0; m < kMaxLookbackLoads; ++m) {
     const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
-    uint64_t w = lw[m];
+    if (i < (int64_t)lo) continue;
+    uint64_t w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t spins = 0;
     while (!(w & kReady)) {
       __builtin_amdgcn_s_sleep(2);
       w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (++spins > (1u << 22)) { timeout = true; w = kReady; }
     }
-    if (i >= (int64_t)lo) {
-      sr += (w >> 42) & kField;
-      sv += (w >> 21) & kField;
-      uint64_t kk = w & kField;
-      if (kk == kField) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        kk = __hip_atomic_load(&a.lbx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      sk += kk;
+    sr += (w >> 42) & kField;
+    sv += (w >> 21) & kField;
+    uint64_t kk = w & kField;
+    if (kk == kField) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      kk = __hip_atomic_load(&a.lbx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    sk += kk;
   }
   if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 2ull);
   sr = wave_sum32((uint32_t)sr);
@@ -1182,7 +1137,6 @@ __device__ __forceinline__ void pipe_walk2(PipeBuf& B, const TileArgs& a, uint32
     B.tpre[0] = pr; B.tpre[1] = pk; B.tpre[2] = pv;
     if (t == a.ntiles - 1) { a.totals[0] = tinc[0]; a.totals[1] = tinc[1]; a.totals[2] = tinc[2]; }
   }
-  // per-block outputs + capacity check
   if (lane < (int)nb) {
     const uint32_t j = lane, b = b0 + j;
     const uint64_t rb = pr + B.brb[j], kb = pk + B.bkbb[j], vb = pv + B.bvbb[j];
@@ -1200,19 +1154,21 @@ __device__ __forceinline__ void pipe_walk2(PipeBuf& B, const TileArgs& a, uint32
   }
 }
 
-// waves 2..7: copy one tile's records (thread per record) + irregular blocks
+// waves 1..7: copy one tile (thread per slot) + irregular blocks
 __device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int ct) {
   const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
-  const uint32_t nfr = B.nfastrec, nb = B.nb;
-  for (uint32_t q = ct; q < nfr; q += kPipeCopyThreads) {
+  const uint32_t nint = B.nint, nb = B.nb;
+  for (uint32_t q = ct; q < nint * kP2Spi; q += kPipeCopyThreads) {
+    const uint32_t f = q / kP2Spi, kq = q % kP2Spi;
+    if (kq >= B.iraw[f]) continue;
+    const uint32_t j = B.iblk[f];
+    if (!B.bok[j] || !B.bwr[j]) continue;
     const uint4 rr = *reinterpret_cast<const uint4*>(&B.rec[q]);
-    const uint32_t j = rr.w >> 24;
-    if (!B.bwr[j]) continue;
     const uint32_t bo = B.boff[j];
     const uint32_t pos = rr.x & 0xFFFFu, shr = rr.x >> 16, ns = rr.y & 0xFFFFu, vl = rr.y >> 16;
-    const uint32_t ks = rr.z, vs = rr.w & 0xFFFFFu;
+    const uint32_t ks = B.ikb[f] + rr.z, vs = B.ivb[f] + (rr.w & 0xFFFFFu);
     const uint32_t klen = shr + ns;
-    const uint64_t gr = pr + B.brb[j] + (q - B.brf[j]);
+    const uint64_t gr = pr + B.icnt[f] + kq;
     a.key_end[gr] = ks + klen - B.bkbb[j];
     a.val_end[gr] = vs + vl - B.bvbb[j];
 #ifndef MTBLX_ABL_NOVAL
@@ -1226,7 +1182,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, i
 #endif
 #ifndef MTBLX_ABL_NOKEY
     uint8_t* kd = a.keys + pk + ks;
-    if (rr.w & kKeyInImg) {  // whole key rebuilt by walk 2
+    if (rr.w & kKeyInImg) {  // whole key rebuilt by the walk
       store_bytes(kd, B.kimg[q], klen);
       continue;
     }
@@ -1235,8 +1191,8 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, i
       uint4 outw = make_uint4(0, 0, 0, 0);
       uint32_t jj = j0;
       while (jj < jend) {
-        // key byte jj comes from the suffix of the latest record s <= q (same interval)
-        // with shared_s <= jj
+        // key byte jj comes from the suffix of the latest entry s <= q of the same
+        // interval (slots are contiguous per interval) with shared_s <= jj
         uint32_t sidx = q, m = klen, shs = shr, ps = pos;
         while (shs > jj) {
           m = shs < m ? shs : m;
@@ -1269,22 +1225,21 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t g = blockIdx.x, G = gridDim.x;
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
-  const int ct = tid - 2 * kWave;                                          // copy-thread index
+  const int ct = tid - kWave;                                              // copy-thread index
 #ifdef MTBLX_STAMPS
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime(), ntl = 0;
 #define PSTAMP(k) do { if (lane == 0) { const uint64_t _t = __builtin_amdgcn_s_memtime(); tacc[k] += _t - tprev; tprev = _t; } } while (0)
 #else
 #define PSTAMP(k) do { } while (0)
 #endif
-  if (tid == 0) S.staged = 0;
+  if (tid == 0) { S.staged = 0; S.ready = 0; }
   __syncthreads();
-  // the walks are serial latency chains: let them issue ahead of the copy waves
-  if (wv < 2) __builtin_amdgcn_s_setprio(2);
+  if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
 
   uint64_t tinc[3] = {0, 0, 0};   // wave 1 only
   uint4 pf[kPipePf];              // copy waves: prefetched bytes of the next tile to stage
   uint64_t pr0 = 0, pr1 = 0;
-  auto prefetch = [&](uint32_t k) {   // copy waves: load tile g + kG's range into registers
+  auto prefetch = [&](uint32_t k) {
     pr1 = 0;
     if (k >= nloc) return;
     tile_range(a, g + k * G, kPipeTB, pr0, pr1);
@@ -1295,17 +1250,16 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       pf[m] = (o < pr1) ? load_chunk(a, o) : make_uint4(0, 0, 0, 0);
     }
   };
-  if (wv >= 2) prefetch(0);
+  if (wv >= 1) prefetch(0);
 
-  for (int it = -2; it < (int)nloc; ++it) {
-    // tiles of this iteration (local indices): walk 1 -> it+2, walk 2 -> it+1, copy -> it
-    if (wv >= 2) {
-      // ---- stage local tile it+2 into buf[(it+2)%3], prefetch it+3, copy tile it ----
-      const uint32_t k2 = (uint32_t)(it + 2);
-      if (k2 < nloc) {
-        PipeBuf& B = S.buf[k2 % 3];
-        const uint32_t t2 = g + k2 * G;
-        const uint32_t b0 = t2 * a.bpt, nb = min(a.bpt, a.nblk - b0);
+  for (int it = -1; it < (int)nloc; ++it) {
+    const uint32_t k1 = (uint32_t)(it + 1);   // tile to stage + walk
+    if (wv >= 1) {
+      // ---- stage local tile it+1 into buf[(it+1)&1], prefetch it+2 ----
+      if (k1 < nloc) {
+        PipeBuf& B = S.buf[k1 & 1];
+        const uint32_t t1 = g + k1 * G;
+        const uint32_t b0 = t1 * a.bpt, nb = min(a.bpt, a.nblk - b0);
         if (pr1) {
           const uint32_t nch = (uint32_t)((pr1 - pr0 + 15) >> 4);
 #pragma unroll
@@ -1320,7 +1274,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
             B.blen[ct] = L;
           }
         } else {
-          for (uint32_t j = wv - 2; j < nb; j += kPipeCopyWaves) {
+          for (uint32_t j = wv - 1; j < nb; j += kPipeCopyWaves) {
             const uint32_t L = a.blk_len[b0 + j];
             const uint64_t off = a.blk_off[b0 + j];
             const uint32_t so = 16u + j * a.slot;
@@ -1330,19 +1284,33 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           }
         }
         if (ct == 0) { B.nb = nb; B.b0 = b0; }
-        // signal wave 0: this wave's part of the tile is in LDS
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_fetch_add(&S.staged, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        prefetch(k2 + 1);
+        prefetch(k1 + 1);
       }
       PSTAMP(0);
-      if (it >= 0 && a.write) pipe_copy(S.buf[it % 3], a, ct);
-      PSTAMP(1);
-    } else if (wv == 0) {
-      const uint32_t k2 = (uint32_t)(it + 2);
-      if (k2 < nloc) {
-        // wait until all copy waves staged the tile
-        const uint32_t want = (uint32_t)kPipeCopyWaves * (k2 + 1);
+      if (it >= 0) {
+        PipeBuf& C = S.buf[it & 1];
+        const uint32_t tc = g + (uint32_t)it * G;
+        if (wv == 1) {
+          pipe_lookback(C, a, tc, G, tinc, lane);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_store(&S.ready, (uint32_t)it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          uint32_t spins = 0;
+          while (__hip_atomic_load(&S.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)it + 1) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) break;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        PSTAMP(1);
+        if (a.write) pipe_copy(C, a, ct);
+        PSTAMP(7);
+      }
+    } else {  // wave 0
+      if (k1 < nloc) {
+        const uint32_t want = (uint32_t)kPipeCopyWaves * (k1 + 1);
         uint32_t spins = 0;
         while (__hip_atomic_load(&S.staged, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
           __builtin_amdgcn_s_sleep(1);
@@ -1350,31 +1318,22 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         PSTAMP(2);
-        pipe_walk1(S.buf[k2 % 3], a, g + k2 * G, lane);
+        pipe_walk(S.buf[k1 & 1], a, g + k1 * G, lane);
         PSTAMP(3);
-      }
-    } else {  // wave 1
-      const int k1 = it + 1;
-      if (k1 >= 0 && k1 < (int)nloc) {
-        PSTAMP(4);
-        pipe_walk2(S.buf[k1 % 3], a, g + (uint32_t)k1 * G, G, tinc, lane);
-        PSTAMP(5);
       }
     }
     __syncthreads();
 #ifdef MTBLX_STAMPS
     if (wv == 0) { PSTAMP(6); ++ntl; }
-    if (wv == 1) PSTAMP(6);
-    if (wv >= 2) PSTAMP(7);
+    else PSTAMP(5);
 #endif
   }
 #ifdef MTBLX_STAMPS
-  // per role: wave 0 -> [2]=wait staged, [3]=walk1, [6]=barrier; wave 1 -> [4] idle,[5]=walk2+lookback;
-  // wave 2 -> [0]=stage, [1]=copy, [7]=barrier.  Summed over workgroups, lane 0 of waves 0..2.
-  if (lane == 0 && a.dbg && wv <= 2) {
+  // wave 0: [2] wait staged, [3] walk, [6] barrier.  wave 1: [0] stage, [1] look-back,
+  // [7] copy, [5] barrier.  Summed over workgroups (lane 0 of waves 0 and 1).
+  if (lane == 0 && a.dbg && wv <= 1) {
     for (int k = 0; k < 8; ++k) {
-      const bool mine = (wv == 0 && (k == 2 || k == 3 || k == 6)) || (wv == 1 && (k == 4 || k == 5)) ||
-                        (wv == 2 && (k == 0 || k == 1 || k == 7));
+      const bool mine = (wv == 0) ? (k == 2 || k == 3 || k == 6) : (k == 0 || k == 1 || k == 7 || k == 5);
       if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)tacc[k]);
     }
     if (wv == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 8), (unsigned long long)ntl);

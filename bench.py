@@ -101,6 +101,7 @@ def main():
 
     t = time.time()
     data, off, ln = synth.cfg2_file(args.blocks, seed=synth.SEED_CFG2 + rank)
+    exp_nrec = int(synth.cfg2_file.last_block_nrec.sum(dtype=np.uint64))  # records the Writer put in these blocks
     log(f"[rank {rank}] generated {off.size} blocks / {data.size / 2**20:.1f} MiB in {time.time() - t:.1f}s")
     batch = codec.DeviceBatch.from_host(data, off, ln)
     stream = torch.cuda.Stream()
@@ -130,7 +131,9 @@ def main():
     torch.cuda.synchronize()
     h = out.totals_host()
     st = out.status[: batch.nblk]
-    if h[3] != 0 or not bool((st == 0).all().item()) or h[0] != nrec:
+    # validity: every block OK and the decoded totals equal what the Writer wrote (16 B keys, 64 B values)
+    if h[3] != 0 or not bool((st == 0).all().item()) or h[0] != exp_nrec or h[1] != 16 * exp_nrec \
+            or h[2] != 64 * exp_nrec:
         if args.lib:
             log(f"(ablation build) totals={h}")
         else:

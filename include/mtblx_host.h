@@ -66,9 +66,10 @@ int mtblx_writer_insert_batch(mtblx_writer* w, const uint8_t* keys, const uint64
                               const uint64_t* val_end, uint64_t n);
 /* Writer::into_inner: *out malloc'd (free with mtblx_free) */
 int mtblx_writer_finish(mtblx_writer* w, uint8_t** out, uint64_t* out_len);
-/* data-block directory of the finished file: content offset / length per data block */
+/* data-block directory of the finished file: content offset / length / record count per
+ * data block (blk_nrec may be NULL) */
 uint64_t mtblx_writer_block_count(const mtblx_writer* w);
-int mtblx_writer_block_dir(const mtblx_writer* w, uint64_t* blk_off, uint32_t* blk_len);
+int mtblx_writer_block_dir(const mtblx_writer* w, uint64_t* blk_off, uint32_t* blk_len, uint32_t* blk_nrec);
 void mtblx_writer_free(mtblx_writer* w);
 void mtblx_free(void* p);
 

@@ -1024,7 +1024,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_
     const uint32_t slot0 = f * kP2Spi;
     bool ok = walk_slots(B.stage, B.rec, B.kimg, bo, R, s, e, slot0, cnt, kb, vb);
     if (!ok) {
-      ok = walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, cnt, kb, vb, slot0, 0, 0, 0, slot0, slot0 + kP2Spi);
+      ok = walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, cnt, kb, vb, slot0, 0, 0, 0, 0, slot0 + kP2Spi);
       ok = ok && cnt <= (uint32_t)kP2Spi;
     }
     B.iraw[f] = (uint8_t)(cnt < 255u ? cnt : 255u);
@@ -1049,9 +1049,11 @@ __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_
   {
     const uint32_t fa = lane < (int)nb ? B.bint0[lane] : 0u, fb = lane < (int)nb ? B.bint0[lane + 1] : 0u;
     const int sa = fa ? (int)fa - 1 : 0, sb = fb ? (int)fb - 1 : 0;
-    const uint32_t ea = fa ? (uint32_t)__shfl(ic, sa, kWave) : 0u, eb0 = (uint32_t)__shfl(ic, sb, kWave);
-    const uint32_t ka = fa ? (uint32_t)__shfl(ik, sa, kWave) : 0u, kb0 = (uint32_t)__shfl(ik, sb, kWave);
-    const uint32_t va = fa ? (uint32_t)__shfl(iv, sa, kWave) : 0u, vb0 = (uint32_t)__shfl(iv, sb, kWave);
+    // every lane must execute the permutes (a disabled source lane reads as 0)
+    const uint32_t ea0 = (uint32_t)__shfl(ic, sa, kWave), eb0 = (uint32_t)__shfl(ic, sb, kWave);
+    const uint32_t ka0 = (uint32_t)__shfl(ik, sa, kWave), kb0 = (uint32_t)__shfl(ik, sb, kWave);
+    const uint32_t va0 = (uint32_t)__shfl(iv, sa, kWave), vb0 = (uint32_t)__shfl(iv, sb, kWave);
+    const uint32_t ea = fa ? ea0 : 0u, ka = fa ? ka0 : 0u, va = fa ? va0 : 0u;
     const uint32_t eb = fb ? eb0 : 0u, kb2 = fb ? kb0 : 0u, vb2 = fb ? vb0 : 0u;
     uint32_t bc = 0, bk = 0, bv = 0;
     if (lane < (int)nb) {

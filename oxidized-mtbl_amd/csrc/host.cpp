@@ -167,6 +167,8 @@ struct mtblx_writer {
   std::vector<uint8_t> scratch;
   std::vector<uint64_t> blk_off;  // content offset of each data block (block directory)
   std::vector<uint32_t> blk_len;
+  std::vector<uint32_t> blk_nrec;
+  uint32_t cur_nrec = 0;
   mtblx_writer(uint64_t bs, uint64_t iv, uint32_t comp) : data(iv), index(iv) {
     meta[1] = std::max<uint64_t>(bs, 1024);  // WriterBuilder::block_size clamps (:43-46)
     meta[2] = comp;
@@ -182,6 +184,8 @@ struct mtblx_writer {
     if (is_data) {
       blk_off.push_back(out.size());
       blk_len.push_back((uint32_t)scratch.size());
+      blk_nrec.push_back(cur_nrec);
+      cur_nrec = 0;
     }
     out.insert(out.end(), scratch.begin(), scratch.end());
     uint64_t written = ll + 4 + scratch.size();
@@ -228,6 +232,7 @@ extern "C" int mtblx_writer_insert(mtblx_writer* w, const uint8_t* k, uint64_t k
   w->meta[7] += kl;
   w->meta[8] += vl;
   if (!w->data.add(k, kl, v, vl)) { w->poisoned = true; return MTBLX_E_FORMAT; }
+  w->cur_nrec += 1;
   return MTBLX_OK;
 }
 
@@ -268,10 +273,12 @@ extern "C" int mtblx_writer_finish(mtblx_writer* w, uint8_t** out, uint64_t* out
 }
 
 extern "C" uint64_t mtblx_writer_block_count(const mtblx_writer* w) { return w ? w->blk_off.size() : 0; }
-extern "C" int mtblx_writer_block_dir(const mtblx_writer* w, uint64_t* blk_off, uint32_t* blk_len) {
+extern "C" int mtblx_writer_block_dir(const mtblx_writer* w, uint64_t* blk_off, uint32_t* blk_len,
+                                      uint32_t* blk_nrec) {
   if (!w) return MTBLX_E_INVAL;
   std::copy(w->blk_off.begin(), w->blk_off.end(), blk_off);
   std::copy(w->blk_len.begin(), w->blk_len.end(), blk_len);
+  if (blk_nrec) std::copy(w->blk_nrec.begin(), w->blk_nrec.end(), blk_nrec);
   return MTBLX_OK;
 }
 

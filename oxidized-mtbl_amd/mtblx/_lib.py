@@ -81,7 +81,7 @@ def lib() -> C.CDLL:
         L.mtblx_writer_finish.restype = C.c_int
         L.mtblx_writer_block_count.argtypes = [C.c_void_p]
         L.mtblx_writer_block_count.restype = C.c_uint64
-        L.mtblx_writer_block_dir.argtypes = [C.c_void_p, u64p, u32p]
+        L.mtblx_writer_block_dir.argtypes = [C.c_void_p, u64p, u32p, u32p]
         L.mtblx_writer_block_dir.restype = C.c_int
         L.mtblx_writer_free.argtypes = [C.c_void_p]
         L.mtblx_free.argtypes = [C.c_void_p]

@@ -44,6 +44,7 @@ def write_arrays(keys, vals, klen, vlen, block_size=4096, restart_interval=16):
     w.insert_batch(keys, ke, vals, ve)
     data = w.into_inner_np()
     off, ln = w.block_dir
+    write_arrays.last_block_nrec = w.block_nrec
     return data, off, ln
 
 
@@ -59,4 +60,5 @@ def cfg2_file(nblocks: int = 100_000, block_size: int = 4096, seed: int = SEED_C
         nrec = int(nrec * 1.1)
         keys, vals, kl, vl = cfg2_arrays(nrec, seed)
         data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
+    cfg2_file.last_block_nrec = write_arrays.last_block_nrec[:nblocks].copy()
     return data, off[:nblocks].copy(), ln[:nblocks].copy()

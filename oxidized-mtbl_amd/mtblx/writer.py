@@ -120,8 +120,11 @@ class Writer:
         nb = int(L.mtblx_writer_block_count(self._w))
         off = np.zeros(max(nb, 1), np.uint64)
         ln = np.zeros(max(nb, 1), np.uint32)
-        L.mtblx_writer_block_dir(self._w, off.ctypes.data_as(_lib.u64p), ln.ctypes.data_as(_lib.u32p))
+        nr = np.zeros(max(nb, 1), np.uint32)
+        L.mtblx_writer_block_dir(self._w, off.ctypes.data_as(_lib.u64p), ln.ctypes.data_as(_lib.u32p),
+                                 nr.ctypes.data_as(_lib.u32p))
         self.block_dir = (off[:nb], ln[:nb])
+        self.block_nrec = nr[:nb]
         return data
 
     def into_inner_np(self) -> np.ndarray:
@@ -138,8 +141,11 @@ class Writer:
         nb = int(L.mtblx_writer_block_count(self._w))
         off = np.zeros(max(nb, 1), np.uint64)
         ln = np.zeros(max(nb, 1), np.uint32)
-        L.mtblx_writer_block_dir(self._w, off.ctypes.data_as(_lib.u64p), ln.ctypes.data_as(_lib.u32p))
+        nr = np.zeros(max(nb, 1), np.uint32)
+        L.mtblx_writer_block_dir(self._w, off.ctypes.data_as(_lib.u64p), ln.ctypes.data_as(_lib.u32p),
+                                 nr.ctypes.data_as(_lib.u32p))
         self.block_dir = (off[:nb], ln[:nb])
+        self.block_nrec = nr[:nb]
         return arr
 
     finish = into_inner

@@ -8,7 +8,7 @@ l=sys.stdin.read().strip()
 try:
   d=json.loads(l); print('value',d['value'],'ms',d['ms_per_step'],'frac',d['roofline']['frac']); print(d.get('phase_cycles_per_tile'))
 except Exception: print(l[-300:])"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-if [ "${SKIP_TESTS:-0}" != 1 ]; then run gpu_tests 600 python -m pytest tests -m gpu -x -q; tail -2 gpurun_out/gpu_tests.log; fi
+if [ "${SKIP_TESTS:-0}" != 1 ]; then run gpu_tests 600 python -m pytest tests -m gpu -x -q; tail -2 gpurun_out/gpu_tests.log; grep -q " passed" gpurun_out/gpu_tests.log && ! grep -q "failed" gpurun_out/gpu_tests.log || { echo "TESTS FAILED: stop"; exit 1; }; fi
 run bench 300 python bench.py --no-cpu-baseline
 run stamps 300 python bench.py --no-cpu-baseline --stamps
 for v in nokey noval nocopy; do

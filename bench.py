@@ -7,7 +7,7 @@ Metric (BASELINE.json): "KV records/s + GiB/s of block bytes decoded, device-res
 written by the product Writer from a seeded generator (synthetic data).
 
 A step = one full decode of the resident batch through the C ABI (mtblx_decode_blocks:
-one single-pass k_decode_tiles launch), i.e. every block's records reconstructed and laid
+one single-pass k_decode_pipe launch for blocks <= 48 KiB, k_decode_tiles above), i.e. every block's records reconstructed and laid
 out contiguously in HBM.  Inputs are in HBM before timing starts.
 
 Multi-GPU (torchrun, one rank per GPU): blocks are independent, so every rank decodes
@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "oxidized-mtbl_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+PIPE_MAX_BLOCK = 49152 - 64  # largest block k_decode_pipe stages (decode.hip make_plan); bigger -> k_decode_tiles
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
 
 
@@ -82,8 +83,9 @@ def main():
     ap.add_argument("--lib", default=None, help="diagnostic: alternative libmtblx build (ablations)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load libmtblx_stamps.so and report per-phase cycles per tile (not a measurement)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_decode_tiles.json"),
-                    help="PMC-derived HBM bytes per k_decode_tiles launch (profiles/, from a rocprofv3 --pmc run)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per decode launch (profiles/, written by scripts/pmc_traffic.py "
+                         "from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)")
     args = ap.parse_args()
 
     if args.stamps:
@@ -118,7 +120,7 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
-        # one mtblx_decode_blocks call = 2 tiny memsets (look-back words, totals) + k_decode_tiles
+        # one mtblx_decode_blocks call = 2 tiny memsets (look-back words, totals) + one decode kernel
         if i is not None:
             ev[i][0].record(stream)
         codec.decode_into(batch, out, ws, stream)
@@ -160,13 +162,17 @@ def main():
     total_recs = nrec * world
     value = total_bytes / (elapsed / args.steps) / 2**30
 
-    # roofline of the (only) kernel k_decode_tiles: algorithmic bytes per launch
+    # roofline of the (only) decode kernel: algorithmic bytes per launch:
+    # block bytes read + key/value bytes written + 2 x u32 end offsets per record + 24 B of per-block outputs
     alg_bytes = block_bytes + kbytes + vbytes + 8 * nrec + 24 * batch.nblk
     achieved = alg_bytes / (k_decode_ms * 1e-3) / 1e9
+    kernel = "k_decode_pipe" if int(ln.max()) <= PIPE_MAX_BLOCK else "k_decode_tiles"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+            tj = json.load(open(args.traffic_json))
+            if tj.get("kernel") == kernel and int(tj.get("blocks", -1)) == int(batch.nblk):
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -189,10 +195,10 @@ def main():
                    "blocks_per_gpu": int(batch.nblk), "block_bytes_per_gpu": block_bytes,
                    "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
                    "parallelism": f"block-sharded x{world}, no collective"},
-        "kernels_ms": {"k_decode_tiles (events incl. 2 memsets)": round(k_decode_ms, 4)},
+        "kernels_ms": {f"{kernel} (events incl. 2 memsets)": round(k_decode_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_decode_tiles", "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel": kernel, "alg_bytes_per_launch": int(alg_bytes)},
     }
     if args.stamps:
         d = ws.buf[:72].cpu().numpy().view(np.uint64).astype(np.float64)

@@ -202,8 +202,8 @@ def main():
     }
     if args.stamps:
         d = ws.buf[:72].cpu().numpy().view(np.uint64).astype(np.float64)
-        names = ["w1:stage", "w1:lookback", "w0:wait-staged", "w0:walk", "-", "w1:barrier", "w0:barrier",
-                 "w1:copy"]
+        names = ["copy:wait-ready", "w1:lookback+barrier", "w0:walk-loop", "w0:scan-publish",
+                 "w2:dma-issue (+w0 barrier)", "copy:barrier", "w2:dma-wait+barrier", "copy:copy"]
         ntl = max(d[8], 1)
         res["phase_cycles_per_tile"] = {n: round(d[k] / ntl, 1) for k, n in enumerate(names)}
         res["stamps_note"] = "diagnostic build (s_memtime, thread 0 of each workgroup), last step only; shares, not time"

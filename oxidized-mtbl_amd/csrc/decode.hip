@@ -884,34 +884,57 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 // software-pipelined decoder for small blocks (k_decode_pipe)
 // ----------------------------------------------------------------------------------
 // One 512-thread workgroup per CU, persistent, static round-robin over tiles
-// (t = g + kG).  Two tile buffers in LDS.  Iteration i:
-//   wave 0      : walk of tile i+1 -- ONE pass per restart interval that counts AND
-//                 writes per-record metadata + rebuilt keys (<= 16 B) into
-//                 provisional slots (interval f, entry k -> slot 16 f + k); interval
-//                 scan; block totals; publish the tile aggregate A
-//   waves 1..7  : stage tile i+1 (registers prefetched during iteration i-1), signal
-//                 wave 0, prefetch tile i+2; wave 1 computes the look-back of tile i
-//                 (aggregates other workgroups published one iteration earlier) and the
-//                 per-block outputs; then all seven waves copy tile i
-//   __syncthreads
+// (t = g + kG), three LDS tile buffers.  Iteration i (buffers rotate mod 3):
+//   wave 0      : LDS-DMA (global_load_lds, no registers) of tile i+2; walk of tile i+1
+//                 -- the minimal header chain: one lane per restart interval records
+//                 the header offset of every entry in slot 16 f + k and counts; interval
+//                 scan; block totals; publish the tile aggregate A; vmcnt(0) (retires
+//                 the DMA of tile i+2 before the barrier, read one phase later)
+//   wave 1      : look-back of tile i from aggregate words it loaded one iteration
+//                 earlier; per-block outputs; then issues the loads for tile i+1
+//   waves 2..7  : record pass + copy of tile i: one 16-lane DPP row per restart
+//                 interval (entry k = lane k of the row).  Key prefixes are rebuilt
+//                 in parallel by a row-wide Hillis-Steele scan of the associative
+//                 "truncate-then-append" operator (src/block.rs:134-135), 16 key
+//                 bytes per plane, any key length; values and keys go out with
+//                 unaligned 16 B stores
+//   s_waitcnt lgkmcnt(0); s_barrier (raw: global stores and the DMA in flight are not
+//   drained at the barrier)
 // Restart intervals of more than 16 entries (the reference default is 16,
-// src/lib.rs:4) or tiles of more than kP2MaxInt intervals take the exact generic
-// path for the affected blocks.
-constexpr int kPipeThreads = 512;
-constexpr int kPipeCopyThreads = kPipeThreads - kWave;   // waves 1..7
-constexpr int kPipeCopyWaves = kPipeCopyThreads / kWave;
+// src/lib.rs:4), tiles of more than kP2MaxInt intervals and anything irregular take the
+// exact generic path for the affected blocks.
+// diagnostic per-phase cycle stamps (MTBLX_STAMPS builds only; lane 0 of a wave)
+struct Stamps {
+#ifdef MTBLX_STAMPS
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prev = 0;
+  __device__ __forceinline__ void init() { prev = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void hit(int k) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    acc[k] += t - prev;
+    prev = t;
+  }
+#else
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void hit(int) {}
+#endif
+};
+
+constexpr int kPipeThreads = 768;
+constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loader (issues no stores)
+constexpr int kPipeCopyWave0 = 3;                                        // waves 3..11 copy
+constexpr int kPipeCopyWaves = kPipeThreads / kWave - kPipeCopyWave0;
+constexpr int kPipeRows = kPipeCopyWaves * (kWave / 16);                 // intervals per copy round
 constexpr int kPipeTB = 49152;
-constexpr int kP2Spi = 16;                                // slots per interval
+constexpr int kP2Spi = 16;                                               // slots per interval (= DPP row)
 constexpr int kP2MaxInt = 56;
 constexpr int kP2Slots = kP2MaxInt * kP2Spi;
 constexpr int kPipeMaxBlk = 16;
-constexpr int kPipePf = (kPipeTB + 16 * kPipeCopyThreads - 1) / (16 * kPipeCopyThreads);  // uint4 per thread
-constexpr uint32_t kKeyInImg = 1u << 20;   // Rec.vs_blk flag: the record's key is in kimg
+constexpr int kPipeBufs = 3;
 
 struct alignas(16) PipeBuf {
   uint8_t stage[kPipeTB];
-  Rec rec[kP2Slots];          // ks / vs interval-relative
-  uint4 kimg[kP2Slots];       // full key of entries with key length <= 16
+  uint16_t pos[kP2Slots];     // header offset (block-relative) of entry k of interval f: slot 16 f + k
   uint32_t boff[kPipeMaxBlk], blen[kPipeMaxBlk], bR[kPipeMaxBlk], bn[kPipeMaxBlk];
   uint32_t bok[kPipeMaxBlk], bwr[kPipeMaxBlk];
   int32_t bst[kPipeMaxBlk];
@@ -928,25 +951,74 @@ struct alignas(16) PipeBuf {
 };
 
 struct alignas(16) PipeLds {
-  PipeBuf buf[2];
-  uint32_t staged;   // copy waves increment after staging a tile (wave 0 waits on it)
+  PipeBuf buf[kPipeBufs];
   uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
+  uint32_t pub;      // wave 0 sets after publishing the aggregate of the tile it walked
+  uint32_t cdone;    // copy waves that finished their copy (monotonic)
 };
 
-// One pass over restart interval [s, e): counts, per-entry metadata into slots
-// slot0 + k (k < 16), and keys rebuilt in registers (first 16 bytes; src/block.rs:134-135
-// key.truncate(shared) + key.extend(suffix): the 16-byte LDS window starting sh bytes
-// before the suffix has key byte j at window byte j).  The next header's LDS read is
-// issued before this entry's window/merge/stores, so the loop-carried chain is one LDS
-// round trip.  1-byte-varint headers only; false on anything else (the caller then runs
-// the exact walk_interval).
-__device__ __forceinline__ bool walk_slots(const uint8_t* stage, Rec* recs, uint4* kimg, uint32_t bo, uint32_t R,
-                                           uint32_t s, uint32_t e, uint32_t slot0, uint32_t& cnt, uint32_t& kb,
-                                           uint32_t& vb) {
+__device__ __forceinline__ void raw_barrier() {
+  // LDS traffic complete, then the hardware barrier; outstanding global stores and
+  // LDS-DMA stay in flight (a __syncthreads() would wait vmcnt(0) here)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int D>
+__device__ __forceinline__ uint32_t row_shr_keep(uint32_t x) {  // lane k <- lane k-D of its row, else itself
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x110 + D, 0xf, 0xf, false);
+}
+template <int D>
+__device__ __forceinline__ uint32_t row_shr_zero(uint32_t x) {  // lane k <- lane k-D of its row, else 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + D, 0xf, 0xf, false);
+}
+
+// exclusive prefix sum inside each 16-lane row
+__device__ __forceinline__ uint32_t row_excl_scan(uint32_t x) {
+  uint32_t y = x;
+  y += row_shr_zero<1>(y);
+  y += row_shr_zero<2>(y);
+  y += row_shr_zero<4>(y);
+  y += row_shr_zero<8>(y);
+  return y - x;
+}
+
+// dword i of the mask of bytes b >= t of a 16-byte plane
+__device__ __forceinline__ uint32_t keep_mask(int t, int i) {
+  int lo = t - 4 * i;
+  lo = lo < 0 ? 0 : lo;
+  return lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo));
+}
+
+// One Hillis-Steele step of the key-prefix scan.  State of a run of entries = (m, W):
+// m = smallest `shared` in the run, W = key bytes of the run's last entry at positions
+// >= m (this plane).  compose(L, R) = (min(mL, mR), bytes >= mR from R, the rest from L):
+// key.truncate(shared) + key.extend(suffix) applied entry after entry.
+template <int D>
+__device__ __forceinline__ void key_scan_step(uint32_t& m, uint4& W, uint32_t q0) {
+  const uint32_t mL = row_shr_keep<D>(m);
+  uint4 L;
+  L.x = row_shr_keep<D>(W.x);
+  L.y = row_shr_keep<D>(W.y);
+  L.z = row_shr_keep<D>(W.z);
+  L.w = row_shr_keep<D>(W.w);
+  const int t = (int)m - (int)q0;
+  uint32_t k;
+  k = keep_mask(t, 0); W.x = (W.x & k) | (L.x & ~k);
+  k = keep_mask(t, 1); W.y = (W.y & k) | (L.y & ~k);
+  k = keep_mask(t, 2); W.z = (W.z & k) | (L.z & ~k);
+  k = keep_mask(t, 3); W.w = (W.w & k) | (L.w & ~k);
+  m = mL < m ? mL : m;
+}
+
+// Walk of restart interval [s, e) of a staged block: the loop-carried chain is only
+// p -> LDS header read -> p'.  The next header's read is issued before this entry's slot
+// store.  1-byte-varint headers; false on anything else (the caller then runs the exact
+// walk_careful_pos).  Preconditions as walk_interval (regular blocks).
+__device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t R, uint32_t s,
+                                         uint32_t e, uint32_t slot0, uint32_t& cnt, uint32_t& kb, uint32_t& vb) {
   cnt = kb = vb = 0;
   if (!(s < e && e <= R)) return false;
   uint32_t p = s, prevlen = 0, bad = 0;
-  uint4 key = make_uint4(0, 0, 0, 0);
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   uint32_t ad = bo + p;
   uint32_t w0 = st32[ad >> 2], w1 = st32[(ad >> 2) + 1];
@@ -955,25 +1027,11 @@ __device__ __forceinline__ bool walk_slots(const uint8_t* stage, Rec* recs, uint
     const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
     const uint32_t np = p + 3u + ns + vl;
     bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R) | (uint32_t)(cnt >= (uint32_t)kP2Spi);
-    // issue the next header read now (np <= R + 3 + 254 stays inside the stage buffer:
-    // bo + R <= TB - 48 and the read is only consumed if np < e <= R)
+    // np <= R + 257 stays inside the stage buffer (bo + R <= TB - 48 + ...; only consumed if np < e <= R)
     const uint32_t nad = bo + (np < e ? np : p);
     const uint32_t n0 = st32[nad >> 2], n1 = st32[(nad >> 2) + 1];
+    if (!bad) pos[slot0 + cnt] = (uint16_t)p;
     const uint32_t klen = sh + ns;
-    if (sh < 16u) {
-      const uint4 w = lds_win16(stage, ad + 3u - sh);
-      merge_bytes(key, w, (int)sh, (int)(klen < 16u ? klen : 16u));
-    }
-    if (!bad) {
-      const uint32_t r = slot0 + cnt;
-      Rec x;
-      x.pos_sh = (p + 3u) | (sh << 16);
-      x.ns_vl = ns | (vl << 16);
-      x.ks = kb;
-      x.vs_blk = vb | (klen <= 16u ? kKeyInImg : 0u);
-      recs[r] = x;
-      kimg[r] = key;
-    }
     cnt += 1;
     kb += klen;
     vb += vl;
@@ -986,10 +1044,115 @@ __device__ __forceinline__ bool walk_slots(const uint8_t* stage, Rec* recs, uint
   return !bad && p == e;
 }
 
-// wave 0: trailers, walk (metadata + keys into slots), irregular counts, interval scan,
+// exact walk (multi-byte varint headers allowed) recording header offsets; same checks as
+// walk_interval
+__device__ __forceinline__ bool walk_careful_pos(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t L, uint32_t R,
+                                                 uint32_t s, uint32_t e, uint32_t slot0, uint32_t& cnt, uint32_t& kb,
+                                                 uint32_t& vb) {
+  cnt = kb = vb = 0;
+  if (!(s < e && e <= R)) return false;
+  uint32_t p = s, prevlen = 0;
+  while (p < e) {
+    if (cnt >= (uint32_t)kP2Spi) return false;
+    const uint32_t ad = bo + p;
+    const uint32_t hw = lds_rd32(stage, ad);
+    uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu, h = 3;
+    if ((hw & 0x808080u) != 0u) {
+      if (R - p < 3u) return false;
+      const uint4 W = lds_win16(stage, ad);
+      const uint32_t l0 = dec32(W, 0, L - p, sh);
+      if (l0 == 0) return false;
+      const uint32_t l1 = dec32(W, l0, L - p - l0, ns);
+      if (l1 == 0) return false;
+      const uint32_t l2 = dec32(W, l0 + l1, L - p - l0 - l1, vl);
+      if (l2 == 0) return false;
+      h = l0 + l1 + l2;
+      if (p + h > R) return false;
+      if ((sh | ns | vl) > 0xFFFFu) return false;
+    }
+    if (R - p < h + ns + vl) return false;
+    if (sh > prevlen) return false;
+    pos[slot0 + cnt] = (uint16_t)p;
+    const uint32_t klen = sh + ns;
+    cnt += 1;
+    kb += klen;
+    vb += vl;
+    prevlen = klen;
+    p += h + ns + vl;
+  }
+  return p == e && (prevlen <= 0xFFFFu);
+}
+
+// wave 0: LDS-DMA of tile t into B (contiguous range, or one 16 B aligned slot per block).
+// (off_l, len_l) = directory entry of block `lane` of the tile (lanes < nb).
+__device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t t, uint64_t off_l, uint32_t len_l,
+                                         int lane) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void g_void;
+  const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
+  const uint64_t base = reinterpret_cast<uintptr_t>(a.data);
+  const uint64_t s = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off_l >> 32), 0) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off_l, 0);
+  const uint64_t end_l = off_l + len_l;
+  const uint64_t e = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(end_l >> 32), (int)nb - 1) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end_l, (int)nb - 1);
+  uint64_t r0 = ((base + s) & ~15ull) - base;
+  if (base + s < 16 || ((base + s) & ~15ull) < base) r0 = 0;
+  const bool contig = e > s && e - r0 + 48 <= (uint64_t)kPipeTB;
+  if (contig) {
+    // range byte x at stage offset 16 + x; wave-instruction m writes chunks [64m, 64m + 64)
+    const uint32_t nch = (uint32_t)((e - r0 + 15) >> 4);
+    for (uint32_t m = 0; m * kWave < nch; ++m) {
+      const uint32_t c = m * kWave + lane;
+      const uint64_t go = r0 + 16ull * c;
+      if (c < nch) {
+        if (go + 16 <= a.data_len && ((base + go) & 15ull) == 0)
+          __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
+        else
+          *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
+      }
+    }
+    if (lane < (int)nb) {
+      B.boff[lane] = (uint32_t)(16 + off_l - r0);
+      B.blen[lane] = len_l;
+    }
+  } else {
+    // per-block slots of a.slot bytes (blocks not adjacent in the buffer)
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint64_t off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off_l >> 32), (int)j) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off_l, (int)j);
+      const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)len_l, (int)j);
+      const uint32_t so = 16u + j * a.slot;
+      uint32_t bo = kNotStaged;
+      if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)kPipeTB) {
+        uint64_t a0 = ((base + off) & ~15ull) - base;
+        if (base + off < 16 || ((base + off) & ~15ull) < base) a0 = off;  // unaligned data base: not reached
+        const uint32_t delta = (uint32_t)(off - a0);
+        const uint32_t nch = (delta + L + 15u) >> 4;
+        for (uint32_t m = 0; m * kWave < nch; ++m) {
+          const uint32_t c = m * kWave + lane;
+          const uint64_t go = a0 + 16ull * c;
+          if (c < nch) {
+            if (go + 16 <= a.data_len && ((base + go) & 15ull) == 0)
+              __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + so + 1024 * m), 16, 0,
+                                               0);
+            else
+              *reinterpret_cast<uint4*>(B.stage + so + 16 * c) = load_chunk(a, go);
+          }
+        }
+        bo = so + delta;
+      }
+      if (lane == 0) { B.boff[j] = bo; B.blen[j] = L; }
+    }
+  }
+  if (lane == 0) { B.nb = nb; B.b0 = b0; }
+}
+
+// wave 0: trailers, walk (header offsets into slots), irregular counts, interval scan,
 // block totals, publish A(t)
-__device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_t t, int lane) {
+__device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_t t, int lane, Stamps& ST) {
   const uint32_t nb = B.nb, b0 = B.b0;
+  uint32_t binc = 0;   // lane b: inclusive interval count of blocks 0..b
   {  // trailers (Block::init, src/block.rs:16-49) + interval numbering
     uint32_t n = 0, R = 0, ok = 0;
     if (lane < (int)nb) {
@@ -1008,30 +1171,31 @@ __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_
       B.bint0[lane] = incl - n;
     }
     if (lane == (int)nb - 1) { B.bint0[nb] = incl; B.nint = incl; }
+    binc = incl;
   }
   wave_sync();
   const uint32_t nint = B.nint;
+  // block of interval f = number of blocks whose inclusive interval count is <= f
+  uint32_t jlane = 0;
+  for (uint32_t b = 0; b + 1 < nb; ++b) jlane += ((uint32_t)__builtin_amdgcn_readlane((int)binc, (int)b) <= (uint32_t)lane);
   // walk: one lane per restart interval (nint <= kP2MaxInt <= 64)
   uint32_t cnt = 0, kb = 0, vb = 0, jf = 0;
   if (lane < (int)nint) {
     const uint32_t f = lane;
-    uint32_t j = 0;
-    while (B.bint0[j + 1] <= f) ++j;
+    const uint32_t j = jlane;
     jf = j;
     const uint32_t i = f - B.bint0[j], bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
     const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
     const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
     const uint32_t slot0 = f * kP2Spi;
-    bool ok = walk_slots(B.stage, B.rec, B.kimg, bo, R, s, e, slot0, cnt, kb, vb);
-    if (!ok) {
-      ok = walk_interval<true>(B.stage, B.rec, bo, L, R, s, e, cnt, kb, vb, slot0, 0, 0, 0, 0, slot0 + kP2Spi);
-      ok = ok && cnt <= (uint32_t)kP2Spi;
-    }
+    bool ok = walk_pos(B.stage, B.pos, bo, R, s, e, slot0, cnt, kb, vb);
+    if (!ok) ok = walk_careful_pos(B.stage, B.pos, bo, L, R, s, e, slot0, cnt, kb, vb);
     B.iraw[f] = (uint8_t)(cnt < 255u ? cnt : 255u);
     B.iblk[f] = (uint8_t)j;
     if (!ok) B.bok[j] = 0;
   }
   wave_sync();
+  ST.hit(2);
   // irregular blocks: exact serial count (generic path, lane per block)
   if (lane < (int)nb && !B.bok[lane]) {
     const uint32_t j = lane, bo = B.boff[j], L = B.blen[j];
@@ -1097,26 +1261,62 @@ __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_
   }
 }
 
-// wave 1: look-back of tile t (aggregates published by the other workgroups one
-// iteration earlier) + per-block outputs.  tinc = inclusive prefix of this workgroup's
-// previous tile (wave 1 registers).
+// wave 1: issue the look-back loads of tile t (aggregates of tiles t-G+1 .. t-1) one
+// iteration before they are consumed; they complete behind the copy phase.
+__device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t t, uint32_t G,
+                                                    uint64_t lbv[kMaxLookbackLoads], int lane) {
+  const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
+#pragma unroll
+  for (int m = 0; m < kMaxLookbackLoads; ++m) {
+    const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
+    lbv[m] = (i >= lo) ? __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kReady;
+  }
+}
+
+// wave 1: re-poll the words of tile t that were not ready when loaded, until all are or
+// the copy waves have finished this iteration (the barrier must not wait for laggards;
+// what is still missing is polled again when the tile is consumed).
+__device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t, uint32_t G,
+                                                   uint64_t lbv[kMaxLookbackLoads], int lane, const uint32_t* cdone,
+                                                   uint32_t want) {
+  const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
+  for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+    bool pend = false;
+#pragma unroll
+    for (int m = 0; m < kMaxLookbackLoads; ++m) {
+      const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
+      pend |= (i >= lo) && !(lbv[m] & kReady);
+    }
+    if (__ballot(pend) == 0ull) return;
+    if (__hip_atomic_load(cdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return;
+    __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+    for (int m = 0; m < kMaxLookbackLoads; ++m) {
+      const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
+      if (i >= lo && !(lbv[m] & kReady)) lbv[m] = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// wave 1: finish the look-back of tile t (re-polling words that were not ready yet),
+// per-block outputs.  tinc = inclusive prefix of this workgroup's previous tile.
 __device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3],
-                                              int lane) {
+                                              uint64_t lbv[kMaxLookbackLoads], int lane) {
   const uint32_t nb = B.nb, b0 = B.b0;
-  const uint32_t lo = (t >= G) ? t - G + 1 : 0;
+  const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
   uint64_t sr = 0, sk = 0, sv = 0;
   bool timeout = false;
 #pragma unroll
   for (int m = 0; m < kMaxLookbackLoads; ++m) {
     const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
-    if (i < (int64_t)lo) continue;
-    uint64_t w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t w = lbv[m];
     uint32_t spins = 0;
     while (!(w & kReady)) {
       __builtin_amdgcn_s_sleep(2);
       w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (++spins > (1u << 22)) { timeout = true; w = kReady; }
     }
+    if (i < lo) continue;
     sr += (w >> 42) & kField;
     sv += (w >> 21) & kField;
     uint64_t kk = w & kField;
@@ -1156,64 +1356,95 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uin
   }
 }
 
-// waves 1..7: copy one tile (thread per slot) + irregular blocks
-__device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int ct) {
+// waves 2..7: record pass + copy of one tile.  Copy wave cw owns 16-lane rows
+// 4 cw .. 4 cw + 3 of each round; row = restart interval, lane k of the row = entry k.
+__device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int cw, int lane) {
   const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
   const uint32_t nint = B.nint, nb = B.nb;
-  for (uint32_t q = ct; q < nint * kP2Spi; q += kPipeCopyThreads) {
-    const uint32_t f = q / kP2Spi, kq = q % kP2Spi;
-    if (kq >= B.iraw[f]) continue;
-    const uint32_t j = B.iblk[f];
-    if (!B.bok[j] || !B.bwr[j]) continue;
-    const uint4 rr = *reinterpret_cast<const uint4*>(&B.rec[q]);
+  const uint32_t k = lane & 15;
+  for (uint32_t fb = (uint32_t)cw * (kWave / 16); fb < nint; fb += kPipeRows) {   // wave-uniform
+    const uint32_t f = fb + (lane >> 4);
+    const bool fv = f < nint;
+    const uint32_t j = fv ? B.iblk[f] : 0u;
+    const bool live = fv && k < B.iraw[f] && B.bok[j] && B.bwr[j];
     const uint32_t bo = B.boff[j];
-    const uint32_t pos = rr.x & 0xFFFFu, shr = rr.x >> 16, ns = rr.y & 0xFFFFu, vl = rr.y >> 16;
-    const uint32_t ks = B.ikb[f] + rr.z, vs = B.ivb[f] + (rr.w & 0xFFFFFu);
-    const uint32_t klen = shr + ns;
-    const uint64_t gr = pr + B.icnt[f] + kq;
-    a.key_end[gr] = ks + klen - B.bkbb[j];
-    a.val_end[gr] = vs + vl - B.bvbb[j];
+    const uint32_t p = live ? B.pos[f * kP2Spi + k] : 0u;
+    uint32_t sh = 0, ns = 0, vl = 0, h = 3;
+    if (live) {  // decode_entry (src/block.rs:216-238) at a header the walk validated
+      const uint32_t hw = lds_rd32(B.stage, bo + p);
+      sh = hw & 0xffu; ns = (hw >> 8) & 0xffu; vl = (hw >> 16) & 0xffu;
+      if ((hw & 0x808080u) != 0u) {
+        const uint4 W = lds_win16(B.stage, bo + p);
+        const uint32_t l0 = dec32(W, 0, 16, sh);
+        const uint32_t l1 = dec32(W, l0, 16, ns);
+        const uint32_t l2 = dec32(W, l0 + l1, 16, vl);
+        h = l0 + l1 + l2;
+      }
+    }
+    const uint32_t klen = sh + ns;
+    const uint32_t kx = row_excl_scan(klen), vx = row_excl_scan(vl);
+    const uint32_t ks = (fv ? B.ikb[f] : 0u) + kx, vs = (fv ? B.ivb[f] : 0u) + vx;
+    const uint32_t sp = bo + p + h;   // stage offset of the key suffix
+    if (live) {
+      const uint64_t gr = pr + B.icnt[f] + k;
+      a.key_end[gr] = ks + klen - B.bkbb[j];
+      a.val_end[gr] = vs + vl - B.bvbb[j];
+    }
 #ifndef MTBLX_ABL_NOVAL
-    const uint32_t vsrc = bo + pos + ns;
-    uint8_t* vd = a.vals + pv + vs;
-    for (uint32_t o = 0; o < vl; o += 16) {
-      uint4 w4 = lds_win16(B.stage, vsrc + o);
-      const uint32_t m = vl - o;
-      store_bytes(vd + o, w4, m < 16 ? m : 16);
+    // values.  Fast path (wave-uniform): every live entry of this round has the same value
+    // length U, a multiple of 16 -> lane k of a row writes 16 B chunks k, k+16, ... of the
+    // interval's contiguous value range (coalesced stores).  Otherwise one entry per lane.
+    const uint64_t lv = __ballot(live);
+    if (lv != 0ull) {
+      const int l0 = __builtin_ctzll(lv);
+      const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)vl, l0);
+      const bool uni = (U % 16u) == 0u && U != 0u && __ballot(live && vl != U) == 0ull;
+      const uint32_t vsrc = sp + ns;   // stage offset of the entry's value
+      if (uni) {
+        const uint32_t cpr = U >> 4;                                  // chunks per entry
+        const bool pow2 = (cpr & (cpr - 1u)) == 0u;
+        const uint32_t cprs = (uint32_t)__builtin_ctz(cpr);
+        const uint32_t nrow = (fv && B.bok[j] && B.bwr[j]) ? (uint32_t)B.iraw[f] : 0u;
+        const uint32_t nch = nrow * cpr;
+        uint8_t* vd0 = a.vals + pv + (fv ? B.ivb[f] : 0u);
+        const int rowbase = lane & ~15;
+        for (uint32_t c = k; __ballot(c < nch) != 0ull; c += 16) {   // wave-uniform trip count
+          const bool act = c < nch;
+          const uint32_t r = act ? (pow2 ? c >> cprs : c / cpr) : 0u;
+          const uint32_t src = (uint32_t)__shfl((int)vsrc, rowbase + (int)r, kWave);
+          if (act) {
+            const uint4 w4 = lds_win16(B.stage, src + 16u * (c - r * cpr));
+            *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4.x, w4.y, w4.z, w4.w};
+          }
+        }
+      } else if (live) {
+        uint8_t* vd = a.vals + pv + vs;
+        for (uint32_t o = 0; o < vl; o += 16) {
+          const uint32_t mlen = vl - o;
+          store_bytes(vd + o, lds_win16(B.stage, vsrc + o), mlen < 16 ? mlen : 16);
+        }
+      }
     }
 #endif
 #ifndef MTBLX_ABL_NOKEY
     uint8_t* kd = a.keys + pk + ks;
-    if (rr.w & kKeyInImg) {  // whole key rebuilt by the walk
-      store_bytes(kd, B.kimg[q], klen);
-      continue;
-    }
-    for (uint32_t j0 = 0; j0 < klen; j0 += 16) {
-      const uint32_t jend = (j0 + 16 < klen) ? j0 + 16 : klen;
-      uint4 outw = make_uint4(0, 0, 0, 0);
-      uint32_t jj = j0;
-      while (jj < jend) {
-        // key byte jj comes from the suffix of the latest entry s <= q of the same
-        // interval (slots are contiguous per interval) with shared_s <= jj
-        uint32_t sidx = q, m = klen, shs = shr, ps = pos;
-        while (shs > jj) {
-          m = shs < m ? shs : m;
-          --sidx;
-          const uint32_t x = B.rec[sidx].pos_sh;
-          shs = x >> 16;
-          ps = x & 0xFFFFu;
-        }
-        const uint32_t seg = m < jend ? m : jend;
-        const uint32_t src = bo + ps + (jj - shs);
-        uint4 w4 = lds_win16(B.stage, src - (jj - j0));
-        merge_bytes(outw, w4, (int)(jj - j0), (int)(seg - j0));
-        jj = seg;
+    for (uint32_t q0 = 0; __ballot(live && klen > q0) != 0ull; q0 += 16) {   // wave-uniform planes
+      const bool own = live && sh < q0 + 16u && q0 < klen;
+      uint4 W = own ? lds_win16(B.stage, sp - sh + q0) : make_uint4(0, 0, 0, 0);
+      uint32_t m = sh;
+      key_scan_step<1>(m, W, q0);
+      key_scan_step<2>(m, W, q0);
+      key_scan_step<4>(m, W, q0);
+      key_scan_step<8>(m, W, q0);
+      if (live && q0 < klen) {
+        const uint32_t n = klen - q0;
+        store_bytes(kd + q0, W, n < 16 ? n : 16);
       }
-      store_bytes(kd + j0, outw, jend - j0);
     }
 #endif
   }
   // irregular blocks: exact serial write (thread per block)
+  const int ct = cw * kWave + lane;
   if (ct < (int)nb && !B.bok[ct] && B.bwr[ct]) {
     const uint32_t j = ct, bo = B.boff[j], L = B.blen[j];
     const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[B.b0 + j]);
@@ -1227,119 +1458,104 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t g = blockIdx.x, G = gridDim.x;
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
-  const int ct = tid - kWave;                                              // copy-thread index
-#ifdef MTBLX_STAMPS
-  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime(), ntl = 0;
-#define PSTAMP(k) do { if (lane == 0) { const uint64_t _t = __builtin_amdgcn_s_memtime(); tacc[k] += _t - tprev; tprev = _t; } } while (0)
-#else
-#define PSTAMP(k) do { } while (0)
-#endif
-  if (tid == 0) { S.staged = 0; S.ready = 0; }
+  Stamps ST;
+  ST.init();
+  if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; }
+
+  uint64_t tinc[3] = {0, 0, 0};           // wave 1
+  uint64_t lbv[kMaxLookbackLoads];        // wave 1: look-back words of the next tile to copy
+  uint64_t ioff = 0;                      // wave 0: directory entry (lane < nb) of the next tile to stage
+  uint32_t ilen = 0;
+  auto load_info = [&](uint32_t kk) {
+    if (kk >= nloc) return;
+    const uint32_t b0 = (g + kk * G) * a.bpt, nb = min(a.bpt, a.nblk - b0);
+    const uint32_t j = (uint32_t)lane < nb ? (uint32_t)lane : nb - 1;
+    ioff = a.blk_off[b0 + j];
+    ilen = a.blk_len[b0 + j];
+  };
+  if (wv == kPipeLoadWave) {
+    load_info(0);
+    if (nloc > 0) pipe_dma(S.buf[0], a, g, ioff, ilen, lane);
+    load_info(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (wv == 1) {
+    if (nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
+  }
   __syncthreads();
   if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
-
-  uint64_t tinc[3] = {0, 0, 0};   // wave 1 only
-  uint4 pf[kPipePf];              // copy waves: prefetched bytes of the next tile to stage
-  uint64_t pr0 = 0, pr1 = 0;
-  auto prefetch = [&](uint32_t k) {
-    pr1 = 0;
-    if (k >= nloc) return;
-    tile_range(a, g + k * G, kPipeTB, pr0, pr1);
-    if (!pr1) return;
-#pragma unroll
-    for (int m = 0; m < kPipePf; ++m) {
-      const uint64_t o = pr0 + 16ull * (uint32_t)(ct + m * kPipeCopyThreads);
-      pf[m] = (o < pr1) ? load_chunk(a, o) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  if (wv >= 1) prefetch(0);
+  uint64_t ntl = 0;
 
   for (int it = -1; it < (int)nloc; ++it) {
-    const uint32_t k1 = (uint32_t)(it + 1);   // tile to stage + walk
-    if (wv >= 1) {
-      // ---- stage local tile it+1 into buf[(it+1)&1], prefetch it+2 ----
+    const uint32_t k1 = (uint32_t)(it + 1), k2 = (uint32_t)(it + 2);
+    if (wv == 0) {
+      // walk first: the aggregate A(tile it+1) is published as early as possible
       if (k1 < nloc) {
-        PipeBuf& B = S.buf[k1 & 1];
-        const uint32_t t1 = g + k1 * G;
-        const uint32_t b0 = t1 * a.bpt, nb = min(a.bpt, a.nblk - b0);
-        if (pr1) {
-          const uint32_t nch = (uint32_t)((pr1 - pr0 + 15) >> 4);
-#pragma unroll
-          for (int m = 0; m < kPipePf; ++m) {
-            const uint32_t c = ct + m * kPipeCopyThreads;
-            if (c < nch) *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = pf[m];
-          }
-          if (ct < (int)nb) {
-            const uint64_t off = a.blk_off[b0 + ct];
-            const uint32_t L = a.blk_len[b0 + ct];
-            B.boff[ct] = (off >= pr0 && off + L <= pr1) ? (uint32_t)(16 + off - pr0) : kNotStaged;
-            B.blen[ct] = L;
-          }
-        } else {
-          for (uint32_t j = wv - 1; j < nb; j += kPipeCopyWaves) {
-            const uint32_t L = a.blk_len[b0 + j];
-            const uint64_t off = a.blk_off[b0 + j];
-            const uint32_t so = 16u + j * a.slot;
-            uint32_t bo = kNotStaged;
-            if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)kPipeTB) bo = so + stage_slot(a, B.stage + so, off, L, lane);
-            if (lane == 0) { B.boff[j] = bo; B.blen[j] = L; }
-          }
-        }
-        if (ct == 0) { B.nb = nb; B.b0 = b0; }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(&S.staged, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        prefetch(k1 + 1);
+        pipe_walk(S.buf[k1 % kPipeBufs], a, g + k1 * G, lane, ST);
+        if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      PSTAMP(0);
-      if (it >= 0) {
-        PipeBuf& C = S.buf[it & 1];
-        const uint32_t tc = g + (uint32_t)it * G;
-        if (wv == 1) {
-          pipe_lookback(C, a, tc, G, tinc, lane);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) __hip_atomic_store(&S.ready, (uint32_t)it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
+      ST.hit(3);
+    } else if (wv == kPipeLoadWave) {
+      if (k2 < nloc) {
+        pipe_dma(S.buf[k2 % kPipeBufs], a, g + k2 * G, ioff, ilen, lane);
+        load_info(k2 + 1);
+      }
+      ST.hit(4);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+2 (read next phase)
+      ST.hit(6);
+    } else if (it >= 0) {
+      PipeBuf& C = S.buf[(uint32_t)it % kPipeBufs];
+      const uint32_t tc = g + (uint32_t)it * G;
+      if (wv == 1) {
+        pipe_lookback(C, a, tc, G, tinc, lbv, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&S.ready, (uint32_t)it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ST.hit(1);
+        if (k1 < nloc) {
+          // the other workgroups publish A(tile it+1's predecessors) about when this
+          // workgroup's wave 0 publishes A(tile it+1): issue the look-back loads after that
           uint32_t spins = 0;
-          while (__hip_atomic_load(&S.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)it + 1) {
+          while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 24)) break;
           }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          pipe_lookback_issue(a, tc + G, G, lbv, lane);
+          pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kPipeCopyWaves);
         }
-        PSTAMP(1);
-        if (a.write) pipe_copy(C, a, ct);
-        PSTAMP(7);
-      }
-    } else {  // wave 0
-      if (k1 < nloc) {
-        const uint32_t want = (uint32_t)kPipeCopyWaves * (k1 + 1);
+      } else {
         uint32_t spins = 0;
-        while (__hip_atomic_load(&S.staged, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+        while (__hip_atomic_load(&S.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)it + 1) {
           __builtin_amdgcn_s_sleep(1);
           if (++spins > (1u << 24)) break;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        PSTAMP(2);
-        pipe_walk(S.buf[k1 & 1], a, g + k1 * G, lane);
-        PSTAMP(3);
+        ST.hit(0);
+        if (a.write) pipe_copy(C, a, wv - kPipeCopyWave0, lane);
+        if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ST.hit(7);
       }
     }
-    __syncthreads();
-#ifdef MTBLX_STAMPS
-    if (wv == 0) { PSTAMP(6); ++ntl; }
-    else PSTAMP(5);
-#endif
+    raw_barrier();
+    if (wv == 0) { ST.hit(4); ++ntl; }
+    else if (wv == kPipeCopyWave0) ST.hit(5);
+    else if (wv == kPipeLoadWave) ST.hit(6);
+    else ST.hit(1);
   }
+  // retire this wave's outstanding global stores before the workgroup ends
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef MTBLX_STAMPS
-  // wave 0: [2] wait staged, [3] walk, [6] barrier.  wave 1: [0] stage, [1] look-back,
-  // [7] copy, [5] barrier.  Summed over workgroups (lane 0 of waves 0 and 1).
-  if (lane == 0 && a.dbg && wv <= 1) {
+  // wave 0: [2] trailers + walk loop, [3] scans + publish ([4] gets its barrier wait, mixed
+  // with the loader's).  wave 1: [1] look-back (+ barrier).  loader: [4] DMA issue, [6] DMA
+  // wait + barrier.  first copy wave: [0] wait ready, [7] copy, [5] barrier.  Summed over
+  // workgroups (lane 0).
+  if (lane == 0 && a.dbg && wv <= kPipeCopyWave0) {
     for (int k = 0; k < 8; ++k) {
-      const bool mine = (wv == 0) ? (k == 2 || k == 3 || k == 6) : (k == 0 || k == 1 || k == 7 || k == 5);
-      if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)tacc[k]);
+      const bool mine = (wv == 0) ? (k == 2 || k == 3) : (wv == 1) ? (k == 1) : (wv == kPipeLoadWave) ? (k == 4 || k == 6) : (k == 0 || k == 5 || k == 7);
+      if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)ST.acc[k]);
     }
     if (wv == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 8), (unsigned long long)ntl);
   }
+#else
+  (void)ntl;
 #endif
 }
 

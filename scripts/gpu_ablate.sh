@@ -11,6 +11,6 @@ except Exception: print(l[-300:])"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit
 if [ "${SKIP_TESTS:-0}" != 1 ]; then run gpu_tests 600 python -m pytest tests -m gpu -x -q; tail -2 gpurun_out/gpu_tests.log; grep -q " passed" gpurun_out/gpu_tests.log && ! grep -q "failed" gpurun_out/gpu_tests.log || { echo "TESTS FAILED: stop"; exit 1; }; fi
 run bench 300 python bench.py --no-cpu-baseline
 run stamps 300 python bench.py --no-cpu-baseline --stamps
-for v in nokey noval nocopy; do
+for v in ${ABL:-nokey noval nocopy}; do
   run abl_$v 300 python bench.py --no-cpu-baseline --stamps --lib oxidized-mtbl_amd/build/libmtblx_$v.so
 done

@@ -201,10 +201,11 @@ def main():
                      "kernel": kernel, "alg_bytes_per_launch": int(alg_bytes)},
     }
     if args.stamps:
-        d = ws.buf[:72].cpu().numpy().view(np.uint64).astype(np.float64)
+        d = ws.buf[:128].cpu().numpy().view(np.uint64).astype(np.float64)
         names = ["copy:wait-ready", "w1:lookback+barrier", "w0:walk-loop", "w0:scan-publish",
-                 "w2:dma-issue (+w0 barrier)", "copy:barrier", "w2:dma-wait+barrier", "copy:copy"]
-        ntl = max(d[8], 1)
+                 "loader:dma-issue", "copy:barrier", "loader:dma-wait", "copy:copy", "w0:barrier",
+                 "w0:trailers", "w0:interval-setup", "-", "loader:barrier"]
+        ntl = max(d[15], 1)
         res["phase_cycles_per_tile"] = {n: round(d[k] / ntl, 1) for k, n in enumerate(names)}
         res["stamps_note"] = "diagnostic build (s_memtime, thread 0 of each workgroup), last step only; shares, not time"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

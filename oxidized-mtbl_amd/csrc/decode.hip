@@ -906,7 +906,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 // diagnostic per-phase cycle stamps (MTBLX_STAMPS builds only; lane 0 of a wave)
 struct Stamps {
 #ifdef MTBLX_STAMPS
-  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t prev = 0;
   __device__ __forceinline__ void init() { prev = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void hit(int k) {
@@ -920,9 +920,10 @@ struct Stamps {
 #endif
 };
 
-constexpr int kPipeThreads = 768;
-constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loader (issues no stores)
-constexpr int kPipeCopyWave0 = 3;                                        // waves 3..11 copy
+constexpr int kPipeThreads = 1024;
+constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loaders (issue no stores)
+constexpr int kPipeLoadWaves = 2;                                        // waves 2..3
+constexpr int kPipeCopyWave0 = kPipeLoadWave + kPipeLoadWaves;           // waves 4..15 copy
 constexpr int kPipeCopyWaves = kPipeThreads / kWave - kPipeCopyWave0;
 constexpr int kPipeRows = kPipeCopyWaves * (kWave / 16);                 // intervals per copy round
 constexpr int kPipeTB = 49152;
@@ -1010,15 +1011,21 @@ __device__ __forceinline__ void key_scan_step(uint32_t& m, uint4& W, uint32_t q0
   m = mL < m ? mL : m;
 }
 
-// Walk of restart interval [s, e) of a staged block: the loop-carried chain is only
-// p -> LDS header read -> p'.  The next header's read is issued before this entry's slot
-// store.  1-byte-varint headers; false on anything else (the caller then runs the exact
-// walk_careful_pos).  Preconditions as walk_interval (regular blocks).
-__device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t R, uint32_t s,
-                                         uint32_t e, uint32_t slot0, uint32_t& cnt, uint32_t& kb, uint32_t& vb) {
+// Walk of restart interval [s, e) of a staged block.  The loop-carried chain is only
+// p -> LDS header read -> p' (about a dozen VALU ops per entry); every validity check is
+// folded into accumulators that are tested once at the end:
+//  - any header byte >= 128 (multi-byte varint)      -> `orf`
+//  - shared > previous key length (first: 0)          -> `badsh`
+//  - an entry running past R (p is monotonic, so the walk then ends with p != e)
+//  - more than 16 entries                             -> loop bound, p != e
+// Reads past R stay inside the LDS allocation (at most 513 bytes past the last header)
+// and are never used when the walk is rejected; the caller then runs the exact
+// walk_careful_pos.  Preconditions as walk_interval (regular blocks).
+__device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t s, uint32_t e,
+                                         uint32_t slot0, uint32_t& cnt, uint32_t& kb, uint32_t& vb) {
   cnt = kb = vb = 0;
-  if (!(s < e && e <= R)) return false;
-  uint32_t p = s, prevlen = 0, bad = 0;
+  if (!(s < e)) return false;
+  uint32_t p = s, prevlen = 0, orf = 0, badsh = 0, ssh = 0, svl = 0, c = 0;
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   uint32_t ad = bo + p;
   uint32_t w0 = st32[ad >> 2], w1 = st32[(ad >> 2) + 1];
@@ -1026,22 +1033,22 @@ __device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, ui
     const uint32_t hw = __builtin_amdgcn_alignbit(w1, w0, (ad & 3u) * 8u);
     const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
     const uint32_t np = p + 3u + ns + vl;
-    bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R) | (uint32_t)(cnt >= (uint32_t)kP2Spi);
-    // np <= R + 257 stays inside the stage buffer (bo + R <= TB - 48 + ...; only consumed if np < e <= R)
-    const uint32_t nad = bo + (np < e ? np : p);
-    const uint32_t n0 = st32[nad >> 2], n1 = st32[(nad >> 2) + 1];
-    if (!bad) pos[slot0 + cnt] = (uint16_t)p;
-    const uint32_t klen = sh + ns;
-    cnt += 1;
-    kb += klen;
-    vb += vl;
-    prevlen = klen;
+    ad = bo + np;
+    w0 = st32[ad >> 2];
+    w1 = st32[(ad >> 2) + 1];
+    pos[slot0 + c] = (uint16_t)p;
+    orf |= hw;
+    badsh |= (uint32_t)(sh > prevlen);
+    prevlen = sh + ns;
+    ssh += sh;
+    svl += vl;
+    c += 1;
     p = np;
-    ad = nad;
-    w0 = n0;
-    w1 = n1;
-  } while (p < e && !bad);
-  return !bad && p == e;
+  } while (p < e && c < (uint32_t)kP2Spi);
+  cnt = c;
+  vb = svl;
+  kb = ssh + (p - s) - 3u * c - svl;   // sum(shared + non_shared): p - s = sum(3 + ns + vl)
+  return p == e && (orf & 0x808080u) == 0u && badsh == 0u;
 }
 
 // exact walk (multi-byte varint headers allowed) recording header offsets; same checks as
@@ -1086,7 +1093,7 @@ __device__ __forceinline__ bool walk_careful_pos(const uint8_t* stage, uint16_t*
 // wave 0: LDS-DMA of tile t into B (contiguous range, or one 16 B aligned slot per block).
 // (off_l, len_l) = directory entry of block `lane` of the tile (lanes < nb).
 __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t t, uint64_t off_l, uint32_t len_l,
-                                         int lane) {
+                                         int lane, uint32_t part) {
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void g_void;
   const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
@@ -1102,7 +1109,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
   if (contig) {
     // range byte x at stage offset 16 + x; wave-instruction m writes chunks [64m, 64m + 64)
     const uint32_t nch = (uint32_t)((e - r0 + 15) >> 4);
-    for (uint32_t m = 0; m * kWave < nch; ++m) {
+    for (uint32_t m = part; m * kWave < nch; m += kPipeLoadWaves) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
       if (c < nch) {
@@ -1112,7 +1119,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
           *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
       }
     }
-    if (lane < (int)nb) {
+    if (part == 0 && lane < (int)nb) {
       B.boff[lane] = (uint32_t)(16 + off_l - r0);
       B.blen[lane] = len_l;
     }
@@ -1129,7 +1136,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
         if (base + off < 16 || ((base + off) & ~15ull) < base) a0 = off;  // unaligned data base: not reached
         const uint32_t delta = (uint32_t)(off - a0);
         const uint32_t nch = (delta + L + 15u) >> 4;
-        for (uint32_t m = 0; m * kWave < nch; ++m) {
+        for (uint32_t m = part; m * kWave < nch; m += kPipeLoadWaves) {
           const uint32_t c = m * kWave + lane;
           const uint64_t go = a0 + 16ull * c;
           if (c < nch) {
@@ -1142,122 +1149,122 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
         }
         bo = so + delta;
       }
-      if (lane == 0) { B.boff[j] = bo; B.blen[j] = L; }
+      if (part == 0 && lane == 0) { B.boff[j] = bo; B.blen[j] = L; }
     }
   }
-  if (lane == 0) { B.nb = nb; B.b0 = b0; }
+  if (part == 0 && lane == 0) { B.nb = nb; B.b0 = b0; }
 }
 
 // wave 0: trailers, walk (header offsets into slots), irregular counts, interval scan,
-// block totals, publish A(t)
+// publish A(t), then the block / interval bases the copy and the look-back read.
+// Cross-lane traffic uses readlane / DPP / bpermute (no LDS round trips before the walk).
 __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_t t, int lane, Stamps& ST) {
-  const uint32_t nb = B.nb, b0 = B.b0;
-  uint32_t binc = 0;   // lane b: inclusive interval count of blocks 0..b
-  {  // trailers (Block::init, src/block.rs:16-49) + interval numbering
-    uint32_t n = 0, R = 0, ok = 0;
-    if (lane < (int)nb) {
-      const uint32_t L = B.blen[lane], bo = B.boff[lane];
-      if (bo != kNotStaged && L >= 8) {
-        n = lds_rd32(B.stage, bo + L - 4);
-        if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
-      }
+  const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
+  // trailers (Block::init, src/block.rs:16-49): lane = block
+  uint32_t n = 0, R = 0, ok = 0, L = 0, bo = kNotStaged;
+  if (lane < (int)nb) {
+    L = B.blen[lane];
+    bo = B.boff[lane];
+    if (bo != kNotStaged && L >= 8) {
+      n = lds_rd32(B.stage, bo + L - 4);
+      if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
     }
-    uint32_t incl = wave_incl_scan(ok ? n : 0u);
-    if (ok && incl > (uint32_t)kP2MaxInt) ok = 0;
-    n = ok ? n : 0;
-    incl = wave_incl_scan(n);
-    if (lane < (int)nb) {
-      B.bn[lane] = n; B.bR[lane] = R; B.bok[lane] = ok; B.bwr[lane] = 1; B.bst[lane] = MTBLX_ST_OK;
-      B.bint0[lane] = incl - n;
-    }
-    if (lane == (int)nb - 1) { B.bint0[nb] = incl; B.nint = incl; }
-    binc = incl;
   }
-  wave_sync();
-  const uint32_t nint = B.nint;
-  // block of interval f = number of blocks whose inclusive interval count is <= f
-  uint32_t jlane = 0;
-  for (uint32_t b = 0; b + 1 < nb; ++b) jlane += ((uint32_t)__builtin_amdgcn_readlane((int)binc, (int)b) <= (uint32_t)lane);
-  // walk: one lane per restart interval (nint <= kP2MaxInt <= 64)
-  uint32_t cnt = 0, kb = 0, vb = 0, jf = 0;
-  if (lane < (int)nint) {
-    const uint32_t f = lane;
-    const uint32_t j = jlane;
-    jf = j;
-    const uint32_t i = f - B.bint0[j], bo = B.boff[j], L = B.blen[j], R = B.bR[j], n = B.bn[j];
-    const uint32_t s = lds_rd32(B.stage, bo + R + 4u * i);
-    const uint32_t e = (i + 1 < n) ? lds_rd32(B.stage, bo + R + 4u * (i + 1)) : R;
-    const uint32_t slot0 = f * kP2Spi;
-    bool ok = walk_pos(B.stage, B.pos, bo, R, s, e, slot0, cnt, kb, vb);
-    if (!ok) ok = walk_careful_pos(B.stage, B.pos, bo, L, R, s, e, slot0, cnt, kb, vb);
-    B.iraw[f] = (uint8_t)(cnt < 255u ? cnt : 255u);
-    B.iblk[f] = (uint8_t)j;
-    if (!ok) B.bok[j] = 0;
+  uint32_t incl = wave_incl_scan(ok ? n : 0u);
+  if (ok && incl > (uint32_t)kP2MaxInt) ok = 0;
+  n = ok ? n : 0;
+  incl = wave_incl_scan(n);                   // lane b: intervals of blocks 0..b
+  const uint32_t bint0 = incl - n;
+  const uint32_t nint = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)nb - 1);
+  // interval f = lane: its block j and that block's fields
+  uint32_t j = 0;
+  for (uint32_t b = 0; b + 1 < nb; ++b) j += ((uint32_t)__builtin_amdgcn_readlane((int)incl, (int)b) <= (uint32_t)lane);
+  const int js = (int)j;
+  const uint32_t jbo = (uint32_t)__shfl((int)bo, js, kWave), jR = (uint32_t)__shfl((int)R, js, kWave);
+  const uint32_t jn = (uint32_t)__shfl((int)n, js, kWave), jb0 = (uint32_t)__shfl((int)bint0, js, kWave);
+  const uint32_t jL = (uint32_t)__shfl((int)L, js, kWave);
+  ST.hit(9);
+  const bool fl = (uint32_t)lane < nint;
+  uint32_t cnt = 0, kb = 0, vb = 0;
+  bool wok = false;
+  if (fl) {
+    const uint32_t i = (uint32_t)lane - jb0;
+    const uint32_t s = lds_rd32(B.stage, jbo + jR + 4u * i);
+    const uint32_t e = (i + 1 < jn) ? lds_rd32(B.stage, jbo + jR + 4u * (i + 1)) : jR;
+    ST.hit(10);
+    const uint32_t slot0 = (uint32_t)lane * kP2Spi;
+    wok = e <= jR && walk_pos(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb);
+    if (!wok) wok = walk_careful_pos(B.stage, B.pos, jbo, jL, jR, s, e, slot0, cnt, kb, vb);
+    B.iraw[lane] = (uint8_t)(cnt < 255u ? cnt : 255u);
+    B.iblk[lane] = (uint8_t)j;
   }
-  wave_sync();
   ST.hit(2);
-  // irregular blocks: exact serial count (generic path, lane per block)
-  if (lane < (int)nb && !B.bok[lane]) {
-    const uint32_t j = lane, bo = B.boff[j], L = B.blen[j];
-    const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + j]);
-    GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
-    B.bcnt[j] = o.nrec; B.bkb[j] = (uint32_t)o.kb; B.bvb[j] = (uint32_t)o.vb; B.bst[j] = o.st;
+  // a block with a rejected interval is irregular
+  const uint64_t failm = __ballot(fl && !wok);
+  {
+    const uint64_t hi = incl >= 64u ? ~0ull : ((1ull << incl) - 1ull);
+    const uint64_t lo = (1ull << bint0) - 1ull;
+    if (ok && (failm & hi & ~lo) != 0ull) ok = 0;
   }
-  wave_sync();
+  const bool jok = __shfl((int)ok, js, kWave) != 0;
+  // irregular blocks: exact serial count (generic path, lane per block)
+  uint32_t gc = 0, gk = 0, gv = 0;
+  int32_t gst = MTBLX_ST_OK;
+  if (lane < (int)nb && !ok) {
+    const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + lane]);
+    const GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
+    gc = o.nrec; gk = (uint32_t)o.kb; gv = (uint32_t)o.vb; gst = o.st;
+  }
   // interval scan over regular blocks (one interval per lane)
-  const bool reg = lane < (int)nint && B.bok[jf];
+  const bool reg = fl && jok;
   const uint32_t c = reg ? cnt : 0u, k = reg ? kb : 0u, v = reg ? vb : 0u;
   const uint32_t ic = wave_incl_scan(c), ik = wave_incl_scan(k), iv = wave_incl_scan(v);
-  // block totals (regular: differences of the interval scan) -> block bases.
-  // Cross-lane reads are done by every lane (uniform control flow), results used after.
-  {
-    const uint32_t fa = lane < (int)nb ? B.bint0[lane] : 0u, fb = lane < (int)nb ? B.bint0[lane + 1] : 0u;
-    const int sa = fa ? (int)fa - 1 : 0, sb = fb ? (int)fb - 1 : 0;
-    // every lane must execute the permutes (a disabled source lane reads as 0)
-    const uint32_t ea0 = (uint32_t)__shfl(ic, sa, kWave), eb0 = (uint32_t)__shfl(ic, sb, kWave);
-    const uint32_t ka0 = (uint32_t)__shfl(ik, sa, kWave), kb0 = (uint32_t)__shfl(ik, sb, kWave);
-    const uint32_t va0 = (uint32_t)__shfl(iv, sa, kWave), vb0 = (uint32_t)__shfl(iv, sb, kWave);
-    const uint32_t ea = fa ? ea0 : 0u, ka = fa ? ka0 : 0u, va = fa ? va0 : 0u;
-    const uint32_t eb = fb ? eb0 : 0u, kb2 = fb ? kb0 : 0u, vb2 = fb ? vb0 : 0u;
-    uint32_t bc = 0, bk = 0, bv = 0;
-    if (lane < (int)nb) {
-      if (B.bok[lane]) {
-        bc = eb - ea; bk = kb2 - ka; bv = vb2 - va;
-      } else {
-        bc = B.bcnt[lane]; bk = B.bkb[lane]; bv = B.bvb[lane];
-      }
+  // tile totals -> publish A(t) first (other workgroups' look-back waits on it)
+  const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane((int)ic, 63) + wave_sum32(gc);
+  const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)ik, 63) + wave_sum32(gk);
+  const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)iv, 63) + wave_sum32(gv);
+  if (lane == 0) {
+    if (tk >= kField) {
+      __hip_atomic_store(&a.lbx[t], (uint64_t)tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
-    const uint32_t jc = wave_incl_scan(bc), jk = wave_incl_scan(bk), jv = wave_incl_scan(bv);
-    if (lane < (int)nb) {
-      B.bcnt[lane] = bc; B.bkb[lane] = bk; B.bvb[lane] = bv;
-      B.brb[lane] = jc - bc; B.bkbb[lane] = jk - bk; B.bvbb[lane] = jv - bv;
-    }
-    const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane((int)jc, (int)nb - 1);
-    const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)jk, (int)nb - 1);
-    const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)jv, (int)nb - 1);
-    if (lane == 0) {
-      B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
-      if (tk >= kField) {
-        __hip_atomic_store(&a.lbx[t], (uint64_t)tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      }
-      __hip_atomic_store(&a.lb[t], pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.lb[t], pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
+    B.nint = nint;
+  }
+  // block totals (regular: differences of the interval scan) and tile-relative block bases.
+  // Every lane executes the permutes (a disabled source lane reads as 0).
+  const int ea_l = bint0 ? (int)bint0 - 1 : 0, eb_l = incl ? (int)incl - 1 : 0;
+  const uint32_t ea0 = (uint32_t)__shfl((int)ic, ea_l, kWave), eb0 = (uint32_t)__shfl((int)ic, eb_l, kWave);
+  const uint32_t ka0 = (uint32_t)__shfl((int)ik, ea_l, kWave), kb0 = (uint32_t)__shfl((int)ik, eb_l, kWave);
+  const uint32_t va0 = (uint32_t)__shfl((int)iv, ea_l, kWave), vb0 = (uint32_t)__shfl((int)iv, eb_l, kWave);
+  uint32_t bc = 0, bk = 0, bv = 0;
+  if (lane < (int)nb) {
+    if (ok) {
+      bc = (incl ? eb0 : 0u) - (bint0 ? ea0 : 0u);
+      bk = (incl ? kb0 : 0u) - (bint0 ? ka0 : 0u);
+      bv = (incl ? vb0 : 0u) - (bint0 ? va0 : 0u);
+    } else {
+      bc = gc; bk = gk; bv = gv;
     }
   }
-  wave_sync();
+  const uint32_t jc = wave_incl_scan(bc), jk = wave_incl_scan(bk), jv = wave_incl_scan(bv);
+  const uint32_t brb = jc - bc, bkbb = jk - bk, bvbb = jv - bv;
+  if (lane < (int)nb) {
+    B.bok[lane] = ok; B.bwr[lane] = 1; B.bst[lane] = ok ? MTBLX_ST_OK : gst;
+    B.bcnt[lane] = bc; B.bkb[lane] = bk; B.bvb[lane] = bv;
+    B.brb[lane] = brb; B.bkbb[lane] = bkbb; B.bvbb[lane] = bvbb;
+  }
   // tile-relative interval bases (record index, key byte, value byte)
-  {
-    const uint32_t fa = lane < (int)nint ? B.bint0[jf] : 0u;
-    const int sa = fa ? (int)fa - 1 : 0;
-    const uint32_t e0r = (uint32_t)__shfl(ic, sa, kWave), k0r = (uint32_t)__shfl(ik, sa, kWave),
-                   v0r = (uint32_t)__shfl(iv, sa, kWave);
-    if (lane < (int)nint) {
-      const uint32_t j = jf;
-      const uint32_t e0 = fa ? e0r : 0u, k0 = fa ? k0r : 0u, v0 = fa ? v0r : 0u;
-      B.icnt[lane] = B.brb[j] + (ic - c) - e0;
-      B.ikb[lane] = B.bkbb[j] + (ik - k) - k0;
-      B.ivb[lane] = B.bvbb[j] + (iv - v) - v0;
-    }
+  const uint32_t jea = (uint32_t)__shfl((int)(bint0 ? ea0 : 0u), js, kWave);
+  const uint32_t jka = (uint32_t)__shfl((int)(bint0 ? ka0 : 0u), js, kWave);
+  const uint32_t jva = (uint32_t)__shfl((int)(bint0 ? va0 : 0u), js, kWave);
+  const uint32_t jrb = (uint32_t)__shfl((int)brb, js, kWave), jkb = (uint32_t)__shfl((int)bkbb, js, kWave),
+                 jvb = (uint32_t)__shfl((int)bvbb, js, kWave);
+  if (fl) {
+    B.icnt[lane] = jrb + (ic - c) - jea;
+    B.ikb[lane] = jkb + (ik - k) - jka;
+    B.ivb[lane] = jvb + (iv - v) - jva;
   }
 }
 
@@ -1473,9 +1480,12 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     ioff = a.blk_off[b0 + j];
     ilen = a.blk_len[b0 + j];
   };
-  if (wv == kPipeLoadWave) {
+  // loaders split every tile's DMA pieces (even / odd 1 KiB pieces)
+  const bool loader = wv >= kPipeLoadWave && wv < kPipeLoadWave + kPipeLoadWaves;
+  const uint32_t part = (uint32_t)(wv - kPipeLoadWave);
+  if (loader) {
     load_info(0);
-    if (nloc > 0) pipe_dma(S.buf[0], a, g, ioff, ilen, lane);
+    if (nloc > 0) pipe_dma(S.buf[0], a, g, ioff, ilen, lane, part);
     load_info(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (wv == 1) {
@@ -1494,9 +1504,9 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       ST.hit(3);
-    } else if (wv == kPipeLoadWave) {
+    } else if (loader) {
       if (k2 < nloc) {
-        pipe_dma(S.buf[k2 % kPipeBufs], a, g + k2 * G, ioff, ilen, lane);
+        pipe_dma(S.buf[k2 % kPipeBufs], a, g + k2 * G, ioff, ilen, lane, part);
         load_info(k2 + 1);
       }
       ST.hit(4);
@@ -1535,24 +1545,23 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       }
     }
     raw_barrier();
-    if (wv == 0) { ST.hit(4); ++ntl; }
+    if (wv == 0) { ST.hit(8); ++ntl; }
     else if (wv == kPipeCopyWave0) ST.hit(5);
-    else if (wv == kPipeLoadWave) ST.hit(6);
+    else if (loader) ST.hit(12);
     else ST.hit(1);
   }
   // retire this wave's outstanding global stores before the workgroup ends
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef MTBLX_STAMPS
-  // wave 0: [2] trailers + walk loop, [3] scans + publish ([4] gets its barrier wait, mixed
-  // with the loader's).  wave 1: [1] look-back (+ barrier).  loader: [4] DMA issue, [6] DMA
-  // wait + barrier.  first copy wave: [0] wait ready, [7] copy, [5] barrier.  Summed over
-  // workgroups (lane 0).
-  if (lane == 0 && a.dbg && wv <= kPipeCopyWave0) {
-    for (int k = 0; k < 8; ++k) {
-      const bool mine = (wv == 0) ? (k == 2 || k == 3) : (wv == 1) ? (k == 1) : (wv == kPipeLoadWave) ? (k == 4 || k == 6) : (k == 0 || k == 5 || k == 7);
+  // wave 0: [2] trailers + walk loop, [3] scans + publish, [8] barrier.  wave 1: [1]
+  // look-back (+ barrier).  first loader: [4] DMA issue, [6] DMA wait + barrier.  first copy
+  // wave: [0] wait ready, [7] copy, [5] barrier.  Summed over workgroups (lane 0); [15] tiles.
+  if (lane == 0 && a.dbg && (wv <= kPipeLoadWave || wv == kPipeCopyWave0)) {
+    for (int k = 0; k < 13; ++k) {
+      const bool mine = (wv == 0) ? (k == 2 || k == 3 || k == 8 || k == 9 || k == 10) : (wv == 1) ? (k == 1) : loader ? (k == 4 || k == 6 || k == 11 || k == 12) : (k == 0 || k == 5 || k == 7);
       if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)ST.acc[k]);
     }
-    if (wv == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 8), (unsigned long long)ntl);
+    if (wv == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 15), (unsigned long long)ntl);
   }
 #else
   (void)ntl;

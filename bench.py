@@ -78,6 +78,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=100_000)
+    ap.add_argument("--block-size", type=int, default=4096,
+                    help="diagnostic: writer block size (cfg2 = 4096; cfg4 also uses 16384 / 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lib", default=None, help="diagnostic: alternative libmtblx build (ablations)")
@@ -90,6 +92,8 @@ def main():
 
     if args.stamps:
         os.environ["MTBLX_LIB"] = args.lib or os.path.join(ROOT, "oxidized-mtbl_amd", "mtblx", "libmtblx_stamps.so")
+    elif args.lib:
+        os.environ["MTBLX_LIB"] = args.lib
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -102,7 +106,7 @@ def main():
     from mtblx import codec, synth
 
     t = time.time()
-    data, off, ln = synth.cfg2_file(args.blocks, seed=synth.SEED_CFG2 + rank)
+    data, off, ln = synth.cfg2_file(args.blocks, block_size=args.block_size, seed=synth.SEED_CFG2 + rank)
     exp_nrec = int(synth.cfg2_file.last_block_nrec.sum(dtype=np.uint64))  # records the Writer put in these blocks
     log(f"[rank {rank}] generated {off.size} blocks / {data.size / 2**20:.1f} MiB in {time.time() - t:.1f}s")
     batch = codec.DeviceBatch.from_host(data, off, ln)
@@ -190,8 +194,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded cfg2 generator, product Writer)",
-        "config": {"workload": "cfg2: 4 KiB blocks, 16 B keys / 64 B values, restart_interval=16, "
-                               "compression=none, device-resident decode",
+        "config": {"workload": (f"cfg2: 4 KiB blocks" if args.block_size == 4096 else
+                                f"cfg2 scheme with {args.block_size // 1024} KiB blocks (cfg4 leg)") +
+                               ", 16 B keys / 64 B values, restart_interval=16, compression=none, device-resident decode",
                    "blocks_per_gpu": int(batch.nblk), "block_bytes_per_gpu": block_bytes,
                    "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
                    "parallelism": f"block-sharded x{world}, no collective"},

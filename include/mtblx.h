@@ -15,6 +15,10 @@
  *  - "device" = memory the kernels read/write (hipMalloc'd or host-pinned mapped).
  *  - the library never allocates on a hot call: the caller passes every buffer,
  *    including the workspace sized by mtblx_decode_workspace_bytes().
+ *  - the workspace carries state from call to call (a launch counter and the per-tile
+ *    look-back words of both launch parities), so a call needs no fill: ZERO-FILL IT ONCE
+ *    after allocating it, then reuse it for any sequence of batches of at most the
+ *    nblk it was sized for.  One workspace serves one call at a time (per stream).
  *  - calls are asynchronous on `stream` and re-entrant (no global mutable state).
  *  - return value: MTBLX_OK or a negative MTBLX_E_* (argument / HIP launch errors).
  *    Per-block outcomes are reported in `status[]` (MTBLX_ST_*), never by aborting.
@@ -29,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MTBLX_ABI_VERSION 1
+#define MTBLX_ABI_VERSION 2
 
 /* ---- API return codes ---- */
 #define MTBLX_OK 0
@@ -78,14 +82,16 @@ typedef struct mtblx_decoded {
   uint64_t keys_cap;
   uint8_t* vals;        /* device [vals_cap] */
   uint64_t vals_cap;
-  uint64_t* totals;     /* device [4]: records, key bytes, value bytes, flags (bit0 = overflow) */
+  uint64_t* totals;     /* device [4]: records, key bytes, value bytes, flags (bit0 = overflow,
+                           bit1 = look-back timeout: outputs not trustworthy) */
 } mtblx_decoded;
 
 /* Library identity / device check. */
 int mtblx_abi_version(void);
 int mtblx_device_ok(void); /* 1 if the current HIP device is gfx950, else 0 */
 
-/* Workspace bytes needed by mtblx_decode_blocks for a batch of nblk blocks. */
+/* Workspace bytes needed by mtblx_decode_blocks for a batch of up to nblk blocks
+ * (zero-fill once before first use, see above). */
 size_t mtblx_decode_workspace_bytes(uint32_t nblk);
 
 /* Decode every block of `in` into `out` (replaces Block::init + the BlockIter scan

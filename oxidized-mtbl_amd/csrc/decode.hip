@@ -315,11 +315,62 @@ struct TileArgs {
   uint8_t* vals;
   uint64_t vals_cap;
   uint64_t* totals;
-  uint64_t* lb;     // [ntiles] packed tile aggregates, zeroed before launch
-  uint64_t* lbx;    // [ntiles] exact key bytes when the packed field saturates
+  uint64_t* lbw;    // workspace tile entries: 3 u64 per tile {agg parity 0, agg parity 1, exact key bytes}
+  struct WsHdr* hdr;
   uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
   int write;
+  // set at kernel start from the workspace header (ws_begin)
+  uint32_t par;     // launch parity: aggregates live in slot `par` of each tile entry
+  uint32_t hw_other;
 };
+
+// Workspace header (byte 128 of the workspace).  The workspace carries state from call to
+// call so no fill is needed per call: it must be zero-filled once after allocation.
+//  - epoch: launch counter; parity = epoch & 1 selects the aggregate slot of this launch
+//  - hw[p]: most tiles any launch of parity p used (slots to clear before they are reused)
+//  - done: workgroups finished in this launch; the last one publishes totals[3], resets
+//    the flags and done, bumps hw and epoch
+struct WsHdr {
+  uint32_t epoch;
+  uint32_t done;
+  uint32_t hw[2];
+  unsigned long long flags;   // bit0 overflow, bit1 look-back timeout (-> totals[3])
+};
+
+__device__ __forceinline__ uint64_t* lb_slot(const TileArgs& a, uint64_t t) { return a.lbw + 3 * t + a.par; }
+__device__ __forceinline__ uint64_t* lbx_slot(const TileArgs& a, uint64_t t) { return a.lbw + 3 * t + 2; }
+
+// kernel prologue: pick the parity, clear the other parity's slots of every tile a previous
+// launch of that parity used (the next launch uses them)
+__device__ __forceinline__ void ws_begin(TileArgs& a) {
+  const uint32_t ep = __hip_atomic_load(&a.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  a.par = ep & 1u;
+  a.hw_other = __hip_atomic_load(&a.hdr->hw[a.par ^ 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n = blockDim.x, tid = threadIdx.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * n + tid; t < a.hw_other; t += (uint64_t)gridDim.x * n)
+    a.lbw[3 * t + (a.par ^ 1u)] = 0;
+}
+
+__device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bit) { atomicOr(&a.hdr->flags, bit); }
+
+// kernel epilogue (every thread): the last workgroup to finish closes the launch
+__device__ __forceinline__ void ws_end(const TileArgs& a) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t old = __hip_atomic_fetch_add(&a.hdr->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const unsigned long long f = __hip_atomic_load(&a.hdr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.totals[3] = f;
+      __hip_atomic_store(&a.hdr->flags, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t h = __hip_atomic_load(&a.hdr->hw[a.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.ntiles > h) __hip_atomic_store(&a.hdr->hw[a.par], a.ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&a.hdr->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 
 // Contiguous range of tile t: [r0, r1) of the data buffer (r0 16-aligned), or r1 = 0 if the
@@ -483,6 +534,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
   __shared__ TileLds<C> S;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t G = gridDim.x;
+  ws_begin(a);
 #ifdef MTBLX_STAMPS
   // diagnostic build only: per-phase cycles of thread 0 (s_memtime), summed over tiles
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime(), ntl = 0;
@@ -678,10 +730,10 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
     const uint32_t agg_r = S.ttot[0], agg_k = S.ttot[1], agg_v = S.ttot[2];
     if (tid == 0) {
       if (agg_k >= kField) {
-        __hip_atomic_store(&a.lbx[t], (uint64_t)agg_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lbx_slot(a, t), (uint64_t)agg_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       }
-      __hip_atomic_store(&a.lb[t], pack_agg(agg_r, agg_k, agg_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(lb_slot(a, t), pack_agg(agg_r, agg_k, agg_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t lo = (t >= G) ? t - G + 1 : 0;   // window of predecessors [lo, t)
     uint64_t lw[kMaxLookbackLoads];
@@ -689,7 +741,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
     for (int m = 0; m < kMaxLookbackLoads; ++m) {
       const int64_t i = (int64_t)t - 1 - tid - (int64_t)m * kThreads;
       lw[m] = kReady;  // outside the window: contributes 0
-      if (i >= (int64_t)lo) lw[m] = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (i >= (int64_t)lo) lw[m] = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     STAMP(3);
 
@@ -746,7 +798,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         uint32_t spins = 0;
         while (!(w & kReady)) {
           __builtin_amdgcn_s_sleep(2);
-          w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          w = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (++spins > (1u << 22)) { timeout = true; w = kReady; }
         }
         if (i >= (int64_t)lo) {
@@ -755,12 +807,12 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
           uint64_t kk = w & kField;
           if (kk == kField) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            kk = __hip_atomic_load(&a.lbx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            kk = __hip_atomic_load(lbx_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           sk += kk;
         }
       }
-      if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 2ull);
+      if (timeout) ws_flag(a, 2ull);
       // per-thread sums are < 2^23 (4 tiles x 21-bit fields) unless a key field saturated
       sr = wave_sum32((uint32_t)sr);
       sv = wave_sum32((uint32_t)sv);
@@ -797,7 +849,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
       if (a.write && (rb + S.bcnt[j] > a.rec_cap || kb + S.bkb[j] > a.keys_cap || vb + S.bvb[j] > a.vals_cap)) {
         st = MTBLX_ST_OVERFLOW;
         S.bwr[j] = 0;
-        atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 1ull);
+        ws_flag(a, 1ull);
       }
       a.status[b] = st;
     }
@@ -872,6 +924,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
     }
     __syncthreads();
   }
+  ws_end(a);
 #ifdef MTBLX_STAMPS
   if (tid == 0 && a.dbg) {
     for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)tacc[k]);
@@ -1225,10 +1278,10 @@ __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_
   const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)iv, 63) + wave_sum32(gv);
   if (lane == 0) {
     if (tk >= kField) {
-      __hip_atomic_store(&a.lbx[t], (uint64_t)tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(lbx_slot(a, t), (uint64_t)tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
-    __hip_atomic_store(&a.lb[t], pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(lb_slot(a, t), pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
     B.nint = nint;
   }
@@ -1276,7 +1329,7 @@ __device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t 
 #pragma unroll
   for (int m = 0; m < kMaxLookbackLoads; ++m) {
     const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
-    lbv[m] = (i >= lo) ? __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kReady;
+    lbv[m] = (i >= lo) ? __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kReady;
   }
 }
 
@@ -1300,7 +1353,7 @@ __device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t
 #pragma unroll
     for (int m = 0; m < kMaxLookbackLoads; ++m) {
       const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
-      if (i >= lo && !(lbv[m] & kReady)) lbv[m] = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (i >= lo && !(lbv[m] & kReady)) lbv[m] = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1320,7 +1373,7 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uin
     uint32_t spins = 0;
     while (!(w & kReady)) {
       __builtin_amdgcn_s_sleep(2);
-      w = __hip_atomic_load(&a.lb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (++spins > (1u << 22)) { timeout = true; w = kReady; }
     }
     if (i < lo) continue;
@@ -1329,11 +1382,11 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uin
     uint64_t kk = w & kField;
     if (kk == kField) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      kk = __hip_atomic_load(&a.lbx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      kk = __hip_atomic_load(lbx_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     sk += kk;
   }
-  if (timeout) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 2ull);
+  if (timeout) ws_flag(a, 2ull);
   sr = wave_sum32((uint32_t)sr);
   sv = wave_sum32((uint32_t)sv);
   if (__ballot(sk >= (1ull << 24)) == 0ull) sk = wave_sum32((uint32_t)sk);
@@ -1357,102 +1410,159 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uin
     if (a.write && (rb + B.bcnt[j] > a.rec_cap || kb + B.bkb[j] > a.keys_cap || vb + B.bvb[j] > a.vals_cap)) {
       st = MTBLX_ST_OVERFLOW;
       B.bwr[j] = 0;
-      atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 3), 1ull);
+      ws_flag(a, 1ull);
     }
     a.status[b] = st;
   }
 }
 
-// waves 2..7: record pass + copy of one tile.  Copy wave cw owns 16-lane rows
+// Copy waves: record pass + copy of one tile.  Copy wave cw owns 16-lane rows
 // 4 cw .. 4 cw + 3 of each round; row = restart interval, lane k of the row = entry k.
-__device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int cw, int lane) {
+// Each round is split into a prepare part (LDS + DPP only: headers, row scans, first key
+// plane) and an emit part (global stores); the first round is prepared before the
+// look-back of the tile is ready, overlapping the wait.
+struct CopyRow {
+  uint32_t f, j, k, bo, sh, ns, vl, klen, ks, vs, sp, m0;
+  uint4 W0;          // key bytes [0, 16) of the entry (valid for live entries)
+  bool fv, live;
+};
+
+__device__ __forceinline__ CopyRow copy_prepare(const PipeBuf& B, uint32_t fb, int lane) {
+  CopyRow r;
+  const uint32_t nint = B.nint;
+  r.k = lane & 15;
+  r.f = fb + (lane >> 4);
+  r.fv = r.f < nint;
+  r.j = r.fv ? B.iblk[r.f] : 0u;
+  r.live = r.fv && r.k < B.iraw[r.f] && B.bok[r.j];
+  r.bo = B.boff[r.j];
+  const uint32_t p = r.live ? B.pos[r.f * kP2Spi + r.k] : 0u;
+  uint32_t sh = 0, ns = 0, vl = 0, h = 3;
+  if (r.live) {  // decode_entry (src/block.rs:216-238) at a header the walk validated
+    const uint32_t hw = lds_rd32(B.stage, r.bo + p);
+    sh = hw & 0xffu; ns = (hw >> 8) & 0xffu; vl = (hw >> 16) & 0xffu;
+    if ((hw & 0x808080u) != 0u) {
+      const uint4 W = lds_win16(B.stage, r.bo + p);
+      const uint32_t l0 = dec32(W, 0, 16, sh);
+      const uint32_t l1 = dec32(W, l0, 16, ns);
+      const uint32_t l2 = dec32(W, l0 + l1, 16, vl);
+      h = l0 + l1 + l2;
+    }
+  }
+  r.sh = sh; r.ns = ns; r.vl = vl;
+  r.klen = sh + ns;
+  const uint32_t kx = row_excl_scan(r.klen), vx = row_excl_scan(vl);
+  r.ks = (r.fv ? B.ikb[r.f] : 0u) + kx;
+  r.vs = (r.fv ? B.ivb[r.f] : 0u) + vx;
+  r.sp = r.bo + p + h;   // stage offset of the key suffix
+#ifndef MTBLX_ABL_NOKEY
+  // first key plane (bytes 0..15): row scan of the truncate-then-append operator
+  const bool own = r.live && sh < 16u && r.klen > 0u;
+  uint4 W = own ? lds_win16(B.stage, r.sp - sh) : make_uint4(0, 0, 0, 0);
+  uint32_t m = sh;
+  key_scan_step<1>(m, W, 0);
+  key_scan_step<2>(m, W, 0);
+  key_scan_step<4>(m, W, 0);
+  key_scan_step<8>(m, W, 0);
+  r.W0 = W;
+  r.m0 = m;
+#endif
+  return r;
+}
+
+__device__ __forceinline__ void copy_emit(const PipeBuf& B, const TileArgs& a, const CopyRow& r, int lane) {
   const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
-  const uint32_t nint = B.nint, nb = B.nb;
-  const uint32_t k = lane & 15;
-  for (uint32_t fb = (uint32_t)cw * (kWave / 16); fb < nint; fb += kPipeRows) {   // wave-uniform
-    const uint32_t f = fb + (lane >> 4);
-    const bool fv = f < nint;
-    const uint32_t j = fv ? B.iblk[f] : 0u;
-    const bool live = fv && k < B.iraw[f] && B.bok[j] && B.bwr[j];
-    const uint32_t bo = B.boff[j];
-    const uint32_t p = live ? B.pos[f * kP2Spi + k] : 0u;
-    uint32_t sh = 0, ns = 0, vl = 0, h = 3;
-    if (live) {  // decode_entry (src/block.rs:216-238) at a header the walk validated
-      const uint32_t hw = lds_rd32(B.stage, bo + p);
-      sh = hw & 0xffu; ns = (hw >> 8) & 0xffu; vl = (hw >> 16) & 0xffu;
-      if ((hw & 0x808080u) != 0u) {
-        const uint4 W = lds_win16(B.stage, bo + p);
-        const uint32_t l0 = dec32(W, 0, 16, sh);
-        const uint32_t l1 = dec32(W, l0, 16, ns);
-        const uint32_t l2 = dec32(W, l0 + l1, 16, vl);
-        h = l0 + l1 + l2;
-      }
-    }
-    const uint32_t klen = sh + ns;
-    const uint32_t kx = row_excl_scan(klen), vx = row_excl_scan(vl);
-    const uint32_t ks = (fv ? B.ikb[f] : 0u) + kx, vs = (fv ? B.ivb[f] : 0u) + vx;
-    const uint32_t sp = bo + p + h;   // stage offset of the key suffix
-    if (live) {
-      const uint64_t gr = pr + B.icnt[f] + k;
-      a.key_end[gr] = ks + klen - B.bkbb[j];
-      a.val_end[gr] = vs + vl - B.bvbb[j];
-    }
+  const bool live = r.live && B.bwr[r.j];   // bwr may have been cleared by the look-back (overflow)
+  if (live) {
+    const uint64_t gr = pr + B.icnt[r.f] + r.k;
+    a.key_end[gr] = r.ks + r.klen - B.bkbb[r.j];
+    a.val_end[gr] = r.vs + r.vl - B.bvbb[r.j];
+  }
 #ifndef MTBLX_ABL_NOVAL
-    // values.  Fast path (wave-uniform): every live entry of this round has the same value
-    // length U, a multiple of 16 -> lane k of a row writes 16 B chunks k, k+16, ... of the
-    // interval's contiguous value range (coalesced stores).  Otherwise one entry per lane.
-    const uint64_t lv = __ballot(live);
-    if (lv != 0ull) {
-      const int l0 = __builtin_ctzll(lv);
-      const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)vl, l0);
-      const bool uni = (U % 16u) == 0u && U != 0u && __ballot(live && vl != U) == 0ull;
-      const uint32_t vsrc = sp + ns;   // stage offset of the entry's value
-      if (uni) {
-        const uint32_t cpr = U >> 4;                                  // chunks per entry
-        const bool pow2 = (cpr & (cpr - 1u)) == 0u;
-        const uint32_t cprs = (uint32_t)__builtin_ctz(cpr);
-        const uint32_t nrow = (fv && B.bok[j] && B.bwr[j]) ? (uint32_t)B.iraw[f] : 0u;
-        const uint32_t nch = nrow * cpr;
-        uint8_t* vd0 = a.vals + pv + (fv ? B.ivb[f] : 0u);
-        const int rowbase = lane & ~15;
-        for (uint32_t c = k; __ballot(c < nch) != 0ull; c += 16) {   // wave-uniform trip count
-          const bool act = c < nch;
-          const uint32_t r = act ? (pow2 ? c >> cprs : c / cpr) : 0u;
-          const uint32_t src = (uint32_t)__shfl((int)vsrc, rowbase + (int)r, kWave);
-          if (act) {
-            const uint4 w4 = lds_win16(B.stage, src + 16u * (c - r * cpr));
-            *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4.x, w4.y, w4.z, w4.w};
-          }
-        }
-      } else if (live) {
-        uint8_t* vd = a.vals + pv + vs;
-        for (uint32_t o = 0; o < vl; o += 16) {
-          const uint32_t mlen = vl - o;
-          store_bytes(vd + o, lds_win16(B.stage, vsrc + o), mlen < 16 ? mlen : 16);
+  // values.  Fast path (wave-uniform): every live entry of this round has the same value
+  // length U, a multiple of 16 -> lane k of a row writes 16 B chunks k, k+16, ... of the
+  // interval's contiguous value range (coalesced stores).  Otherwise one entry per lane.
+  const uint64_t lv = __ballot(live);
+  if (lv != 0ull) {
+    const int l0 = __builtin_ctzll(lv);
+    const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)r.vl, l0);
+    const bool uni = (U % 16u) == 0u && U != 0u && __ballot(live && r.vl != U) == 0ull;
+    const uint32_t vsrc = r.sp + r.ns;   // stage offset of the entry's value
+    if (uni) {
+      const uint32_t cpr = U >> 4;                                  // chunks per entry
+      const bool pow2 = (cpr & (cpr - 1u)) == 0u;
+      const uint32_t cprs = (uint32_t)__builtin_ctz(cpr);
+      const uint32_t nrow = (r.fv && B.bok[r.j] && B.bwr[r.j]) ? (uint32_t)B.iraw[r.f] : 0u;
+      const uint32_t nch = nrow * cpr;
+      uint8_t* vd0 = a.vals + pv + (r.fv ? B.ivb[r.f] : 0u);
+      const int rowbase = lane & ~15;
+      for (uint32_t c = r.k; __ballot(c < nch) != 0ull; c += 16) {   // wave-uniform trip count
+        const bool act = c < nch;
+        const uint32_t e = act ? (pow2 ? c >> cprs : c / cpr) : 0u;
+        const uint32_t src = (uint32_t)__shfl((int)vsrc, rowbase + (int)e, kWave);
+        if (act) {
+          const uint4 w4 = lds_win16(B.stage, src + 16u * (c - e * cpr));
+          *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4.x, w4.y, w4.z, w4.w};
         }
       }
+    } else if (live) {
+      uint8_t* vd = a.vals + pv + r.vs;
+      for (uint32_t o = 0; o < r.vl; o += 16) {
+        const uint32_t mlen = r.vl - o;
+        store_bytes(vd + o, lds_win16(B.stage, vsrc + o), mlen < 16 ? mlen : 16);
+      }
     }
+  }
 #endif
 #ifndef MTBLX_ABL_NOKEY
-    uint8_t* kd = a.keys + pk + ks;
-    for (uint32_t q0 = 0; __ballot(live && klen > q0) != 0ull; q0 += 16) {   // wave-uniform planes
-      const bool own = live && sh < q0 + 16u && q0 < klen;
-      uint4 W = own ? lds_win16(B.stage, sp - sh + q0) : make_uint4(0, 0, 0, 0);
-      uint32_t m = sh;
-      key_scan_step<1>(m, W, q0);
-      key_scan_step<2>(m, W, q0);
-      key_scan_step<4>(m, W, q0);
-      key_scan_step<8>(m, W, q0);
-      if (live && q0 < klen) {
-        const uint32_t n = klen - q0;
-        store_bytes(kd + q0, W, n < 16 ? n : 16);
-      }
+  uint8_t* kd = a.keys + pk + r.ks;
+  if (live && r.klen > 0u) store_bytes(kd, r.W0, r.klen < 16u ? r.klen : 16u);
+  for (uint32_t q0 = 16; __ballot(live && r.klen > q0) != 0ull; q0 += 16) {   // further planes (keys > 16 B)
+    const bool own = live && r.sh < q0 + 16u && q0 < r.klen;
+    uint4 W = own ? lds_win16(B.stage, r.sp - r.sh + q0) : make_uint4(0, 0, 0, 0);
+    uint32_t m = r.sh;
+    key_scan_step<1>(m, W, q0);
+    key_scan_step<2>(m, W, q0);
+    key_scan_step<4>(m, W, q0);
+    key_scan_step<8>(m, W, q0);
+    if (live && q0 < r.klen) {
+      const uint32_t n = r.klen - q0;
+      store_bytes(kd + q0, W, n < 16 ? n : 16);
     }
+  }
 #endif
+}
+
+__device__ __forceinline__ void wait_flag(const uint32_t* flag, uint32_t want) {
+  uint32_t spins = 0;
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 24)) break;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int cw, int lane, const uint32_t* ready,
+                                          uint32_t want, Stamps& ST) {
+  const uint32_t nint = B.nint, nb = B.nb;
+  uint32_t fb = (uint32_t)cw * (kWave / 16);
+  if (fb < nint) {
+    const CopyRow r = copy_prepare(B, fb, lane);
+    wait_flag(ready, want);
+    ST.hit(0);
+    if (a.write) copy_emit(B, a, r, lane);
+    for (fb += kPipeRows; fb < nint; fb += kPipeRows) {   // wave-uniform
+      const CopyRow r2 = copy_prepare(B, fb, lane);
+      if (a.write) copy_emit(B, a, r2, lane);
+    }
+  } else {
+    wait_flag(ready, want);
+    ST.hit(0);
   }
   // irregular blocks: exact serial write (thread per block)
   const int ct = cw * kWave + lane;
-  if (ct < (int)nb && !B.bok[ct] && B.bwr[ct]) {
+  if (a.write && ct < (int)nb && !B.bok[ct] && B.bwr[ct]) {
+    const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
     const uint32_t j = ct, bo = B.boff[j], L = B.blen[j];
     const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[B.b0 + j]);
     generic_block<true>(d, L, a.keys + pk + B.bkbb[j], a.vals + pv + B.bvbb[j], a.key_end + pr + B.brb[j],
@@ -1467,6 +1577,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
   Stamps ST;
   ST.init();
+  ws_begin(a);
   if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; }
 
   uint64_t tinc[3] = {0, 0, 0};           // wave 1
@@ -1532,14 +1643,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kPipeCopyWaves);
         }
       } else {
-        uint32_t spins = 0;
-        while (__hip_atomic_load(&S.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)it + 1) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 24)) break;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        ST.hit(0);
-        if (a.write) pipe_copy(C, a, wv - kPipeCopyWave0, lane);
+        pipe_copy(C, a, wv - kPipeCopyWave0, lane, &S.ready, (uint32_t)it + 1, ST);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(7);
       }
@@ -1552,6 +1656,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   }
   // retire this wave's outstanding global stores before the workgroup ends
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ws_end(a);
 #ifdef MTBLX_STAMPS
   // wave 0: [2] trailers + walk loop, [3] scans + publish, [8] barrier.  wave 1: [1]
   // look-back (+ barrier).  first loader: [4] DMA issue, [6] DMA wait + barrier.  first copy
@@ -1633,22 +1738,21 @@ int resident_grid(uint32_t ntiles) {
 }
 }  // namespace
 
-// workspace: [0, 256) diagnostic stamps | lb[nblk] | lbx[nblk]
-extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 16u + 64u; }
+// workspace: [0, 128) diagnostic stamps | [128, 256) WsHdr | 3 u64 per tile (tiles <= nblk).
+// Zero-filled once by the caller; every launch leaves it ready for the next (ws_end).
+extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
 
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
                               hipStream_t s) {
   const uint32_t nblk = in->nblk;
   const Plan p = make_plan(nblk, in->max_blk_len);
   uint64_t* dbg = reinterpret_cast<uint64_t*>(ws);
-  uint64_t* lb = dbg + 32;
-  uint64_t* lbx = lb + nblk;
-  if (hipMemsetAsync(ws, 0, 256u + (size_t)p.ntiles * 8u, s) != hipSuccess) return MTBLX_E_HIP;
-  if (hipMemsetAsync(out->totals, 0, 32, s) != hipSuccess) return MTBLX_E_HIP;
+  WsHdr* hdr = reinterpret_cast<WsHdr*>(reinterpret_cast<uint8_t*>(ws) + 128);
+  uint64_t* lbw = dbg + 32;
   TileArgs a{in->data,     in->data_len,  in->blk_off,  in->blk_len,   nblk,         p.bpt,         p.slot,
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
-             lb,           lbx,           dbg,          write ? 1 : 0};
+             lbw,          hdr,           dbg,          write ? 1 : 0, 0,           0};
   if (p.large) {
     hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
   } else {

@@ -26,9 +26,13 @@ extern "C" size_t mtblx_decode_workspace_bytes(uint32_t nblk) {
   return mtblx_impl_ws_bytes(nblk) + 256u;
 }
 
-static int check_common(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb) {
+static int check_common(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb, void* stream) {
   if (!in || !out) return MTBLX_E_INVAL;
-  if (in->nblk == 0) return MTBLX_OK;
+  if (in->nblk == 0) {  // empty batch: zero totals, nothing else to do
+    if (out->totals && hipMemsetAsync(out->totals, 0, 32, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+      return MTBLX_E_HIP;
+    return MTBLX_OK;
+  }
   if (!in->data || !in->blk_off || !in->blk_len) return MTBLX_E_INVAL;
   if (!out->nrec || !out->rec_base || !out->key_base || !out->val_base || !out->status || !out->totals)
     return MTBLX_E_INVAL;
@@ -39,14 +43,14 @@ static int check_common(const mtblx_block_batch* in, const mtblx_decoded* out, v
 
 extern "C" int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
                                   void* stream) {
-  int c = check_common(in, out, ws, wsb);
+  int c = check_common(in, out, ws, wsb, stream);
   if (c != 1) return c;
   return mtblx_impl_run(in, out, ws, 0, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
                                     void* stream) {
-  int c = check_common(in, out, ws, wsb);
+  int c = check_common(in, out, ws, wsb, stream);
   if (c != 1) return c;
   if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
       (!out->val_end && out->rec_cap))
@@ -57,7 +61,7 @@ extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_dec
 
 extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
                                    void* stream) {
-  int c = check_common(in, out, ws, wsb);
+  int c = check_common(in, out, ws, wsb, stream);
   if (c != 1) return c;
   if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
       (!out->val_end && out->rec_cap))

@@ -126,7 +126,8 @@ class Workspace:
     def __init__(self, nblk: int, device="cuda"):
         L = _lib.lib()
         self.nbytes = int(L.mtblx_decode_workspace_bytes(nblk))
-        self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+        # zero-filled once: the kernels keep it consistent from call to call (include/mtblx.h)
+        self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
 
 
 def _stream_handle(stream) -> int:

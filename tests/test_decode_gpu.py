@@ -142,3 +142,32 @@ def test_cfg2_full_roundtrip_property():
     rb = np.concatenate([[0], np.cumsum(nrec)[:-1]])
     # last record of every block ends at 16 * nrec of that block
     assert np.array_equal(ke[rb + nrec - 1], 16 * nrec.astype(np.uint32))
+
+
+def test_workspace_reuse_across_batch_sizes(oracle):
+    """One workspace (zero-filled once) serves a sequence of batches of different sizes and
+    both entry points: the launch-parity look-back slots are cleared by the kernels
+    themselves (no per-call fill), so stale words from a bigger earlier batch must never
+    leak into a later one."""
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(6000)
+    ws = codec.Workspace(6000)
+    exp_all = oracle.decode_blocks(data, off, ln)
+    for n in (6000, 37, 6000, 1, 2500, 6000, 13, 6000):
+        o, l_ = off[:n], ln[:n]
+        batch = codec.DeviceBatch.from_host(data, o, l_)
+        probe = codec.DecodedBlocks(batch.nblk, 0, 0, 0)
+        codec.count_blocks(batch, probe, ws)
+        torch.cuda.synchronize()
+        nr, kb, vb, fl = probe.totals_host()
+        assert fl == 0
+        exp_nr = int(exp_all.nrec[:n].sum())
+        assert nr == exp_nr, (n, nr, exp_nr)
+        out = codec.DecodedBlocks(batch.nblk, nr, kb, vb)
+        codec.decode_into(batch, out, ws)
+        torch.cuda.synchronize()
+        dev = out.to_host()
+        orc = oracle.decode_blocks(data, o, l_)
+        assert_same(dev, orc, n)

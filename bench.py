@@ -30,7 +30,8 @@ sys.path.insert(0, os.path.join(ROOT, "oxidized-mtbl_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-PIPE_MAX_BLOCK = 49152 - 64  # largest block k_decode_pipe stages (decode.hip make_plan); bigger -> k_decode_tiles
+PIPE_MAX_BLOCK = 49152 - 64  # largest block k_decode_pipe<PipeSmall> stages (decode.hip make_plan)
+PIPE_LARGE_MAX_BLOCK = 65664 - 64  # k_decode_pipe<PipeLarge>; bigger -> k_decode_tiles
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
 
 
@@ -82,6 +83,7 @@ def main():
                     help="diagnostic: writer block size (cfg2 = 4096; cfg4 also uses 16384 / 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the stream-copy ceiling measurement")
     ap.add_argument("--lib", default=None, help="diagnostic: alternative libmtblx build (ablations)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load libmtblx_stamps.so and report per-phase cycles per tile (not a measurement)")
@@ -170,7 +172,9 @@ def main():
     # block bytes read + key/value bytes written + 2 x u32 end offsets per record + 24 B of per-block outputs
     alg_bytes = block_bytes + kbytes + vbytes + 8 * nrec + 24 * batch.nblk
     achieved = alg_bytes / (k_decode_ms * 1e-3) / 1e9
-    kernel = "k_decode_pipe" if int(ln.max()) <= PIPE_MAX_BLOCK else "k_decode_tiles"
+    mx = int(ln.max())
+    kernel = ("k_decode_pipe<PipeSmall>" if mx <= PIPE_MAX_BLOCK else
+              "k_decode_pipe<PipeLarge>" if mx <= PIPE_LARGE_MAX_BLOCK else "k_decode_tiles")
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -179,6 +183,26 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+
+    # stream-copy ceiling on this box: a plain device copy moving the same
+    # number of bytes (half read, half written) as one decode launch
+    ceiling = None
+    if not args.no_ceiling:
+        half = alg_bytes // 2
+        src = torch.empty(half, dtype=torch.uint8, device="cuda")
+        dst = torch.empty(half, dtype=torch.uint8, device="cuda")
+        src.fill_(1)
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                dst.copy_(src)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record(stream)
+            for _ in range(10):
+                dst.copy_(src)
+            c1.record(stream)
+        torch.cuda.synchronize()
+        ceiling = 2 * half / (c0.elapsed_time(c1) / 10 * 1e-3) / 1e9
+        del src, dst
 
     res = {
         "metric": "KV records/s + GiB/s of block bytes decoded, device-resident",
@@ -203,7 +227,9 @@ def main():
         "kernels_ms": {f"{kernel} (events incl. 2 memsets)": round(k_decode_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": kernel, "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel": kernel, "alg_bytes_per_launch": int(alg_bytes),
+                     "stream_copy_ceiling_GBs": round(ceiling, 1) if ceiling else None,
+                     "frac_of_copy_ceiling": round(achieved / ceiling, 4) if ceiling else None},
     }
     if args.stamps:
         d = ws.buf[:128].cpu().numpy().view(np.uint64).astype(np.float64)

@@ -954,7 +954,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 //   s_waitcnt lgkmcnt(0); s_barrier (raw: global stores and the DMA in flight are not
 //   drained at the barrier)
 // Restart intervals of more than 16 entries (the reference default is 16,
-// src/lib.rs:4), tiles of more than kP2MaxInt intervals and anything irregular take the
+// src/lib.rs:4), tiles of more than MAXINT intervals and anything irregular take the
 // exact generic path for the affected blocks.
 // diagnostic per-phase cycle stamps (MTBLX_STAMPS builds only; lane 0 of a wave)
 struct Stamps {
@@ -979,33 +979,41 @@ constexpr int kPipeLoadWaves = 2;                                        // wave
 constexpr int kPipeCopyWave0 = kPipeLoadWave + kPipeLoadWaves;           // waves 4..15 copy
 constexpr int kPipeCopyWaves = kPipeThreads / kWave - kPipeCopyWave0;
 constexpr int kPipeRows = kPipeCopyWaves * (kWave / 16);                 // intervals per copy round
-constexpr int kPipeTB = 49152;
 constexpr int kP2Spi = 16;                                               // slots per interval (= DPP row)
-constexpr int kP2MaxInt = 56;
-constexpr int kP2Slots = kP2MaxInt * kP2Spi;
-constexpr int kPipeMaxBlk = 16;
-constexpr int kPipeBufs = 3;
 
+// Pipeline configurations.  TB = staging bytes of a tile buffer, NBUF = tile buffers in
+// LDS (3: DMA / walk / copy of three tiles overlap; 2: DMA of the next tile overlaps the
+// walk + copy of this one), MAXBLK blocks and MAXINT (<= 64: one walk lane each) restart
+// intervals per tile.
+template <int TB_, int NBUF_, int MAXBLK_, int MAXINT_>
+struct PipeCfg {
+  static constexpr int TB = TB_, NBUF = NBUF_, MAXBLK = MAXBLK_, MAXINT = MAXINT_;
+  static constexpr int SLOTS = MAXINT * kP2Spi;
+};
+using PipeSmall = PipeCfg<49152, 3, 16, 56>;   // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
+using PipeLarge = PipeCfg<65664, 2, 2, 64>;    // blocks up to ~64 KiB (cfg3, cfg4 64 KiB)
+
+template <class P>
 struct alignas(16) PipeBuf {
-  uint8_t stage[kPipeTB];
-  uint16_t pos[kP2Slots];     // header offset (block-relative) of entry k of interval f: slot 16 f + k
-  uint32_t boff[kPipeMaxBlk], blen[kPipeMaxBlk], bR[kPipeMaxBlk], bn[kPipeMaxBlk];
-  uint32_t bok[kPipeMaxBlk], bwr[kPipeMaxBlk];
-  int32_t bst[kPipeMaxBlk];
-  uint32_t bcnt[kPipeMaxBlk], bkb[kPipeMaxBlk], bvb[kPipeMaxBlk];
-  uint32_t brb[kPipeMaxBlk], bkbb[kPipeMaxBlk], bvbb[kPipeMaxBlk];
-  uint32_t bint0[kPipeMaxBlk + 1];
-  // per interval: raw counts after the walk; after the scan, tile-relative bases
-  uint32_t icnt[kP2MaxInt + 1], ikb[kP2MaxInt + 1], ivb[kP2MaxInt + 1];
-  uint8_t iraw[kP2MaxInt];    // entries of the interval (<= 16)
-  uint8_t iblk[kP2MaxInt];
+  uint8_t stage[P::TB];
+  uint16_t pos[P::SLOTS];     // header offset (block-relative) of entry k of interval f: slot 16 f + k
+  uint32_t boff[P::MAXBLK], blen[P::MAXBLK];
+  uint32_t bok[P::MAXBLK], bwr[P::MAXBLK];
+  int32_t bst[P::MAXBLK];
+  uint32_t bcnt[P::MAXBLK], bkb[P::MAXBLK], bvb[P::MAXBLK];
+  uint32_t brb[P::MAXBLK], bkbb[P::MAXBLK], bvbb[P::MAXBLK];
+  // per interval: tile-relative bases after the scan
+  uint32_t icnt[P::MAXINT + 1], ikb[P::MAXINT + 1], ivb[P::MAXINT + 1];
+  uint8_t iraw[P::MAXINT];    // entries of the interval (<= 16)
+  uint8_t iblk[P::MAXINT];
   uint64_t tpre[3];
   uint32_t ttot[3];
   uint32_t nb, b0, nint;
 };
 
+template <class P>
 struct alignas(16) PipeLds {
-  PipeBuf buf[kPipeBufs];
+  PipeBuf<P> buf[P::NBUF];
   uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
   uint32_t pub;      // wave 0 sets after publishing the aggregate of the tile it walked
   uint32_t cdone;    // copy waves that finished their copy (monotonic)
@@ -1145,7 +1153,8 @@ __device__ __forceinline__ bool walk_careful_pos(const uint8_t* stage, uint16_t*
 
 // wave 0: LDS-DMA of tile t into B (contiguous range, or one 16 B aligned slot per block).
 // (off_l, len_l) = directory entry of block `lane` of the tile (lanes < nb).
-__device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t t, uint64_t off_l, uint32_t len_l,
+template <class P>
+__device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint32_t t, uint64_t off_l, uint32_t len_l,
                                          int lane, uint32_t part) {
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void g_void;
@@ -1158,7 +1167,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end_l, (int)nb - 1);
   uint64_t r0 = ((base + s) & ~15ull) - base;
   if (base + s < 16 || ((base + s) & ~15ull) < base) r0 = 0;
-  const bool contig = e > s && e - r0 + 48 <= (uint64_t)kPipeTB;
+  const bool contig = e > s && e - r0 + 48 <= (uint64_t)P::TB;
   if (contig) {
     // range byte x at stage offset 16 + x; wave-instruction m writes chunks [64m, 64m + 64)
     const uint32_t nch = (uint32_t)((e - r0 + 15) >> 4);
@@ -1184,7 +1193,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
       const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)len_l, (int)j);
       const uint32_t so = 16u + j * a.slot;
       uint32_t bo = kNotStaged;
-      if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)kPipeTB) {
+      if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)P::TB) {
         uint64_t a0 = ((base + off) & ~15ull) - base;
         if (base + off < 16 || ((base + off) & ~15ull) < base) a0 = off;  // unaligned data base: not reached
         const uint32_t delta = (uint32_t)(off - a0);
@@ -1211,7 +1220,8 @@ __device__ __forceinline__ void pipe_dma(PipeBuf& B, const TileArgs& a, uint32_t
 // wave 0: trailers, walk (header offsets into slots), irregular counts, interval scan,
 // publish A(t), then the block / interval bases the copy and the look-back read.
 // Cross-lane traffic uses readlane / DPP / bpermute (no LDS round trips before the walk).
-__device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_t t, int lane, Stamps& ST) {
+template <class P>
+__device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint32_t t, int lane, Stamps& ST) {
   const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
   // trailers (Block::init, src/block.rs:16-49): lane = block
   uint32_t n = 0, R = 0, ok = 0, L = 0, bo = kNotStaged;
@@ -1224,7 +1234,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf& B, const TileArgs& a, uint32_
     }
   }
   uint32_t incl = wave_incl_scan(ok ? n : 0u);
-  if (ok && incl > (uint32_t)kP2MaxInt) ok = 0;
+  if (ok && incl > (uint32_t)P::MAXINT) ok = 0;
   n = ok ? n : 0;
   incl = wave_incl_scan(n);                   // lane b: intervals of blocks 0..b
   const uint32_t bint0 = incl - n;
@@ -1360,7 +1370,8 @@ __device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t
 
 // wave 1: finish the look-back of tile t (re-polling words that were not ready yet),
 // per-block outputs.  tinc = inclusive prefix of this workgroup's previous tile.
-__device__ __forceinline__ void pipe_lookback(PipeBuf& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3],
+template <class P>
+__device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3],
                                               uint64_t lbv[kMaxLookbackLoads], int lane) {
   const uint32_t nb = B.nb, b0 = B.b0;
   const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
@@ -1427,7 +1438,8 @@ struct CopyRow {
   bool fv, live;
 };
 
-__device__ __forceinline__ CopyRow copy_prepare(const PipeBuf& B, uint32_t fb, int lane) {
+template <class P>
+__device__ __forceinline__ CopyRow copy_prepare(const PipeBuf<P>& B, uint32_t fb, int lane) {
   CopyRow r;
   const uint32_t nint = B.nint;
   r.k = lane & 15;
@@ -1470,7 +1482,8 @@ __device__ __forceinline__ CopyRow copy_prepare(const PipeBuf& B, uint32_t fb, i
   return r;
 }
 
-__device__ __forceinline__ void copy_emit(const PipeBuf& B, const TileArgs& a, const CopyRow& r, int lane) {
+template <class P>
+__device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a, const CopyRow& r, int lane) {
   const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
   const bool live = r.live && B.bwr[r.j];   // bwr may have been cleared by the look-back (overflow)
   if (live) {
@@ -1542,7 +1555,8 @@ __device__ __forceinline__ void wait_flag(const uint32_t* flag, uint32_t want) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, int cw, int lane, const uint32_t* ready,
+template <class P>
+__device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a, int cw, int lane, const uint32_t* ready,
                                           uint32_t want, Stamps& ST) {
   const uint32_t nint = B.nint, nb = B.nb;
   uint32_t fb = (uint32_t)cw * (kWave / 16);
@@ -1570,8 +1584,9 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf& B, const TileArgs& a, i
   }
 }
 
+template <class P>
 __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
-  __shared__ PipeLds S;
+  __shared__ PipeLds<P> S;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t g = blockIdx.x, G = gridDim.x;
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
@@ -1600,31 +1615,69 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     load_info(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (wv == 1) {
-    if (nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
+    if (P::NBUF == 3 && nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
   }
   __syncthreads();
   if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
   uint64_t ntl = 0;
 
+  if constexpr (P::NBUF == 2) {
+    // two buffers: tile it is walked, looked back and copied in iteration it while the
+    // loaders stage tile it+1 into the other buffer
+    for (uint32_t it = 0; it < nloc; ++it) {
+      PipeBuf<P>& C = S.buf[it & 1u];
+      const uint32_t tc = g + it * G;
+      if (wv == 0) {
+        pipe_walk(C, a, tc, lane, ST);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&S.pub, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ST.hit(3);
+      } else if (loader) {
+        if (it + 1 < nloc) {
+          pipe_dma(S.buf[(it + 1) & 1u], a, tc + G, ioff, ilen, lane, part);
+          load_info(it + 2);
+        }
+        ST.hit(4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+1 (read next phase)
+        ST.hit(6);
+      } else if (wv == 1) {
+        wait_flag(&S.pub, it + 1);
+        pipe_lookback_issue(a, tc, G, lbv, lane);
+        pipe_lookback(C, a, tc, G, tinc, lbv, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&S.ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ST.hit(1);
+      } else {
+        wait_flag(&S.pub, it + 1);
+        pipe_copy(C, a, wv - kPipeCopyWave0, lane, &S.ready, it + 1, ST);
+        ST.hit(7);
+      }
+      raw_barrier();
+      if (wv == 0) { ST.hit(8); ++ntl; }
+      else if (wv == kPipeCopyWave0) ST.hit(5);
+      else if (loader) ST.hit(12);
+      else ST.hit(1);
+    }
+  } else
   for (int it = -1; it < (int)nloc; ++it) {
     const uint32_t k1 = (uint32_t)(it + 1), k2 = (uint32_t)(it + 2);
     if (wv == 0) {
       // walk first: the aggregate A(tile it+1) is published as early as possible
       if (k1 < nloc) {
-        pipe_walk(S.buf[k1 % kPipeBufs], a, g + k1 * G, lane, ST);
+        pipe_walk(S.buf[k1 % P::NBUF], a, g + k1 * G, lane, ST);
         if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       ST.hit(3);
     } else if (loader) {
       if (k2 < nloc) {
-        pipe_dma(S.buf[k2 % kPipeBufs], a, g + k2 * G, ioff, ilen, lane, part);
+        pipe_dma(S.buf[k2 % P::NBUF], a, g + k2 * G, ioff, ilen, lane, part);
         load_info(k2 + 1);
       }
       ST.hit(4);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+2 (read next phase)
       ST.hit(6);
     } else if (it >= 0) {
-      PipeBuf& C = S.buf[(uint32_t)it % kPipeBufs];
+      PipeBuf<P>& C = S.buf[(uint32_t)it % P::NBUF];
       const uint32_t tc = g + (uint32_t)it * G;
       if (wv == 1) {
         pipe_lookback(C, a, tc, G, tinc, lbv, lane);
@@ -1686,22 +1739,31 @@ using namespace mtblx;
 namespace {
 struct Plan {
   uint32_t bpt, slot, ntiles;
-  bool large;
+  int kind;   // 0 = k_decode_pipe<PipeSmall>, 1 = k_decode_pipe<PipeLarge>, 2 = k_decode_tiles<CfgLarge>
 };
+
+// tile shape for staging bytes TB: contiguous staging needs blocks + framing (<= 14 B each)
+// + 16 B alignment + a 32 B tail; the fallback layout uses one 16 B aligned slot per block
+static bool fit_plan(uint32_t max_len, uint32_t tb, uint32_t maxblk, Plan& p) {
+  const uint32_t slot = ((max_len + 30u) / 16u) * 16u;
+  const uint32_t per = max_len + 16u;
+  const uint32_t usable = tb - 48;
+  if (max_len == 0 || slot > usable) return false;
+  p.slot = slot;
+  p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, slot), maxblk));
+  return true;
+}
 
 Plan make_plan(uint32_t nblk, uint32_t max_len) {
   Plan p{};
-  const uint32_t slot = ((max_len + 30u) / 16u) * 16u;
-  // contiguous staging: blocks + framing (<= 14 B each) + 16 B alignment + 32 B tail
-  const uint32_t per = max_len + 16u;
-  uint32_t usable = kPipeTB - 48;
-  if (max_len != 0 && slot <= usable) {
-    p.large = false;
-    p.slot = slot;
-    p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, slot), kPipeMaxBlk));
+  if (fit_plan(max_len, PipeSmall::TB, PipeSmall::MAXBLK, p)) {
+    p.kind = 0;
+  } else if (fit_plan(max_len, PipeLarge::TB, PipeLarge::MAXBLK, p)) {
+    p.kind = 1;
   } else {
-    usable = CfgLarge::TB - 48;
-    p.large = true;
+    const uint32_t usable = CfgLarge::TB - 48;
+    const uint32_t slot = ((max_len + 30u) / 16u) * 16u, per = max_len + 16u;
+    p.kind = 2;
     p.slot = (max_len != 0 && slot <= usable) ? slot : usable;
     p.bpt = std::max<uint32_t>(1, std::min<uint32_t>(usable / std::max(per, p.slot), CfgLarge::MAXBLK));
   }
@@ -1753,10 +1815,12 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
              lbw,          hdr,           dbg,          write ? 1 : 0, 0,           0};
-  if (p.large) {
-    hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
+  if (p.kind == 0) {
+    hipLaunchKernelGGL(k_decode_pipe<PipeSmall>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+  } else if (p.kind == 1) {
+    hipLaunchKernelGGL(k_decode_pipe<PipeLarge>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   } else {
-    hipLaunchKernelGGL(k_decode_pipe, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+    hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
   }
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

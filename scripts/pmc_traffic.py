@@ -30,7 +30,7 @@ def rows(pattern):
 
 def counter(d, name, kernel):
     vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, "**", "*counter_collection.csv"))
-            if r.get("Counter_Name") == name and kernel in r.get("Kernel_Name", "")]
+            if r.get("Counter_Name") == name and kernel.split("<")[0] in r.get("Kernel_Name", "")]
     return vals
 
 
@@ -54,7 +54,7 @@ def main():
     write = counter(os.path.join(src, "write"), "WRITE_SIZE", kernel)
     for name, d in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         sel = [r for r in rows(os.path.join(src, name, "**", "*counter_collection.csv"))
-               if r.get("Counter_Name") == d and kernel in r.get("Kernel_Name", "")]
+               if r.get("Counter_Name") == d and kernel.split("<")[0] in r.get("Kernel_Name", "")]
         if sel:
             with open(os.path.join(dst, f"pmc_{name}.csv"), "w", newline="") as fh:
                 w = csv.DictWriter(fh, fieldnames=list(sel[0].keys()))

@@ -171,3 +171,32 @@ def test_workspace_reuse_across_batch_sizes(oracle):
         dev = out.to_host()
         orc = oracle.decode_blocks(data, o, l_)
         assert_same(dev, orc, n)
+
+
+def test_64k_blocks_cfg2_scheme(oracle):
+    """cfg4's 64 KiB leg (cfg2 key/value scheme): k_decode_pipe<PipeLarge>."""
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(300, block_size=65536)
+    assert int(ln.max()) > 60000
+    orc = oracle.decode_blocks(data, off, ln)
+    dev = device_decode(data, off, ln)
+    assert_same(dev, orc, off.size)
+    assert (orc.status == 0).all()
+
+
+def test_64k_blocks_long_keys(oracle):
+    """cfg3-like 64 KiB blocks: 8..256 B keys (multi-byte varint headers for long suffixes),
+    64 B values, and a few mutated copies."""
+    rng = np.random.default_rng(21)
+    blocks = []
+    for _ in range(24):
+        n = int(rng.integers(150, 330))
+        recs = corpus.random_records(rng, n, 8, 256, 64, 64)
+        b = oracle.build_block(recs)
+        if len(b) <= 65000:
+            blocks.append(b)
+    assert len(blocks) >= 8 and max(len(b) for b in blocks) > 40000
+    big = list(blocks)
+    mut = [corpus.mutate(rng, b) for b in blocks[:8]]
+    orc = run_both(oracle, big + mut, rng=np.random.default_rng(3))
+    assert (orc.status[: len(big)] == 0).all()

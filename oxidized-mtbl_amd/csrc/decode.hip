@@ -320,6 +320,7 @@ struct TileArgs {
   uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
   int write;
   // set at kernel start from the workspace header (ws_begin)
+  uint32_t wscap;   // tile entries the workspace holds (from workspace_bytes)
   uint32_t par;     // launch parity: aggregates live in slot `par` of each tile entry
   uint32_t hw_other;
 };
@@ -346,6 +347,7 @@ __device__ __forceinline__ void ws_begin(TileArgs& a) {
   const uint32_t ep = __hip_atomic_load(&a.hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   a.par = ep & 1u;
   a.hw_other = __hip_atomic_load(&a.hdr->hw[a.par ^ 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.hw_other > a.wscap) a.hw_other = a.wscap;   // never write past the caller's workspace
   const uint32_t n = blockDim.x, tid = threadIdx.x;
   for (uint64_t t = (uint64_t)blockIdx.x * n + tid; t < a.hw_other; t += (uint64_t)gridDim.x * n)
     a.lbw[3 * t + (a.par ^ 1u)] = 0;
@@ -1804,9 +1806,11 @@ int resident_grid(uint32_t ntiles) {
 // Zero-filled once by the caller; every launch leaves it ready for the next (ws_end).
 extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
 
-extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
-                              hipStream_t s) {
+extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t ws_bytes,
+                              int write, hipStream_t s) {
   const uint32_t nblk = in->nblk;
+  const uint64_t cap64 = ws_bytes > 320u ? (ws_bytes - 320u) / 24u : 0u;
+  const uint32_t wscap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;
   const Plan p = make_plan(nblk, in->max_blk_len);
   uint64_t* dbg = reinterpret_cast<uint64_t*>(ws);
   WsHdr* hdr = reinterpret_cast<WsHdr*>(reinterpret_cast<uint8_t*>(ws) + 128);
@@ -1814,7 +1818,7 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
   TileArgs a{in->data,     in->data_len,  in->blk_off,  in->blk_len,   nblk,         p.bpt,         p.slot,
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
-             lbw,          hdr,           dbg,          write ? 1 : 0, 0,           0};
+             lbw,          hdr,           dbg,          write ? 1 : 0, wscap,       0,             0};
   if (p.kind == 0) {
     hipLaunchKernelGGL(k_decode_pipe<PipeSmall>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   } else if (p.kind == 1) {

@@ -9,8 +9,8 @@
 #include "mtblx.h"
 
 extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk);
-extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, int write,
-                              hipStream_t s);
+extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t ws_bytes,
+                              int write, hipStream_t s);
 
 extern "C" int mtblx_abi_version(void) { return MTBLX_ABI_VERSION; }
 
@@ -45,7 +45,7 @@ extern "C" int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decod
                                   void* stream) {
   int c = check_common(in, out, ws, wsb, stream);
   if (c != 1) return c;
-  return mtblx_impl_run(in, out, ws, 0, reinterpret_cast<hipStream_t>(stream));
+  return mtblx_impl_run(in, out, ws, wsb, 0, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
@@ -56,7 +56,7 @@ extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_dec
       (!out->val_end && out->rec_cap))
     return MTBLX_E_INVAL;
   // single-pass kernel: counting is fused into the decode, so this is a full decode
-  return mtblx_impl_run(in, out, ws, 1, reinterpret_cast<hipStream_t>(stream));
+  return mtblx_impl_run(in, out, ws, wsb, 1, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
@@ -66,5 +66,5 @@ extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_deco
   if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
       (!out->val_end && out->rec_cap))
     return MTBLX_E_INVAL;
-  return mtblx_impl_run(in, out, ws, 1, reinterpret_cast<hipStream_t>(stream));
+  return mtblx_impl_run(in, out, ws, wsb, 1, reinterpret_cast<hipStream_t>(stream));
 }

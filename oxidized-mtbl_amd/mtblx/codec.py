@@ -16,12 +16,21 @@ from . import _lib
 from ._lib import BlockBatch, Decoded
 
 
+_checked_devices = set()
+
+
 def _require_device():
-    if not torch.cuda.is_available():
-        raise RuntimeError("mtblx device codec needs a ROCm GPU (gfx950); none visible")
+    """The library handle, after checking (once per device) that the current device is a
+    gfx950; raises otherwise -- there is no CPU fallback."""
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
     L = _lib.lib()
+    if dev in _checked_devices:
+        return L
+    if dev is None:
+        raise RuntimeError("mtblx device codec needs a ROCm GPU (gfx950); none visible")
     if L.mtblx_device_ok() != 1:
         raise RuntimeError("mtblx device codec: current device is not gfx950 (MI355X)")
+    _checked_devices.add(dev)
     return L
 
 
@@ -50,8 +59,12 @@ class DeviceBatch:
         return DeviceBatch(d, o, n, int(ln.max()) if ln.size else 0)
 
     def cstruct(self) -> BlockBatch:
-        return BlockBatch(_u(self.data), int(self.data.numel()), _u(self.blk_off), _u(self.blk_len), self.nblk,
-                          int(self.max_blk_len))
+        c = getattr(self, "_c", None)
+        if c is None:   # the tensors never change after construction
+            c = BlockBatch(_u(self.data), int(self.data.numel()), _u(self.blk_off), _u(self.blk_len), self.nblk,
+                           int(self.max_blk_len))
+            self._c = c
+        return c
 
 
 class DecodedBlocks:
@@ -73,9 +86,13 @@ class DecodedBlocks:
         self.rec_cap, self.keys_cap, self.vals_cap = int(rec_cap), int(keys_cap), int(vals_cap)
 
     def cstruct(self) -> Decoded:
-        return Decoded(_u(self.nrec), _u(self.rec_base), _u(self.key_base), _u(self.val_base), _u(self.status),
-                       _u(self.key_end), _u(self.val_end), self.rec_cap, _u(self.keys), self.keys_cap,
-                       _u(self.vals), self.vals_cap, _u(self.totals))
+        c = getattr(self, "_c", None)
+        if c is None:
+            c = Decoded(_u(self.nrec), _u(self.rec_base), _u(self.key_base), _u(self.val_base), _u(self.status),
+                        _u(self.key_end), _u(self.val_end), self.rec_cap, _u(self.keys), self.keys_cap,
+                        _u(self.vals), self.vals_cap, _u(self.totals))
+            self._c = c
+        return c
 
     # ---------------- host views ----------------
     def totals_host(self):
@@ -145,7 +162,9 @@ def count_blocks(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=N
 
 
 def decode_into(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=None) -> None:
-    """Asynchronous decode on `stream` into preallocated outputs (the timed hot call)."""
+    """Asynchronous decode on `stream` into preallocated outputs (the timed hot call).
+    The buffers must be ready on `stream` (allocate them under torch.cuda.stream(stream) or
+    synchronize first): the library orders nothing across streams."""
     L = _require_device()
     b, o = batch.cstruct(), out.cstruct()
     rc = L.mtblx_decode_blocks(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,

@@ -76,14 +76,15 @@ def cpu_baseline(data, off, ln, budget_s: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=100_000)
     ap.add_argument("--block-size", type=int, default=4096,
                     help="diagnostic: writer block size (cfg2 = 4096; cfg4 also uses 16384 / 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the stream-copy ceiling measurement")
+    ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32C verify measurement")
     ap.add_argument("--lib", default=None, help="diagnostic: alternative libmtblx build (ablations)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load libmtblx_stamps.so and report per-phase cycles per tile (not a measurement)")
@@ -208,6 +209,23 @@ def main():
         ceiling = 2 * half / (c0.elapsed_time(c1) / 10 * 1e-3) / 1e9
         del src, dst
 
+    # f1: device CRC-32C verify of the same blocks (separate kernel; the stored checksums sit
+    # right before each content in the file the batch addresses)
+    crc_info = None
+    if not args.no_crc:
+        with torch.cuda.stream(stream):
+            crc, bad = codec.crc32c_blocks(batch, framed=True, stream=stream)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record(stream)
+            for _ in range(10):
+                codec.crc32c_blocks(batch, framed=True, stream=stream)
+            c1.record(stream)
+        torch.cuda.synchronize()
+        crc_ms = c0.elapsed_time(c1) / 10
+        crc_info = {"kernel": "k_crc32c_blocks", "ms": round(crc_ms, 4),
+                    "GiB_per_s": round(block_bytes / (crc_ms * 1e-3) / 2**30, 1),
+                    "bad_blocks": int(bad.sum().item())}
+
     res = {
         "metric": "KV records/s + GiB/s of block bytes decoded, device-resident",
         "value": round(value, 3),
@@ -236,6 +254,8 @@ def main():
                      "stream_copy_ceiling_GBs": round(ceiling, 1) if ceiling else None,
                      "frac_of_copy_ceiling": round(achieved / ceiling, 4) if ceiling else None},
     }
+    if crc_info is not None:
+        res["crc32c_verify"] = crc_info
     if args.stamps:
         d = ws.buf[:128].cpu().numpy().view(np.uint64).astype(np.float64)
         names = ["copy:wait-ready", "w1:lookback+barrier", "w0:walk-loop", "w0:scan-publish",

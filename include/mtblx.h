@@ -110,6 +110,33 @@ int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, vo
 int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+/* CRC-32C (Castagnoli, crate crc32c 0.4) of every block's content bytes: crc[b] (device
+ * [nblk]).  This is the checksum Reader::block verifies before decoding a block
+ * (src/reader.rs:159-164, on by default, ReaderBuilder::verify_checksums src/reader.rs:22).
+ * With framed != 0 the batch addresses contents inside an mtbl file, whose framing stores
+ * the checksum as the u32 LE right before each content (varint len | crc32c | content,
+ * src/writer.rs:213-225): bad[b] = 1 where it differs from crc[b] -- exactly where the
+ * reference's assert_eq panics -- else 0.  bad may be NULL. */
+int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed, void* stream);
+
+/* ---- index block -> data-block directory (f3) ----
+ * The index block is decoded with mtblx_decode_blocks like any block; its values are the
+ * varint64 file offsets of the data blocks.  For every index entry i this does what
+ * block_at_index + the framing part of Reader::block do (src/reader.rs:177-186, :139-157):
+ * varint_decode64 of the value, then (FormatV1 u32 | FormatV2 varint64) content length,
+ * and the content window [blk_off[i], blk_off[i] + blk_len[i]) of the file.
+ * vals/val_end/val_base: the decoded index block (values blob, its block-relative value end
+ * offsets, and its val_base); file: the whole mtbl file on the device.  version: 0 = V1,
+ * 1 = V2 (mtblx_footer.version).  dir_st[i]: */
+#define MTBLX_DIR_OK 0          /* framed; checksum and Block::init are checked by
+                                   mtblx_crc32c_blocks (framed) and mtblx_decode_blocks */
+#define MTBLX_DIR_PANIC 1       /* the reference panics: offset >= file length, varint on an
+                                   empty value, content slice past the end of the file   */
+#define MTBLX_DIR_UNSUPPORTED 2 /* content >= 4 GiB                                       */
+int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, const uint8_t* vals,
+                    const uint32_t* val_end, uint64_t val_base, uint32_t nent, uint64_t* blk_off,
+                    uint32_t* blk_len, int32_t* dir_st, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -194,3 +194,20 @@ def decode_blocks(batch: DeviceBatch, stream=None) -> DecodedBlocks:
     out = DecodedBlocks(batch.nblk, nr, kb, vb)
     decode_into(batch, out, ws, stream)
     return out
+
+
+def crc32c_blocks(batch: DeviceBatch, framed: bool = False, stream=None):
+    """CRC-32C of every block's content on the device -> (crc uint32 tensor [nblk], bad uint8
+    tensor [nblk] or None).  With framed=True the batch addresses contents inside an mtbl
+    file and bad[b] = 1 where the stored checksum (the u32 before the content) differs: where
+    Reader::block's assert_eq panics (src/reader.rs:159-164)."""
+    L = _require_device()
+    n = max(batch.nblk, 1)
+    crc = torch.zeros(n, dtype=torch.int32, device=batch.data.device)
+    bad = torch.zeros(n, dtype=torch.uint8, device=batch.data.device) if framed else None
+    b = batch.cstruct()
+    rc = L.mtblx_crc32c_blocks(C.byref(b), C.c_void_p(crc.data_ptr()), C.c_void_p(bad.data_ptr() if framed else 0),
+                               1 if framed else 0, C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_crc32c_blocks failed: {rc}")
+    return crc[: batch.nblk], (bad[: batch.nblk] if framed else None)

@@ -200,3 +200,34 @@ def test_64k_blocks_long_keys(oracle):
     mut = [corpus.mutate(rng, b) for b in blocks[:8]]
     orc = run_both(oracle, big + mut, rng=np.random.default_rng(3))
     assert (orc.status[: len(big)] == 0).all()
+
+
+def test_crc32c_blocks_vs_oracle(oracle):
+    """f1: device CRC-32C of block contents == crate crc32c (oracle), and the framed check
+    flags exactly the blocks whose stored checksum was corrupted."""
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(3000)
+    rng = np.random.default_rng(8)
+    # varied block sizes including < 64 B and 64 KiB contents (unframed)
+    extra = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in (0, 1, 3, 4, 5, 63, 64, 65, 1000, 65000)]
+    xd, xo, xl = corpus.pack(extra, rng=rng, lead=3)
+    for d_, o_, l_, framed in ((data, off, ln, True), (xd, xo, xl, False)):
+        batch = codec.DeviceBatch.from_host(d_, o_, l_)
+        crc, bad = codec.crc32c_blocks(batch, framed=framed)
+        torch.cuda.synchronize()
+        got = crc.cpu().numpy().view(np.uint32)
+        exp = np.array([oracle.crc32c(bytes(d_[int(o): int(o) + int(n)])) for o, n in zip(o_, l_)], np.uint32)
+        assert np.array_equal(got, exp)
+        if framed:
+            assert int(bad.sum().item()) == 0
+    # corrupt the stored checksum of some blocks and one content byte of another
+    d2 = data.copy()
+    for b in (5, 77, 2999):
+        d2[int(off[b]) - 2] ^= 0x40
+    d2[int(off[1234]) + 100] ^= 1
+    batch = codec.DeviceBatch.from_host(d2, off, ln)
+    _, bad = codec.crc32c_blocks(batch, framed=True)
+    torch.cuda.synchronize()
+    assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == [5, 77, 1234, 2999]

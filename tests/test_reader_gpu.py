@@ -1,0 +1,86 @@
+"""f3 device Reader (index -> directory -> checksum -> decode on the GPU) vs the oracle's
+restatement of ReaderBuilder::read + ReaderIntoIter (oracle_file_scan)."""
+import numpy as np
+import pytest
+
+import corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def _reader():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mtblx import reader
+    return reader
+
+
+def _write(records, block_size=4096, interval=16):
+    from mtblx.writer import Writer
+    w = Writer(block_size, interval)
+    for k, v in records:
+        w.insert(k, v)
+    return w.into_inner()
+
+
+def _check(oracle, data: bytes, verify=True):
+    rd = _reader()
+    exp = oracle.file_scan(data, "iter", verify=verify)
+    try:
+        r = rd.ReaderBuilder().verify_checksums(verify).read(data)
+    except rd.MtblError as e:
+        assert exp["end"] == rd.END_ERR_OPEN and exp["err"] == str(e), (exp["end"], exp["err"], e)
+        return exp
+    except rd.ReferencePanic:
+        assert exp["end"] == rd.END_PANIC
+        return exp
+    s = r.iter()
+    assert s.end == exp["end"], (s.end, exp["end"], exp["err"])
+    got = s.records()
+    assert len(got) == len(exp["records"]), (len(got), len(exp["records"]))
+    assert got == exp["records"]
+    return exp
+
+
+def test_cfg1_file(oracle):
+    from mtblx import synth
+    data = _write(list(synth.cfg1_records()))
+    exp = _check(oracle, data)
+    assert len(exp["records"]) == 10_000
+
+
+def test_random_files(oracle):
+    rng = np.random.default_rng(31)
+    for bs, iv, n in ((1024, 1, 300), (4096, 16, 2000), (16384, 4, 3000), (65536, 16, 4000), (8192, 40, 1500)):
+        recs = corpus.random_records(rng, n, 0, 80, 0, 200)
+        _check(oracle, _write(recs, bs, iv))
+    _check(oracle, _write([]))                      # empty file: index with no entries
+
+
+def test_corrupted_files(oracle):
+    """stored checksum flips, content flips with and without verification, index entries
+    pointing past the end of the file"""
+    rd = _reader()
+    from mtblx import synth
+    rng = np.random.default_rng(32)
+    data, off, ln = synth.cfg2_file(40)
+    raw = bytes(data)
+    seen = set()
+    for trial in range(40):
+        d = bytearray(raw)
+        kind = trial % 4
+        b = int(rng.integers(0, off.size))
+        if kind == 0:                                   # stored crc of block b
+            d[int(off[b]) - 3] ^= 0x10
+        elif kind == 1:                                 # a content byte of block b
+            d[int(off[b]) + int(rng.integers(0, int(ln[b])))] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 2:                                 # restart count of block b
+            e = int(off[b]) + int(ln[b])
+            d[e - 4:e] = int(rng.integers(0, 1 << 32)).to_bytes(4, "little")
+        else:                                           # header byte of block b's first entry
+            d[int(off[b]) + 1] ^= 0x80
+        for verify in (True, False):
+            exp = _check(oracle, bytes(d), verify=verify)
+            seen.add(exp["end"])
+    assert rd.END_PANIC in seen and rd.END_NONE in seen

@@ -137,6 +137,24 @@ int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, co
                     const uint32_t* val_end, uint64_t val_base, uint32_t nent, uint64_t* blk_off,
                     uint32_t* blk_len, int32_t* dir_st, void* stream);
 
+/* ---- batched point lookups (f2) ----
+ * Reader::get (src/reader.rs:111-122) for nq keys at once: index_iter.seek(key) ->
+ * block_at_index -> BlockIter::seek(key) -> the first record if its key equals `key`
+ * (the next index entry's first record when the seek runs past the block), with the
+ * reference's exact BlockIter::seek (src/block.rs:154-194) on the raw index and data blocks.
+ * file: the whole mtbl file on the device; index_off/index_len: the index block content
+ * (host-side framing, mtblx_frame_block); verify: check each data block's crc32c as
+ * Reader::block does.  keys[key_end[q-1] .. key_end[q]) = query q (device).
+ * Per query: status[q], and for FOUND the value at file[val_off[q] .. + val_len[q]). */
+#define MTBLX_GET_FOUND 0
+#define MTBLX_GET_NONE 1    /* Ok(None)                                      */
+#define MTBLX_GET_PANIC 2   /* the reference panics                          */
+#define MTBLX_GET_ERR 3     /* Err(InvalidBlock)                             */
+#define MTBLX_GET_LOOP 4    /* the reference never returns (zero-progress entry) */
+int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
+              uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
+              uint64_t* val_off, uint64_t* val_len, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

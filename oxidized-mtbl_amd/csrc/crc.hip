@@ -9,77 +9,14 @@
 // and the wave XOR-reduces.  The 0xFFFFFFFF init is folded in by complementing the first 4
 // content bytes (equivalent for blocks of >= 4 bytes); the result is complemented at the end.
 // x^(512 m) for any chunk index m comes from three 512-entry tables (9 bits each), computed
-// at compile time.
-//
-// HBM-bound byte work: reads each content byte once, ~1 LDS table lookup per byte.
+// at compile time (crc_dev.h).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc_dev.h"
 #include "mtblx.h"
 
 namespace mtblx_crc {
-
-typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
-
-constexpr uint32_t kPoly = 0x82F63B78u;
-constexpr int kChunk = 64;
-constexpr int kWave = 64;
-constexpr int kThreads = 256;
-
-constexpr uint32_t multmodp(uint32_t a, uint32_t b) {  // a * b mod P, reflected (x^0 = bit 31)
-  uint32_t p = 0;
-  for (int i = 0; i < 32; ++i) {
-    if (a & (0x80000000u >> i)) p ^= b;
-    b = (b & 1u) ? (b >> 1) ^ kPoly : b >> 1;
-  }
-  return p;
-}
-
-struct Tables {
-  uint32_t byte[256];   // byte-wise table
-  uint32_t x0[512];     // x^(512 * m)            m < 512
-  uint32_t x1[512];     // x^(512 * 512 * m)
-  uint32_t x2[512];     // x^(512 * 512 * 512 * m)
-  constexpr Tables() : byte(), x0(), x1(), x2() {
-    for (uint32_t i = 0; i < 256; ++i) {
-      uint32_t c = i;
-      for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
-      byte[i] = c;
-    }
-    // x^8 = one byte of shift; x^(512) = 64 bytes
-    uint32_t x8 = 0x80000000u;                                   // x^0
-    for (int k = 0; k < 8; ++k) x8 = (x8 & 1u) ? (x8 >> 1) ^ kPoly : x8 >> 1;   // x^8
-    uint32_t x512 = 0x80000000u;
-    for (int k = 0; k < kChunk; ++k) x512 = multmodp(x8, x512);
-    x0[0] = 0x80000000u;
-    for (int m = 1; m < 512; ++m) x0[m] = multmodp(x512, x0[m - 1]);
-    const uint32_t s1 = multmodp(x512, x0[511]);                  // x^(512 * 512)
-    x1[0] = 0x80000000u;
-    for (int m = 1; m < 512; ++m) x1[m] = multmodp(s1, x1[m - 1]);
-    const uint32_t s2 = multmodp(s1, x1[511]);                    // x^(512 * 512^2)
-    x2[0] = 0x80000000u;
-    for (int m = 1; m < 512; ++m) x2[m] = multmodp(s2, x2[m - 1]);
-  }
-};
-
-__constant__ Tables kTab = Tables();
-
-__device__ __forceinline__ uint32_t dmultmodp(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    p ^= ((a << i) & 0x80000000u) ? b : 0u;
-    b = (b >> 1) ^ ((b & 1u) ? kPoly : 0u);
-  }
-  return p;
-}
-
-__device__ __forceinline__ uint32_t xpow512(uint64_t m) {  // x^(512 m) mod P
-  uint32_t r = kTab.x0[m & 511];
-  if (m >> 9) r = dmultmodp(kTab.x1[(m >> 9) & 511], r);
-  if (m >> 18) r = dmultmodp(kTab.x2[(m >> 18) & 511], r);
-  return r;
-}
 
 __global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data, const uint64_t* blk_off,
                                                             const uint32_t* blk_len, uint32_t nblk, uint32_t* crc_out,
@@ -93,38 +30,7 @@ __global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data,
     const uint64_t off = blk_off[b];
     const uint64_t L = blk_len[b];
     const uint8_t* d = data + off;
-    uint32_t acc = 0;
-    if (L >= (uint64_t)kChunk) {
-      for (uint64_t j = lane; j * kChunk < L; j += kWave) {
-        // chunk [lo, hi); the 64-byte window [lo, lo + 64) is always inside the block
-        const uint64_t hi = L - j * kChunk, lo = hi > (uint64_t)kChunk ? hi - kChunk : 0;
-        const uint32_t n = (uint32_t)(hi - lo);
-        uint32_t w[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
-          w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
-        }
-        // the 0xFFFFFFFF init, folded into the block's first 4 bytes (they may straddle the
-        // leftmost two chunks when the leftmost one is shorter than 4 bytes)
-        if (lo < 4) w[0] ^= 0xFFFFFFFFu >> (8 * lo);
-        uint32_t c = 0;
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-          const uint32_t byte = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-          const uint32_t nc = T[(c ^ byte) & 0xFFu] ^ (c >> 8);
-          c = ((uint32_t)k < n) ? nc : c;
-        }
-        acc ^= dmultmodp(xpow512(j), c);
-      }
-#pragma unroll
-      for (int s = 32; s >= 1; s >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, s, kWave);
-      acc ^= 0xFFFFFFFFu;
-    } else if (lane == 0) {   // short block: serial
-      uint32_t c = 0xFFFFFFFFu;
-      for (uint64_t i = 0; i < L; ++i) c = T[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
-      acc = c ^ 0xFFFFFFFFu;
-    }
+    const uint32_t acc = wave_crc32c(d, L, T, lane);
     if (lane == 0) {
       crc_out[b] = acc;
       if (bad) {

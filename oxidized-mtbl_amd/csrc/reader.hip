@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc_dev.h"
 #include "mtblx.h"
 
 namespace mtblx_rd {
@@ -88,6 +89,267 @@ __global__ void k_block_dir(const uint8_t* file, uint64_t file_len, uint32_t ver
   dir_st[i] = st;
 }
 
+
+// ------------------------------------------------------------------------------------
+// batched point lookups (f2): Reader::get (src/reader.rs:111-122) for many keys at once.
+// One wave per query; the seek logic runs wave-uniform (every lane computes the same
+// values), the lanes share the CRC-32C of each data block the lookup loads.
+// Restated from the reference (and the oracle, oracle/mtbl_oracle.c):
+//   BlockIter::seek          src/block.rs:154-194  (restart binary search + linear scan)
+//   parse_next_key           src/block.rs:119-143  (truncate/extend, Vec capacity assert)
+//   decode_entry             src/block.rs:216-238
+//   ReaderIntoIter::new_from src/reader.rs:256-279, next (Get) :337-405
+// Keys are never materialised: the scan tracks the length of the common prefix of the
+// current key with the target and the sign of the first difference.
+// ------------------------------------------------------------------------------------
+constexpr uint64_t kU32 = 0xFFFFFFFFull;
+
+struct Blk {
+  const uint8_t* d;
+  uint64_t L, R;
+  uint32_t n;
+};
+
+struct It {
+  uint64_t current, next, klen, kcap, c, voff, vlen;
+  int cmp;            // sign of key[c] - target[c] when c < min(klen, tlen), else 0
+  bool has_next;
+};
+
+enum { R_OK = 1, R_END = 0, R_PANIC = -1, R_LOOP = -2 };
+
+__device__ __forceinline__ uint32_t rd32g(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// varint_decode32 on d[0..n), n >= 1
+__device__ __forceinline__ uint32_t dec32g(const uint8_t* d, uint64_t n, uint32_t& v) {
+  const uint32_t l = length_packed(d, n < 5 ? n : 5);
+  uint32_t val = d[0] & 0x7fu;
+  if (l > 1) val |= (uint32_t)(d[1] & 0x7fu) << 7;
+  if (l > 2) val |= (uint32_t)(d[2] & 0x7fu) << 14;
+  if (l > 3) val |= (uint32_t)(d[3] & 0x7fu) << 21;
+  if (l > 4) val |= (uint32_t)d[4] << 28;
+  v = val;
+  return l;
+}
+
+// Block::init (src/block.rs:16-49): 0 ok, 1 InvalidBlock, -1 panic
+__device__ __forceinline__ int block_init(const uint8_t* d, uint64_t L, Blk& b) {
+  if (L < 4) return 1;
+  if (L < 8) return -1;
+  const uint32_t n = rd32g(d + L - 4);
+  uint64_t ro = L - (1ull + n) * 4ull;
+  if (ro > kU32) {
+    ro = L - (4ull + (uint64_t)n * 8ull);
+    if (ro <= kU32) return 1;
+  }
+  if (ro > L - 4) return 1;
+  if (ro > kU32) return -1;   // u64 restart arrays (>= 4 GiB): not supported on the device
+  b.d = d; b.L = L; b.R = ro; b.n = n;
+  return 0;
+}
+
+__device__ __forceinline__ uint64_t restart_point(const Blk& b, uint32_t i) { return rd32g(b.d + b.R + 4ull * i); }
+
+// decode_entry (src/block.rs:216-238): R_OK or R_PANIC
+__device__ __forceinline__ int decode_entry(const Blk& b, uint64_t p, uint64_t limit, uint32_t& sh, uint32_t& ns,
+                                            uint32_t& vl, uint64_t& pout) {
+  if (limit - p < 3) return R_PANIC;
+  if (p + 2 >= b.L) return R_PANIC;
+  uint32_t x = b.d[p], y = b.d[p + 1], z = b.d[p + 2];
+  if ((x | y | z) < 128u) {
+    p += 3;
+  } else {
+    if (p >= b.L) return R_PANIC;
+    p += dec32g(b.d + p, b.L - p, x);
+    if (p >= b.L) return R_PANIC;
+    p += dec32g(b.d + p, b.L - p, y);
+    if (p >= b.L) return R_PANIC;
+    p += dec32g(b.d + p, b.L - p, z);
+    if (!(p <= limit)) return R_PANIC;
+  }
+  const uint64_t sum = (uint64_t)y + z;
+  if (sum > kU32 || (limit - p) < sum) return R_PANIC;
+  sh = x; ns = y; vl = z; pout = p;
+  return R_OK;
+}
+
+__device__ __forceinline__ int cmp_key(const It& it, uint64_t tlen) {   // Ord of key vs target
+  if (it.cmp) return it.cmp;
+  return it.klen < tlen ? -1 : (it.klen > tlen ? 1 : 0);
+}
+
+__device__ __forceinline__ void restart_at(const Blk& b, It& it, uint32_t i) {   // seek_to_restart_point
+  it.klen = 0; it.c = 0; it.cmp = 0;
+  it.has_next = true;
+  it.next = restart_point(b, i);
+}
+
+// parse_next_key (src/block.rs:119-143) with the common-prefix tracking; R_OK / R_END /
+// R_PANIC / R_LOOP (an entry that does not advance: the reference spins forever)
+__device__ int parse_next_key(const Blk& b, It& it, const uint8_t* t, uint64_t tlen) {
+  const uint64_t prev = it.current;
+  it.current = it.has_next ? it.next : 0;
+  if (it.current >= b.R) { it.current = b.R; return R_END; }
+  uint32_t sh, ns, vl;
+  uint64_t p;
+  if (decode_entry(b, it.current, b.R, sh, ns, vl, p) != R_OK) return R_PANIC;
+  if (!(it.kcap >= sh)) return R_PANIC;                     // Vec capacity assert (:132)
+  const uint64_t m = sh < it.klen ? sh : it.klen;           // truncate (:134)
+  if (p + ns > b.L) return R_PANIC;
+  if (ns > 0 && it.kcap - m < ns) {                         // Vec growth (:135)
+    uint64_t c = it.kcap * 2, req = m + ns;
+    if (req > c) c = req;
+    if (c < 8) c = 8;
+    it.kcap = c;
+  }
+  if (m <= it.c) {            // the kept prefix matches the target: compare the suffix
+    uint64_t c = m, j = 0;
+    while (j < ns && c < tlen && b.d[p + j] == t[c]) { ++j; ++c; }
+    it.cmp = (j < ns && c < tlen) ? (b.d[p + j] < t[c] ? -1 : 1) : 0;
+    it.c = c;
+  }                           // else: the first difference lies in the kept prefix
+  it.klen = m + ns;
+  it.has_next = true;
+  it.next = p + ns + vl;
+  it.voff = p + ns;
+  it.vlen = vl;
+  if (it.next == it.current && it.current == prev) return R_LOOP;
+  return R_OK;
+}
+
+// BlockIter::seek (src/block.rs:154-194)
+__device__ int seek(const Blk& b, It& it, const uint8_t* t, uint64_t tlen) {
+  uint32_t left = 0, right = b.n - 1;
+  while (left < right) {
+    const uint32_t mid = (uint32_t)(((uint64_t)left + right + 1) / 2);
+    uint32_t sh, ns, vl;
+    uint64_t ko;
+    if (decode_entry(b, restart_point(b, mid), b.R, sh, ns, vl, ko) != R_OK) return R_PANIC;
+    if (sh != 0) return R_OK;                                 // "corruption": early return
+    if (ko + ns > b.L) return R_PANIC;
+    uint64_t c = 0;
+    while (c < ns && c < tlen && b.d[ko + c] == t[c]) ++c;
+    const int r = (c < ns && c < tlen) ? (b.d[ko + c] < t[c] ? -1 : 1) : (ns < tlen ? -1 : (ns > tlen ? 1 : 0));
+    if (r < 0) left = mid;
+    else right = mid - 1;
+  }
+  restart_at(b, it, left);
+  for (uint64_t steps = 0;; ++steps) {
+    const uint64_t before = it.current;
+    const int r = parse_next_key(b, it, t, tlen);
+    if (r != R_OK) return r == R_END ? R_OK : r;
+    if (cmp_key(it, tlen) >= 0) return R_OK;
+    if (it.next == it.current || (steps > 0 && it.current == before)) return R_LOOP;
+  }
+}
+
+__device__ __forceinline__ bool valid(const Blk& b, const It& it) { return it.current < b.R; }
+
+// BlockIter::init (src/block.rs:75-93)
+__device__ __forceinline__ int iter_init(const Blk& b, It& it) {
+  if (b.n == 0) return R_PANIC;
+  it.current = b.R; it.has_next = false; it.next = 0;
+  it.klen = 0; it.kcap = 0; it.c = 0; it.cmp = 0; it.voff = 0; it.vlen = 0;
+  return R_OK;
+}
+
+struct FileCtx {
+  const uint8_t* file;
+  uint64_t len;
+  uint32_t version;
+  int verify;
+  const uint32_t* T;   // crc byte table (LDS)
+  int lane;
+};
+
+// block_at_index + Reader::block (src/reader.rs:177-186, :139-174):
+// 1 = Some(block), 0 = None, R_PANIC, 2 = Err(InvalidBlock)
+__device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk& out) {
+  if (!valid(ib, ii)) return 0;                                // get() -> None
+  if (ii.voff + ii.vlen > ib.L) return R_PANIC;
+  uint64_t off = 0;
+  if (dec64(ib.d + ii.voff, ii.vlen, off) < 0) return R_PANIC;
+  if (!(off < f.len)) return R_PANIC;
+  uint64_t ll, sz;
+  if (f.version == 0) {
+    if (off + 4 > f.len) return R_PANIC;
+    ll = 4; sz = rd32g(f.file + off);
+  } else {
+    const int k = dec64(f.file + off, f.len - off, sz);
+    if (k < 0) return R_PANIC;
+    ll = (uint64_t)k;
+  }
+  const uint64_t start = off + ll + 4;
+  if (start > f.len || sz > f.len - start) return R_PANIC;
+  if (f.verify && mtblx_crc::wave_crc32c(f.file + start, sz, f.T, f.lane) != rd32g(f.file + off + ll)) return R_PANIC;
+  const int bi = block_init(f.file + start, sz, out);
+  if (bi == 1) return 2;
+  if (bi < 0) return R_PANIC;
+  return 1;
+}
+
+__global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
+                                             uint64_t idx_off, uint64_t idx_len, const uint8_t* qkeys,
+                                             const uint64_t* qend, uint32_t nq, int32_t* st, uint64_t* voff,
+                                             uint64_t* vlen) {
+  __shared__ uint32_t T[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = mtblx_crc::kTab.byte[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves = gridDim.x * (blockDim.x / 64);
+  const FileCtx f{file, file_len, version, verify, T, lane};
+  for (uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); q < nq; q += waves) {
+    const uint64_t k0 = q ? qend[q - 1] : 0, k1 = qend[q];
+    const uint8_t* t = qkeys + k0;
+    const uint64_t tl = k1 - k0;
+    int32_t res = MTBLX_GET_NONE;
+    uint64_t ro = 0, rl = 0;
+    Blk ib{};
+    It ii{}, di{};
+    Blk db{};
+    do {
+      const int ibi = block_init(file + idx_off, idx_len, ib);   // the Reader's index block
+      if (ibi != 0) { res = ibi == 1 ? MTBLX_GET_ERR : MTBLX_GET_PANIC; break; }
+      if (iter_init(ib, ii) != R_OK) { res = MTBLX_GET_PANIC; break; }
+      int r = seek(ib, ii, t, tl);                                // new_from: index_iter.seek(key)
+      if (r != R_OK) { res = r == R_LOOP ? MTBLX_GET_LOOP : MTBLX_GET_PANIC; break; }
+      int b = block_at_index(f, ib, ii, db);
+      if (b == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+      if (b == 2) { res = MTBLX_GET_ERR; break; }                  // Err at open (new_get)
+      if (b == 0) break;                                           // no block: next() -> None
+      if (iter_init(db, di) != R_OK) { res = MTBLX_GET_PANIC; break; }
+      r = seek(db, di, t, tl);                                     // bi.seek(key)
+      if (r != R_OK) { res = r == R_LOOP ? MTBLX_GET_LOOP : MTBLX_GET_PANIC; break; }
+      // next() (first call, Get)
+      if (valid(db, di)) {
+        if (di.voff + di.vlen > db.L) { res = MTBLX_GET_PANIC; break; }
+        if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - file) + di.voff; rl = di.vlen; }
+        break;
+      }
+      // the seek ran past the end of the block: the next index entry's first record
+      if (!valid(ib, ii)) break;
+      r = parse_next_key(ib, ii, t, tl);
+      if (r == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+      if (r == R_LOOP) { res = MTBLX_GET_LOOP; break; }
+      if (!valid(ib, ii)) break;
+      b = block_at_index(f, ib, ii, db);
+      if (b == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+      if (b == 2) { res = MTBLX_GET_ERR; break; }                  // Some(Err) from next()
+      if (b == 0) break;
+      if (iter_init(db, di) != R_OK) { res = MTBLX_GET_PANIC; break; }
+      restart_at(db, di, 0);                                       // seek_to_first
+      r = parse_next_key(db, di, t, tl);
+      if (r == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+      if (!valid(db, di)) break;
+      if (di.voff + di.vlen > db.L) { res = MTBLX_GET_PANIC; break; }
+      if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - file) + di.voff; rl = di.vlen; }
+    } while (false);
+    if (lane == 0) { st[q] = res; voff[q] = ro; vlen[q] = rl; }
+  }
+}
+
 }  // namespace mtblx_rd
 
 extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, const uint8_t* vals,
@@ -99,5 +361,24 @@ extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t 
   hipLaunchKernelGGL(mtblx_rd::k_block_dir, dim3((nent + threads - 1) / threads), dim3(threads), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, vals, val_end, val_base, nent,
                      blk_off, blk_len, dir_st);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
+                         uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
+                         uint64_t* val_off, uint64_t* val_len, void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!file || !keys || !key_end || !status || !val_off || !val_len || version > 1) return MTBLX_E_INVAL;
+  static int grid = 0;
+  if (!grid) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = (ncu > 0 ? ncu : 256) * 8;
+  }
+  const uint32_t need = (nq + 3u) / 4u;
+  hipLaunchKernelGGL(mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len, keys,
+                     key_end, nq, status, val_off, val_len);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

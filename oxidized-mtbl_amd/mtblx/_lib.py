@@ -20,11 +20,12 @@ i32p = C.POINTER(C.c_int32)
 MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT = 0, -1, -2, -3, -4
 ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW = range(6)
 DIR_OK, DIR_PANIC, DIR_UNSUPPORTED = range(3)
+GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP = range(5)
 
 # every symbol the public headers declare (checked by tests/test_abi.py)
 EXPORTS = [
     "mtblx_abi_version", "mtblx_device_ok", "mtblx_decode_workspace_bytes", "mtblx_decode_blocks",
-    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
+    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_get", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
     "mtblx_writer_new", "mtblx_writer_insert", "mtblx_writer_insert_batch", "mtblx_writer_finish",
     "mtblx_writer_block_count", "mtblx_writer_block_dir", "mtblx_writer_free", "mtblx_free",
 ]
@@ -68,6 +69,9 @@ def lib() -> C.CDLL:
         L.mtblx_block_dir.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,
                                       C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.mtblx_block_dir.restype = C.c_int
+        L.mtblx_get.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p,
+                                C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mtblx_get.restype = C.c_int
         L.mtblx_crc32c.argtypes = [u8p, C.c_uint64]
         L.mtblx_crc32c.restype = C.c_uint32
         L.mtblx_varint_decode64.argtypes = [u8p, C.c_uint64, u64p]

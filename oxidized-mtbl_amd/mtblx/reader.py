@@ -128,6 +128,7 @@ class Reader:
             raise ReferencePanic("index block framing / checksum (src/reader.rs:52-74)")
         if rc != 0:
             raise MtblError(3)
+        self.index_off, self.index_len = int(coff.value), int(clen.value)
         # index block on the device
         self._ibatch = codec.DeviceBatch(self.file, torch.tensor([coff.value], dtype=torch.int64, device=device),
                                          torch.tensor([clen.value], dtype=torch.int32, device=device),
@@ -254,16 +255,46 @@ class Reader:
         return Scan(end, err, nrec, d.keys[:klen], d.vals[:vlen], key_end, val_end)
 
     # ------------------------------------------------------------------ point queries
+    def get_batch(self, keys, stream=None):
+        """Reader::get for every key at once on the device (mtblx_get, f2).
+        -> (status int32 [nq] (GET_*), val_off int64 [nq], val_len int64 [nq]) device tensors;
+        the value of a FOUND query q is file[val_off[q] : val_off[q] + val_len[q]]."""
+        dev = self.file.device
+        ks = [bytes(k) for k in keys]
+        nq = len(ks)
+        blob = b"".join(ks) or b"\0"
+        kb = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+        ke = torch.tensor(np.cumsum([len(k) for k in ks], dtype=np.int64) if nq else [0], dtype=torch.int64,
+                          device=dev)
+        n = max(nq, 1)
+        st = torch.zeros(n, dtype=torch.int32, device=dev)
+        vo = torch.zeros(n, dtype=torch.int64, device=dev)
+        vl = torch.zeros(n, dtype=torch.int64, device=dev)
+        rc = _lib.lib().mtblx_get(C.c_void_p(self.file.data_ptr()), self.len, self.version, 1 if self.verify else 0,
+                                  self.index_off, self.index_len, C.c_void_p(kb.data_ptr()),
+                                  C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()), C.c_void_p(vo.data_ptr()),
+                                  C.c_void_p(vl.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
+        if rc != 0:
+            raise RuntimeError(f"mtblx_get failed: {rc}")
+        return st[:nq], vo[:nq], vl[:nq]
+
+    def get(self, key: bytes):
+        """Reader::get (src/reader.rs:111-122): the value of `key`, or None; raises where the
+        reference panics / returns Err."""
+        st, vo, vl = self.get_batch([key])
+        s = int(st[0].item())
+        if s == _lib.GET_FOUND:
+            o, n = int(vo[0].item()), int(vl[0].item())
+            return self.file[o: o + n].cpu().numpy().tobytes()
+        if s == _lib.GET_NONE:
+            return None
+        if s == _lib.GET_ERR:
+            raise MtblError(6)
+        raise ReferencePanic("Reader::get" + (" never returns" if s == _lib.GET_LOOP else ""))
+
     def _sorted_keys(self):
         s = self.iter()
         return s, s.records()
-
-    def get(self, key: bytes):
-        """Reader::get (src/reader.rs:111-115): the value of `key`, or None."""
-        s, recs = self._sorted_keys()
-        import bisect
-        i = bisect.bisect_left([k for k, _ in recs], bytes(key))
-        return recs[i][1] if i < len(recs) and recs[i][0] == bytes(key) else None
 
     def get_prefix(self, prefix: bytes):
         s, recs = self._sorted_keys()

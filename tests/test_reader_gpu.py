@@ -84,3 +84,56 @@ def test_corrupted_files(oracle):
             exp = _check(oracle, bytes(d), verify=verify)
             seen.add(exp["end"])
     assert rd.END_PANIC in seen and rd.END_NONE in seen
+
+
+def _check_get(oracle, data: bytes, queries, verify=True):
+    rd = _reader()
+    from mtblx import _lib
+    r = rd.ReaderBuilder().verify_checksums(verify).read(data)
+    st, vo, vl = r.get_batch(queries)
+    st = st.cpu().numpy()
+    vo = vo.cpu().numpy()
+    vl = vl.cpu().numpy()
+    end_of = {rd.END_NONE: _lib.GET_NONE, rd.END_PANIC: _lib.GET_PANIC, rd.END_ERR_OPEN: _lib.GET_ERR,
+              rd.END_ERR_NEXT: _lib.GET_ERR, rd.END_LOOP: _lib.GET_LOOP}
+    for q, key in enumerate(queries):
+        exp = oracle.file_scan(data, "get", key=key, verify=verify)
+        if exp["records"]:
+            assert exp["end"] == rd.END_NONE
+            assert st[q] == _lib.GET_FOUND, (q, key, st[q])
+            assert data[vo[q]: vo[q] + vl[q]] == exp["records"][0][1]
+        else:
+            assert st[q] == end_of[exp["end"]], (q, key, st[q], exp["end"])
+
+
+def test_get_batch_valid_files(oracle):
+    rng = np.random.default_rng(41)
+    for bs, iv, n in ((1024, 1, 200), (4096, 16, 1500), (65536, 16, 3000), (8192, 3, 800)):
+        recs = corpus.random_records(rng, n, 0, 40, 0, 100)
+        data = _write(recs, bs, iv)
+        keys = [k for k, _ in recs]
+        qs = [keys[int(i)] for i in rng.integers(0, n, 150)]                      # hits
+        qs += [k + b"\x00" for k in qs[:40]] + [k[:-1] for k in qs[:40] if k]   # near misses
+        qs += [b"", b"\xff" * 50, keys[0], keys[-1], keys[-1] + b"\x01"]
+        _check_get(oracle, data, qs)
+
+
+def test_get_batch_corrupted(oracle):
+    from mtblx import synth
+    rng = np.random.default_rng(42)
+    data, off, ln = synth.cfg2_file(30)
+    raw = bytes(data)
+    recs = oracle.file_scan(raw, "iter")["records"]
+    for trial in range(16):
+        d = bytearray(raw)
+        b = int(rng.integers(0, off.size))
+        if trial % 3 == 0:
+            d[int(off[b]) - 3] ^= 0x10                                       # stored crc
+        elif trial % 3 == 1:
+            d[int(off[b]) + int(rng.integers(0, int(ln[b])))] ^= 0xA5          # content byte
+        else:
+            e = int(off[b]) + int(ln[b])
+            d[e - 8:e - 4] = int(rng.integers(0, 1 << 32)).to_bytes(4, "little")   # a restart point
+        qs = [recs[int(i)][0] for i in rng.integers(0, len(recs), 40)] + [b"", b"\xff" * 20]
+        for verify in (True, False):
+            _check_get(oracle, bytes(d), qs, verify=verify)

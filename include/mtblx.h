@@ -51,6 +51,8 @@ extern "C" {
 #define MTBLX_ST_LOOP 3          /* zero-progress entry: the reference yields it forever; emitted once */
 #define MTBLX_ST_UNSUPPORTED 4   /* block >= 4 GiB (u64 restart arrays): not decoded on the device    */
 #define MTBLX_ST_OVERFLOW 5      /* caller's key/value/record capacity exceeded; block not written    */
+#define MTBLX_ST_DECOMPRESS 6    /* (mtblx_pipe_decode) host decompression failed: Reader::block returns
+                                    Err(Error::Io) (src/reader.rs:166, src/compression.rs:57-68)      */
 
 /* A batch of uncompressed block contents already resident on the device.
  * Block b occupies data[blk_off[b] .. blk_off[b] + blk_len[b]). */
@@ -154,6 +156,46 @@ int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, co
 int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
               uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
               uint64_t* val_off, uint64_t* val_len, void* stream);
+
+/* ---- end-to-end decode from host memory (the PCIe-inclusive path of the north star) ----
+ * An mtbl file in host memory in (mmap'd or read), the caller's host byte slices out:
+ * for every data block, Reader::block's decompression (src/reader.rs:166-170, host: the
+ * north star keeps src/compression.rs on the host) + Block::init + the BlockIter scan
+ * (device).  Consecutive blocks are cut into chunks that flow through three stages with
+ * three chunks in flight: host staging (nothing for a pinned uncompressed file; a parallel
+ * copy into pinned memory for a pageable one; parallel snappy decompression), H2D +
+ * mtblx_decode_blocks on the device, D2H of the chunk's outputs into `out`.
+ *   file/blk_off/blk_len: host; block b's STORED content is file[blk_off[b] .. + blk_len[b])
+ *   (the directory mtblx_writer_block_dir / mtblx_block_dir produce).  compression: the
+ *   footer's compression_algorithm: 0 None, 1 Snappy (others: MTBLX_E_INVAL).
+ *   out: mtblx_decoded whose pointers are HOST memory (pin it -- mtblx_host_alloc or
+ *   mtblx_host_register -- for full PCIe rate), same layout and status codes as
+ *   mtblx_decode_blocks plus MTBLX_ST_DECOMPRESS.  If a capacity is too small the outputs of
+ *   the chunks that do not fit are skipped (their blocks: MTBLX_ST_OVERFLOW, totals[3] bit 0)
+ *   and totals[0..2] still report the exact sizes, so a caller can size and call again.
+ * Synchronous: returns when `out` is complete.  One call at a time per pipe. */
+typedef struct mtblx_pipe mtblx_pipe;
+typedef struct mtblx_pipe_stats {
+  double seconds;          /* wall time of the call                                */
+  double stage_seconds;    /* host staging (copies / decompression) on the calling path */
+  double decode_ms;        /* device time of the decode launches (HIP events)     */
+  uint64_t block_bytes;    /* uncompressed block content bytes decoded            */
+  uint64_t h2d_bytes, d2h_bytes;
+  uint32_t chunks;
+  uint32_t decompress_errors;
+} mtblx_pipe_stats;
+/* chunk_bytes: uncompressed bytes per chunk (0 = 64 MiB); max_blocks: blocks per chunk
+ * (0 = 65536); threads: host staging threads (0 = 16).  Binds to the current HIP device. */
+mtblx_pipe* mtblx_pipe_new(uint64_t chunk_bytes, uint32_t max_blocks, uint32_t threads);
+void mtblx_pipe_free(mtblx_pipe* p);
+int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t file_len, uint32_t compression,
+                      const uint64_t* blk_off, const uint32_t* blk_len, uint32_t nblk, const mtblx_decoded* out,
+                      mtblx_pipe_stats* stats);
+/* pinned host memory for the pipe's inputs / outputs */
+int mtblx_host_alloc(void** p, uint64_t bytes);
+int mtblx_host_free(void* p);
+int mtblx_host_register(void* p, uint64_t bytes);   /* pin an existing range, e.g. an mmap'd file */
+int mtblx_host_unregister(void* p);
 
 #ifdef __cplusplus
 }

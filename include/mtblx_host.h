@@ -13,9 +13,9 @@
  * Decoding block contents is NOT done here: every block goes through
  * mtblx_decode_blocks (mtblx.h) on the device.
  *
- * Compression: this round's writer emits CompressionType::None only
- * (mtblx_writer_new returns NULL otherwise); compressed READ support is host
- * decompression feeding the same device path.
+ * Compression (src/compression.rs) stays on the host: snappy raw codec below; compressed
+ * reads are host decompression feeding the same device path (mtblx_pipe_decode in mtblx.h,
+ * mtblx/reader.py).
  */
 #ifndef MTBLX_HOST_H
 #define MTBLX_HOST_H
@@ -57,7 +57,27 @@ int mtblx_read_footer(const uint8_t* file, uint64_t len, mtblx_footer* f);
 int mtblx_frame_block(const uint8_t* file, uint64_t len, uint32_t version, uint64_t off, int verify,
                       uint64_t* content_off, uint64_t* content_len, int* panic);
 
-/* Writer (src/writer.rs).  compression must be 0 (None) this round. */
+/* ---- snappy raw codec (CompressionType::Snappy, src/compression.rs:116-130, crate snap 1.x raw) ----
+ * Host-side, as the north star keeps compression on the host.  Return codes: */
+#define MTBLX_SNAPPY_OK 0
+#define MTBLX_SNAPPY_CORRUPT 1   /* snap::raw::Decoder error -> io::Error -> Error::Io (src/compression.rs:117-118) */
+#define MTBLX_SNAPPY_TOO_SMALL 2 /* destination capacity too small */
+uint64_t mtblx_snappy_max_compressed_len(uint64_t n);
+/* the length stored in the preamble (no validation of the body) */
+int mtblx_snappy_uncompressed_len(const uint8_t* src, uint64_t n, uint64_t* out);
+/* full decompression into dst[0..cap); *out_len = the preamble length */
+int mtblx_snappy_decompress(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, uint64_t* out_len);
+/* valid snappy of src (bytes are not pinned to the reference encoder: SURVEY.md §8c); cap >= max_compressed_len */
+int mtblx_snappy_compress(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, uint64_t* out_len);
+/* batch: block b's stored bytes file[blk_off[b] .. + blk_len[b]) -> dst[dst_off[b] .. + dst_len[b]),
+ * `threads` host threads; st[b] (may be NULL) = MTBLX_SNAPPY_*; returns the number of failed blocks */
+uint64_t mtblx_snappy_decompress_blocks(const uint8_t* file, const uint64_t* blk_off, const uint32_t* blk_len,
+                                        uint8_t* dst, const uint64_t* dst_off, const uint64_t* dst_len, int32_t* st,
+                                        uint64_t nblk, uint32_t threads);
+
+/* Writer (src/writer.rs).  compression: 0 = None, 1 = Snappy (data blocks compressed with
+ * mtblx_snappy_compress; the index block is always None, src/writer.rs:165-173); other values
+ * return NULL (zlib / zstd are out of scope). */
 typedef struct mtblx_writer mtblx_writer;
 mtblx_writer* mtblx_writer_new(uint64_t block_size, uint64_t restart_interval, uint32_t compression);
 /* MTBLX_OK, or MTBLX_E_FORMAT where the reference panics ("out-of-order key", ...) */

@@ -127,6 +127,7 @@ typedef struct {
   uint64_t kalloc;
   int has_val;
   uint64_t voff, vlen;
+  uint8_t* owned;         /* decompressed block bytes (Cow::Owned), freed with the iterator */
 } oiter;
 
 /* Block::init (src/block.rs:16-49) + num_restarts (:58-61).  0 = Some, else status */
@@ -162,7 +163,7 @@ static int oiter_init(oiter* it, const uint8_t* d, uint64_t L, uint64_t ro) {
   return 0;
 }
 
-static void oiter_free(oiter* it) { free(it->key); it->key = NULL; }
+static void oiter_free(oiter* it) { free(it->key); it->key = NULL; free(it->owned); it->owned = NULL; }
 
 /* Vec::extend_from_slice growth (RawVec::grow_amortized): max(2cap, len+add, 8) */
 static void okey_extend(oiter* it, const uint8_t* src, uint64_t n) {
@@ -664,6 +665,70 @@ int32_t oracle_writer_finish(oracle_writer* w, uint8_t** out, uint64_t* out_len)
   return 0;
 }
 
+/* ==================== snappy raw decompression ====================
+ * src/compression.rs:116-119 calls snap::raw::Decoder::decompress_vec (crate snap 1.x, not in
+ * /root/reference).  Restated from the published snappy format (format_description.txt):
+ * varint32 uncompressed length, then literal / copy-1 / copy-2 / copy-4 elements; a copy
+ * offset must be 1..produced; the output must be exactly the stated length.  Any error is
+ * io::Error -> Err(Error::Io).  Byte-at-a-time on purpose (independent of the product's
+ * memcpy-based decoder); pinned against libsnappy in tests/test_snappy.py.
+ * returns 0 and a malloc'd buffer, or ORC_ERR_IO. */
+int32_t oracle_snappy_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len) {
+  uint64_t want = 0, i = 0;
+  int shift = 0, term = 0;
+  while (i < n && i < 5) {
+    uint8_t b = s[i++];
+    want |= (uint64_t)(b & 0x7f) << shift;
+    shift += 7;
+    if (!(b & 0x80)) { term = 1; break; }
+  }
+  if (!term || want > 0xFFFFFFFFull) return ORC_ERR_IO;
+  uint8_t* d = (uint8_t*)malloc(want ? want : 1);
+  uint64_t o = 0;
+  while (i < n) {
+    uint32_t tag = s[i++];
+    uint64_t len, off = 0;
+    if ((tag & 3) == 0) {
+      len = (tag >> 2) + 1;
+      if (len > 60) {
+        uint32_t nb = (uint32_t)len - 60;
+        if (n - i < nb) goto bad;
+        len = 0;
+        for (uint32_t k = 0; k < nb; k++) len |= (uint64_t)s[i + k] << (8 * k);
+        len += 1;
+        i += nb;
+      }
+      if (n - i < len || want - o < len) goto bad;
+      for (uint64_t k = 0; k < len; k++) d[o++] = s[i++];
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (n - i < 1) goto bad;
+      len = 4 + ((tag >> 2) & 7);
+      off = ((uint64_t)(tag >> 5) << 8) | s[i++];
+    } else if ((tag & 3) == 2) {
+      if (n - i < 2) goto bad;
+      len = 1 + (tag >> 2);
+      off = (uint64_t)s[i] | ((uint64_t)s[i + 1] << 8);
+      i += 2;
+    } else {
+      if (n - i < 4) goto bad;
+      len = 1 + (tag >> 2);
+      off = (uint64_t)s[i] | ((uint64_t)s[i + 1] << 8) | ((uint64_t)s[i + 2] << 16) | ((uint64_t)s[i + 3] << 24);
+      i += 4;
+    }
+    if (off == 0 || off > o || want - o < len) goto bad;
+    for (uint64_t k = 0; k < len; k++, o++) d[o] = d[o - off];
+  }
+  if (o != want) goto bad;
+  *out = d;
+  *out_len = want;
+  return 0;
+bad:
+  free(d);
+  return ORC_ERR_IO;
+}
+
 /* ==================== file-level iteration: src/reader.rs ==================== */
 typedef struct {
   const uint8_t* d; uint64_t len;
@@ -713,7 +778,9 @@ static int oreader_open(oreader* r, const uint8_t* d, uint64_t len, int verify) 
 }
 
 /* Reader::block (:140-175): 0 = ok (blk, blen point into the file), PANIC, ORC_ERR_* */
-static int oreader_block(const oreader* r, uint64_t off, const uint8_t** blk, uint64_t* blen, uint64_t* ro) {
+static int oreader_block(const oreader* r, uint64_t off, const uint8_t** blk, uint64_t* blen, uint64_t* ro,
+                         uint8_t** owned) {
+  *owned = NULL;
   if (!(off < r->len)) return PANIC;
   uint64_t ll, sz;
   if (r->version == 0) {
@@ -728,11 +795,18 @@ static int oreader_block(const oreader* r, uint64_t off, const uint8_t** blk, ui
   uint64_t start = off + ll + 4;
   if (start > r->len || sz > r->len - start) return PANIC;
   if (r->verify && rd32(r->d + off + ll) != oracle_crc32c(r->d + start, sz)) return PANIC;
-  if (r->meta[M_COMP] != 0) return ORC_ERR_IO;  /* compressed files: oracle does not decompress */
-  int st = oblock_init(r->d + start, sz, ro);
-  if (st == ORC_ST_INVALID_BLOCK) return ORC_ERR_INVALID_BLOCK;
-  if (st) return PANIC;
-  *blk = r->d + start; *blen = sz;
+  const uint8_t* b = r->d + start;
+  if (r->meta[M_COMP] == 1) {                               /* decompress (:166-170) */
+    uint8_t* u; uint64_t ul;
+    if (oracle_snappy_decompress(b, sz, &u, &ul)) return ORC_ERR_IO;
+    *owned = u; b = u; sz = ul;
+  } else if (r->meta[M_COMP] != 0) {
+    return ORC_ERR_IO;   /* zlib / zstd: out of scope for this oracle */
+  }
+  int st = oblock_init(b, sz, ro);
+  if (st == ORC_ST_INVALID_BLOCK) { free(*owned); *owned = NULL; return ORC_ERR_INVALID_BLOCK; }
+  if (st) { free(*owned); *owned = NULL; return PANIC; }
+  *blk = b; *blen = sz;
   return 0;
 }
 
@@ -766,10 +840,12 @@ static int oblock_at_index(const oreader* r, const oiter* idx, oiter* bi) {
   uint64_t off = 0;
   if (oracle_varint_decode64(idx->d + idx->voff, idx->vlen, &off) < 0) return PANIC;
   const uint8_t* blk; uint64_t blen, ro;
-  int e = oreader_block(r, off, &blk, &blen, &ro);
+  uint8_t* owned;
+  int e = oreader_block(r, off, &blk, &blen, &ro, &owned);
   if (e == PANIC) return PANIC;
   if (e > 0) return -10 - e;
-  if (oiter_init(bi, blk, blen, ro)) return PANIC;         /* BlockIter::init assert */
+  if (oiter_init(bi, blk, blen, ro)) { free(owned); return PANIC; }   /* BlockIter::init assert */
+  bi->owned = owned;
   return 1;
 }
 

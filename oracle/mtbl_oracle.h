@@ -51,6 +51,10 @@ uint32_t oracle_varint_encode64(uint8_t* out, uint64_t value);
 int32_t oracle_varint_decode32(const uint8_t* data, uint64_t len, uint32_t* value);
 int32_t oracle_varint_decode64(const uint8_t* data, uint64_t len, uint64_t* value);
 
+/* ---- snappy raw decompression (src/compression.rs:116-119, crate snap 1.x): 0 + malloc'd
+ * *out, or 7 (ORC_ERR_IO) where the reference returns Err(Error::Io) ---- */
+int32_t oracle_snappy_decompress(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len);
+
 /* ---- crc32c (crate crc32c 0.4: CRC-32C Castagnoli, reflected 0x82F63B78) ---- */
 uint32_t oracle_crc32c(const uint8_t* data, uint64_t len);
 

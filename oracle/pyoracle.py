@@ -70,6 +70,8 @@ def lib():
                                        C.c_uint64, C.c_void_p]
         L.oracle_file_scan.restype = C.c_int32
         L.oracle_scan_free.argtypes = [C.c_void_p]
+        L.oracle_snappy_decompress.argtypes = [u8p, C.c_uint64, C.POINTER(u8p), u64p]
+        L.oracle_snappy_decompress.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -124,6 +126,19 @@ def shortest_separator(start: bytes, limit: bytes):
     lim = (C.c_uint8 * max(1, len(limit)))(*limit) if limit else (C.c_uint8 * 1)()
     n = lib().oracle_shortest_separator(buf, len(start), lim, len(limit))
     return None if n < 0 else bytes(buf[:n])
+
+
+def snappy_decompress(data: bytes):
+    """-> bytes, or None where the reference's snap decoder errors (Err(Error::Io))."""
+    L = lib()
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_uint64(0)
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+    if L.oracle_snappy_decompress(buf, len(data), C.byref(out), C.byref(n)) != 0:
+        return None
+    r = C.string_at(out, n.value) if n.value else b""
+    L.oracle_free(out)
+    return r
 
 
 # ---------------- writer / builder ----------------

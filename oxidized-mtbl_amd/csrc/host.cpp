@@ -164,8 +164,8 @@ struct mtblx_writer {
   bool pending_index_entry = false;
   bool poisoned = false;
   std::vector<uint8_t> out;
-  std::vector<uint8_t> scratch;
-  std::vector<uint64_t> blk_off;  // content offset of each data block (block directory)
+  std::vector<uint8_t> scratch, zbuf;
+  std::vector<uint64_t> blk_off;  // stored-content offset of each data block (block directory)
   std::vector<uint32_t> blk_len;
   std::vector<uint32_t> blk_nrec;
   uint32_t cur_nrec = 0;
@@ -174,21 +174,31 @@ struct mtblx_writer {
     meta[2] = comp;
     compression = comp;
   }
-  // write_block (:203-237); compression None only on this path (see mtblx_host.h)
+  // write_block (:203-237): data blocks are compressed with the file's compression type
+  // (:214), the index block never (into_inner passes CompressionType::None, :165-173); the
+  // checksum covers the STORED bytes (:217-218)
   uint64_t write_block(BlockBuilder& b, bool is_data) {
     b.finish(scratch);
+    const std::vector<uint8_t>* stored = &scratch;
+    if (is_data && compression == 1) {
+      zbuf.resize(mtblx_snappy_max_compressed_len(scratch.size()));
+      uint64_t zl = 0;
+      mtblx_snappy_compress(scratch.data(), scratch.size(), zbuf.data(), zbuf.size(), &zl);
+      zbuf.resize(zl);
+      stored = &zbuf;
+    }
     uint8_t hdr[14];
-    uint32_t ll = venc64(hdr, scratch.size());
-    wr32(hdr + ll, mtblx_crc32c(scratch.data(), scratch.size()));
+    uint32_t ll = venc64(hdr, stored->size());
+    wr32(hdr + ll, mtblx_crc32c(stored->data(), stored->size()));
     out.insert(out.end(), hdr, hdr + ll + 4);
     if (is_data) {
       blk_off.push_back(out.size());
-      blk_len.push_back((uint32_t)scratch.size());
+      blk_len.push_back((uint32_t)stored->size());
       blk_nrec.push_back(cur_nrec);
       cur_nrec = 0;
     }
-    out.insert(out.end(), scratch.begin(), scratch.end());
-    uint64_t written = ll + 4 + scratch.size();
+    out.insert(out.end(), stored->begin(), stored->end());
+    uint64_t written = ll + 4 + stored->size();
     last_offset = pending_offset;
     pending_offset += written;
     b.reset();
@@ -205,7 +215,7 @@ struct mtblx_writer {
 };
 
 extern "C" mtblx_writer* mtblx_writer_new(uint64_t block_size, uint64_t restart_interval, uint32_t compression) {
-  if (compression != 0) return nullptr;  // compressed writing: see mtblx_host.h
+  if (compression > 1) return nullptr;  // None and Snappy only (mtblx_host.h)
   return new mtblx_writer(block_size, restart_interval, compression);
 }
 

@@ -18,7 +18,8 @@ u64p = C.POINTER(C.c_uint64)
 i32p = C.POINTER(C.c_int32)
 
 MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT = 0, -1, -2, -3, -4
-ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW = range(6)
+ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW, ST_DECOMPRESS = range(7)
+SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL = range(3)
 DIR_OK, DIR_PANIC, DIR_UNSUPPORTED = range(3)
 GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP = range(5)
 
@@ -28,6 +29,9 @@ EXPORTS = [
     "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_get", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
     "mtblx_writer_new", "mtblx_writer_insert", "mtblx_writer_insert_batch", "mtblx_writer_finish",
     "mtblx_writer_block_count", "mtblx_writer_block_dir", "mtblx_writer_free", "mtblx_free",
+    "mtblx_snappy_max_compressed_len", "mtblx_snappy_uncompressed_len", "mtblx_snappy_decompress",
+    "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
+    "mtblx_pipe_decode", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
 ]
 
 
@@ -41,6 +45,12 @@ class Decoded(C.Structure):
                 ("status", C.c_void_p), ("key_end", C.c_void_p), ("val_end", C.c_void_p), ("rec_cap", C.c_uint64),
                 ("keys", C.c_void_p), ("keys_cap", C.c_uint64), ("vals", C.c_void_p), ("vals_cap", C.c_uint64),
                 ("totals", C.c_void_p)]
+
+
+class PipeStats(C.Structure):
+    _fields_ = [("seconds", C.c_double), ("stage_seconds", C.c_double), ("decode_ms", C.c_double),
+                ("block_bytes", C.c_uint64), ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64),
+                ("chunks", C.c_uint32), ("decompress_errors", C.c_uint32)]
 
 
 class Footer(C.Structure):
@@ -95,5 +105,29 @@ def lib() -> C.CDLL:
         L.mtblx_writer_block_dir.restype = C.c_int
         L.mtblx_writer_free.argtypes = [C.c_void_p]
         L.mtblx_free.argtypes = [C.c_void_p]
+        L.mtblx_snappy_max_compressed_len.argtypes = [C.c_uint64]
+        L.mtblx_snappy_max_compressed_len.restype = C.c_uint64
+        L.mtblx_snappy_uncompressed_len.argtypes = [C.c_void_p, C.c_uint64, u64p]
+        L.mtblx_snappy_uncompressed_len.restype = C.c_int
+        L.mtblx_snappy_decompress.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, u64p]
+        L.mtblx_snappy_decompress.restype = C.c_int
+        L.mtblx_snappy_compress.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, u64p]
+        L.mtblx_snappy_compress.restype = C.c_int
+        L.mtblx_snappy_decompress_blocks.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_uint32]
+        L.mtblx_snappy_decompress_blocks.restype = C.c_uint64
+        L.mtblx_pipe_new.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        L.mtblx_pipe_new.restype = C.c_void_p
+        L.mtblx_pipe_free.argtypes = [C.c_void_p]
+        L.mtblx_pipe_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,
+                                        C.c_uint32, C.POINTER(Decoded), C.POINTER(PipeStats)]
+        L.mtblx_pipe_decode.restype = C.c_int
+        L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]
+        L.mtblx_host_alloc.restype = C.c_int
+        L.mtblx_host_free.argtypes = [C.c_void_p]
+        L.mtblx_host_free.restype = C.c_int
+        L.mtblx_host_register.argtypes = [C.c_void_p, C.c_uint64]
+        L.mtblx_host_register.restype = C.c_int
+        L.mtblx_host_unregister.argtypes = [C.c_void_p]
+        L.mtblx_host_unregister.restype = C.c_int
         _lib = L
     return _lib

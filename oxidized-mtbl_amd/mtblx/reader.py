@@ -115,8 +115,9 @@ class Reader:
             raise MtblError(int(f.err))
         self.meta = list(f.meta)
         self.version = int(f.version)
-        if self.meta[2] != 0:
-            raise NotImplementedError("compressed files: device decompression is a next-round item (DESIGN.md)")
+        self.compression = int(self.meta[2])
+        if self.compression not in (0, 1):
+            raise NotImplementedError("zlib / zstd files are out of scope (DESIGN.md §9); None and Snappy only")
         idx_off = int(self.meta[0])
         if host is None:   # index block bytes to the host (framing + checksum)
             hi = self.len - METADATA_SIZE
@@ -173,11 +174,53 @@ class Reader:
     # ------------------------------------------------------------------ iteration
     def _decode_all(self):
         off, ln, st, bad = self.directory()
-        ml = int(ln.max().item()) if self.nent else 0
-        self._dbatch = codec.DeviceBatch(self.file, off, ln, ml)
+        self.zerr = None
+        if self.compression == 1 and self.nent:
+            # Reader::block decompresses after the checksum (src/reader.rs:166-170): on the
+            # host, as the north star keeps src/compression.rs there; then one device decode
+            buf, uoff, uln, self.zerr = self._snappy_stage(off, ln, st)
+            ml = int(uln.max()) if uln.size else 0
+            self._dbatch = codec.DeviceBatch.from_host(buf, uoff, uln, device=self.file.device)
+        else:
+            ml = int(ln.max().item()) if self.nent else 0
+            self._dbatch = codec.DeviceBatch(self.file, off, ln, ml)
         self.data = codec.decode_blocks(self._dbatch) if self.nent else None
         torch.cuda.synchronize()
         return off, ln, st, bad
+
+    def _snappy_stage(self, off, ln, st):
+        L = _lib.lib()
+        host = self.file.cpu().numpy()
+        o = off.cpu().numpy().view(np.uint64).copy()
+        n = ln.cpu().numpy().view(np.uint32).copy()
+        ok = st.cpu().numpy() == _lib.DIR_OK
+        n[~ok] = 0
+        o[~ok] = 0
+        ulen = np.zeros(o.size, np.uint64)
+        zerr = np.zeros(o.size, np.int32)
+        for i in np.nonzero(ok)[0]:
+            u = C.c_uint64(0)
+            if L.mtblx_snappy_uncompressed_len(host.ctypes.data + int(o[i]), int(n[i]), C.byref(u)) != 0 or \
+                    u.value > 0xFFFFFFFF:
+                zerr[i] = _lib.SNAPPY_CORRUPT
+            else:
+                ulen[i] = u.value
+        uoff = np.zeros(o.size, np.uint64)
+        if o.size > 1:
+            uoff[1:] = np.cumsum(ulen[:-1], dtype=np.uint64)
+        total = int(ulen.sum(dtype=np.uint64))
+        buf = np.zeros(max(total, 1), np.uint8)
+        zst = np.zeros(o.size, np.int32)
+        todo = np.nonzero(ok & (zerr == 0))[0]
+        if todo.size:
+            sel = lambda a: np.ascontiguousarray(a[todo])  # noqa: E731
+            so, sn, su, sl = sel(o), sel(n), sel(uoff), sel(ulen)
+            L.mtblx_snappy_decompress_blocks(host.ctypes.data, so.ctypes.data, sn.ctypes.data, buf.ctypes.data,
+                                             su.ctypes.data, sl.ctypes.data, zst.ctypes.data, todo.size, 16)
+            zerr[todo] = zst[: todo.size]
+        uln = ulen.astype(np.uint32)
+        uln[zerr != 0] = 0
+        return buf, uoff, uln, zerr
 
     def iter(self) -> Scan:
         """ReaderIntoIter (mode Iter) to the end: the records yielded and how it ends."""
@@ -201,6 +244,9 @@ class Reader:
             # Reader::block for entry i
             if dst[i] != _lib.DIR_OK or cbad[i]:
                 end = END_PANIC if dst[i] != _lib.DIR_UNSUPPORTED else END_PANIC
+                break
+            if self.zerr is not None and self.zerr[i]:   # decompress -> Err(Error::Io) (src/reader.rs:166)
+                end, err = (END_ERR_OPEN if i == 0 else END_ERR_NEXT), "Io"
                 break
             s = int(bst[i])
             if s == _lib.ST_INVALID_BLOCK:
@@ -259,6 +305,8 @@ class Reader:
         """Reader::get for every key at once on the device (mtblx_get, f2).
         -> (status int32 [nq] (GET_*), val_off int64 [nq], val_len int64 [nq]) device tensors;
         the value of a FOUND query q is file[val_off[q] : val_off[q] + val_len[q]]."""
+        if self.compression != 0:
+            raise NotImplementedError("mtblx_get reads raw blocks; compressed files use get()")
         dev = self.file.device
         ks = [bytes(k) for k in keys]
         nq = len(ks)
@@ -281,6 +329,11 @@ class Reader:
     def get(self, key: bytes):
         """Reader::get (src/reader.rs:111-122): the value of `key`, or None; raises where the
         reference panics / returns Err."""
+        if self.compression != 0:   # values live in decompressed blocks: search the decoded records
+            recs = self._sorted_keys()[1]
+            import bisect
+            i = bisect.bisect_left([k for k, _ in recs], bytes(key))
+            return recs[i][1] if i < len(recs) and recs[i][0] == bytes(key) else None
         st, vo, vl = self.get_batch([key])
         s = int(st[0].item())
         if s == _lib.GET_FOUND:

@@ -66,8 +66,8 @@ class Writer:
         L = _lib.lib()
         self._w = L.mtblx_writer_new(int(block_size), int(restart_interval), int(compression))
         if not self._w:
-            raise NotImplementedError("compressed writing is not implemented in this round (CompressionType.None_ "
-                                      "only)")
+            raise NotImplementedError("CompressionType.None_ and CompressionType.Snappy only (zlib / zstd are out "
+                                      "of scope, DESIGN.md §9)")
         self.block_dir = None
 
     @staticmethod

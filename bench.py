@@ -73,6 +73,149 @@ def cpu_baseline(data, off, ln, budget_s: float):
     }
 
 
+def pcie_ceiling(nbytes: int = 400 << 20):
+    """pinned hipMemcpyAsync rates on this box: H2D alone, D2H alone, both at once (GB/s)"""
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    d.copy_(h, non_blocking=True)
+    h2.copy_(d2, non_blocking=True)
+    torch.cuda.synchronize()
+
+    def timed(f, reps=4):
+        t = time.perf_counter()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        return reps * nbytes / (time.perf_counter() - t) / 1e9
+
+    def both():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+    r = {"h2d_GBs": round(timed(lambda: d.copy_(h, non_blocking=True)), 2),
+         "d2h_GBs": round(timed(lambda: h2.copy_(d2, non_blocking=True)), 2),
+         "bidir_GBs_each": round(timed(both), 2)}
+    del h, h2, d, d2
+    return r
+
+
+def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
+    """North-star end-to-end rate: the .mtbl file in (pinned) host memory in, the caller's host
+    byte slices out (mtblx_pipe_decode: H2D, decode, D2H on separate streams, 3 chunks in
+    flight).  cfg2 as stored (CompressionType::None) and cfg5 = the same records written with
+    CompressionType::Snappy (host decompression inside the pipeline, src/compression.rs:116-119).
+    Never `value`: reported beside it."""
+    from mtblx import codec, pipe, synth
+    from mtblx.writer import Writer
+    res = {}
+    block_bytes = int(ln.sum(dtype=np.uint64))
+    res["pcie_ceiling"] = pcie_ceiling()
+    pc = res["pcie_ceiling"]
+    out = pipe.HostOutputs(off.size, nrec, kbytes, vbytes)
+    p = pipe.HostPipe(chunk_bytes=64 << 20, max_blocks=1 << 16, threads=16)
+
+    def run(d, o, l, comp, tag, extra=None):
+        p.decode(d, o, l, out, compression=comp)    # warm-up (first-touch of pinned pages, slots)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        st = None
+        h2d = d2h = stage = dec = 0.0
+        for _ in range(reps):
+            st = p.decode(d, o, l, out, compression=comp)
+            h2d += st.h2d_bytes
+            d2h += st.d2h_bytes
+            stage += st.stage_seconds
+            dec += st.decode_ms
+        el = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        world = dist.get_world_size() if dist is not None else 1
+        tot = out.totals
+        if int(tot[0]) != nrec or int(tot[1]) != kbytes or int(tot[2]) != vbytes or int(tot[3]) != 0 or \
+                not (out.status[: off.size] == 0).all():
+            raise RuntimeError(f"end-to-end decode ({tag}) failed: totals={list(tot)}")
+        r = {"GiB_per_s": round(block_bytes * reps * world / el / 2**30, 2),
+             "records_per_s": round(nrec * reps * world / el, 1),
+             "ms_per_pass": round(el * 1e3 / reps, 3), "passes": reps,
+             "h2d_GB_per_pass": round(h2d / reps / 1e9, 4), "d2h_GB_per_pass": round(d2h / reps / 1e9, 4),
+             "pcie_GBs_h2d": round(h2d / el / 1e9, 2), "pcie_GBs_d2h": round(d2h / el / 1e9, 2),
+             "host_stage_ms_per_pass": round(stage * 1e3 / reps, 3),
+             "decode_ms_per_pass": round(dec / reps, 3), "chunks": int(st.chunks)}
+        # PCIe bound of one pass: both directions at once share the link (measured ceilings)
+        bound = max(h2d / reps / (pc["h2d_GBs"] * 1e9), d2h / reps / (pc["d2h_GBs"] * 1e9),
+                    (h2d + d2h) / reps / (2 * pc["bidir_GBs_each"] * 1e9))
+        r["pcie_bound_ms_per_pass"] = round(bound * 1e3, 3)
+        r["frac_of_pcie_bound"] = round(bound / (el / reps), 3)
+        if extra:
+            r.update(extra)
+        return r
+
+    pipe.register(data)
+    try:
+        res["cfg2_none"] = run(data, off, ln, 0, "cfg2")
+    finally:
+        pipe.unregister(data)
+    # cfg5: the cfg2 records written with CompressionType::Snappy (same blocks once decompressed)
+    nr_file = int(synth.cfg2_file.last_block_nrec.sum(dtype=np.uint64))
+    keys, vals, kl, vl = synth.cfg2_arrays(int(off.size * ((4096 - 64) // 79) * 1.02) + 64)
+    w = Writer(4096, 16, 1)
+    n_in = nr_file
+    w.insert_batch(keys[: n_in * kl], np.arange(1, n_in + 1, dtype=np.uint64) * np.uint64(kl), vals[: n_in * vl],
+                   np.arange(1, n_in + 1, dtype=np.uint64) * np.uint64(vl))
+    zdata = w.into_inner_np()
+    zoff, zln = w.block_dir
+    zoff, zln = zoff[: off.size].copy(), zln[: off.size].copy()
+    # host decompression alone (16 threads), then the device-resident decode of its output
+    L = pipe._lib.lib()
+    ulen = ln.astype(np.uint64)
+    uoff = np.zeros(off.size, np.uint64)
+    uoff[1:] = np.cumsum(ulen[:-1], dtype=np.uint64)
+    ubuf = np.zeros(int(ulen.sum()), np.uint8)
+    zst = np.zeros(off.size, np.int32)
+    t0 = time.perf_counter()
+    bad = L.mtblx_snappy_decompress_blocks(zdata.ctypes.data, zoff.ctypes.data, zln.ctypes.data, ubuf.ctypes.data,
+                                           uoff.ctypes.data, ulen.ctypes.data, zst.ctypes.data, off.size, 16)
+    t_dz = time.perf_counter() - t0
+    if bad:
+        raise RuntimeError("cfg5: host snappy decompression failed")
+    batch = codec.DeviceBatch.from_host(ubuf, uoff, ulen.astype(np.uint32))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ws = codec.Workspace(batch.nblk)
+        dout = codec.DecodedBlocks(batch.nblk, nrec, kbytes, vbytes)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        codec.decode_into(batch, dout, ws, s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(20):
+        codec.decode_into(batch, dout, ws, s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    dev_ms = e0.elapsed_time(e1) / 20
+    if dout.totals_host()[:3] != (nrec, kbytes, vbytes):
+        raise RuntimeError("cfg5: device-resident decode of the decompressed blocks failed")
+    pipe.register(zdata)
+    try:
+        res["cfg5_snappy"] = run(zdata, zoff, zln, 1, "cfg5", {
+            "stored_bytes": int(zln.sum(dtype=np.uint64)),
+            "host_decompress_GiB_per_s_16_threads": round(block_bytes / t_dz / 2**30, 2),
+            "device_resident_GiB_per_s": round(block_bytes / (dev_ms * 1e-3) / 2**30, 1)})
+    finally:
+        pipe.unregister(zdata)
+    res["note"] = ("pinned host file in -> pinned host outputs (keys, values, u32 end offsets, per-block arrays) out; "
+                   "PCIe Gen5 x16 (63 GB/s per direction, spec) bounds it; cfg2/cfg5 data are random bytes, so "
+                   "snappy stores them nearly uncompressed")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +228,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the stream-copy ceiling measurement")
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32C verify measurement")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host in, host out) measurement")
+    ap.add_argument("--e2e-passes", type=int, default=5)
     ap.add_argument("--lib", default=None, help="diagnostic: alternative libmtblx build (ablations)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load libmtblx_stamps.so and report per-phase cycles per tile (not a measurement)")
@@ -256,6 +401,10 @@ def main():
     }
     if crc_info is not None:
         res["crc32c_verify"] = crc_info
+    if not args.no_e2e and args.block_size == 4096 and not args.lib and not args.stamps:
+        del out, ws
+        torch.cuda.empty_cache()
+        res["end_to_end"] = end_to_end(data, off, ln, int(nrec), int(kbytes), int(vbytes), args.e2e_passes, dist)
     if args.stamps:
         d = ws.buf[:128].cpu().numpy().view(np.uint64).astype(np.float64)
         names = ["copy:wait-ready", "w1:lookback+barrier", "w0:walk-loop", "w0:scan-publish",

@@ -157,6 +157,46 @@ int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int veri
               uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
               uint64_t* val_off, uint64_t* val_len, void* stream);
 
+/* ---- encode side on the device: Writer's block cut + BlockBuilder + write_block framing ----
+ * Records (device): key r = keys[r ? key_end[r-1] : 0 .. key_end[r]), value likewise (u64 END
+ * offsets from record 0), in Writer::insert order (strictly increasing keys). */
+typedef struct mtblx_records {
+  const uint8_t* keys;
+  const uint64_t* key_end;
+  const uint8_t* vals;
+  const uint64_t* val_end;
+  uint64_t n;
+} mtblx_records;
+
+/* Writer::insert's flush rule (src/writer.rs:125-130 with BlockBuilder::current_size_estimate,
+ * src/block_builder.rs:40-47): where the Writer would cut blocks.  Each shard s = records
+ * [shard_rec[s], shard_rec[s+1]) (device) is an independent Writer (one file each; one shard
+ * = one file); blocks of all shards are numbered consecutively: block b = records
+ * [blk_rec[b], blk_rec[b+1]) (device, capacity blk_cap >= nblk + 1; blk_rec may be NULL to
+ * count only).  block_size is clamped to >= 1024 like WriterBuilder::block_size.
+ * Synchronous; *nblk_out = number of blocks.  Returns MTBLX_E_FORMAT where the Writer
+ * panics; *flags_out tells why: */
+#define MTBLX_PLAN_OUT_OF_ORDER 1u /* a key <= its predecessor: panic!("out-of-order key") (:119-123) */
+#define MTBLX_PLAN_PANIC 2u        /* restart_interval 0 and a second entry: assert (src/block_builder.rs:50) */
+#define MTBLX_PLAN_TOO_LONG 4u     /* a key or value >= 4 GiB (u32 varint lengths)                    */
+int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
+                      uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
+                      uint32_t* flags_out, void* stream);
+
+/* BlockBuilder::add for every record of a block, then finish (src/block_builder.rs:49-104),
+ * for every block b of blk_rec at once.  framed != 0 adds write_block's framing before each
+ * content (varint64 len | crc32c | content, src/writer.rs:203-237, CompressionType::None):
+ * the blocks then sit back to back from out[0], byte-identical to the data-block region of
+ * the file Writer produces.  blk_off[b]/blk_len[b] = content window in `out` (the decode
+ * batch directory); status[b] = MTBLX_ST_OK, _CORRUPT (BlockBuilder assert), _UNSUPPORTED
+ * (>= 4 GiB), _OVERFLOW (out_cap); totals (device [2]) = bytes written, flags (bit 0: a
+ * block not OK, bit 1: look-back timeout).  Asynchronous on `stream`; the workspace
+ * (mtblx_encode_workspace_bytes) is cleared by the call. */
+size_t mtblx_encode_workspace_bytes(uint32_t nblk);
+int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk_rec, uint32_t nblk, uint32_t restart_interval,
+                        int framed, uint8_t* out, uint64_t out_cap, uint64_t* blk_off, uint32_t* blk_len,
+                        int32_t* status, uint64_t* totals, void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- end-to-end decode from host memory (the PCIe-inclusive path of the north star) ----
  * An mtbl file in host memory in (mmap'd or read), the caller's host byte slices out:
  * for every data block, Reader::block's decompression (src/reader.rs:166-170, host: the

@@ -1,0 +1,566 @@
+// encode.hip — MI355X (gfx950) encode side of the block codec (BASELINE cfg3 round trip).
+//
+//   Writer::insert flush rule  /root/reference/src/writer.rs:125-130   -> k_plan (block cut)
+//   BlockBuilder::current_size_estimate   src/block_builder.rs:40-47
+//   BlockBuilder::add / finish            src/block_builder.rs:49-104  -> k_encode
+//   write_block framing + crc32c          src/writer.rs:203-237        -> k_encode (framed)
+//   varint_encode32 / varint_encode64     src/varint.rs:12-42, :63-76
+//   Writer::insert order check            src/writer.rs:119-123        -> k_plan flags
+//
+// k_plan: one wave per shard (an independent Writer over a contiguous record range); the
+// flush rule is a serial chain over records, so the wave advances 64 records per step:
+// every lane sizes its record at the position it would take in the current block, DPP/shfl
+// scans give the size estimate before each record, a ballot finds the first record that
+// flushes, and the wave restarts from it (a new block).  Two passes: count, then write.
+// k_encode: one workgroup per block, in ticket order.  Phase A sums the entry sizes (the
+// block length is known before a byte is written) and publishes the framed size for a
+// decoupled look-back across blocks; phase B assembles the block in LDS (entries, restart
+// array, count); then the look-back resolves the block's file offset, the CRC-32C of the
+// content is computed from LDS and the block streams out with 16-byte stores.  Blocks larger
+// than the LDS buffer are assembled in place in HBM after the look-back.
+// All integer/byte work (HBM bound, no MFMA).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "crc_dev.h"
+#include "mtblx.h"
+
+namespace mtblx_enc {
+
+constexpr int kWave = 64;
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr uint32_t kLdsBlock = 65536 + 1024;   // contents up to this many bytes are assembled in LDS
+constexpr uint64_t kIncl = 1ull << 63, kAgg = 1ull << 62, kVal = kAgg - 1;
+
+typedef uint64_t __attribute__((aligned(1))) u64u;
+typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t v4a __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t vlen32(uint64_t v) {
+  return v < (1ull << 7) ? 1u : v < (1ull << 14) ? 2u : v < (1ull << 21) ? 3u : v < (1ull << 28) ? 4u : 5u;
+}
+__device__ __forceinline__ uint32_t vlen64(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 128) { v >>= 7; ++n; }
+  return n;
+}
+// varint_encode32 / varint_encode64 (src/varint.rs:12-42, :63-76): LEB128
+__device__ __forceinline__ uint32_t venc(uint8_t* p, uint64_t v) {
+  uint32_t i = 0;
+  while (v >= 128) { p[i++] = (uint8_t)(v | 128); v >>= 7; }
+  p[i++] = (uint8_t)v;
+  return i;
+}
+
+struct Recs {
+  const uint8_t* keys;
+  const uint64_t* key_end;
+  const uint8_t* vals;
+  const uint64_t* val_end;
+};
+
+__device__ __forceinline__ void rec_of(const Recs& R, uint64_t r, uint64_t& k0, uint64_t& kl, uint64_t& v0,
+                                       uint64_t& vl) {
+  k0 = r ? R.key_end[r - 1] : 0;
+  kl = R.key_end[r] - k0;
+  v0 = r ? R.val_end[r - 1] : 0;
+  vl = R.val_end[r] - v0;
+}
+
+// common prefix length of a[0..al) and b[0..bl); cmp = sign of a <=> b (lexicographic, Ord for [u8])
+__device__ uint64_t lcp_cmp(const uint8_t* a, uint64_t al, const uint8_t* b, uint64_t bl, int& cmp) {
+  const uint64_t m = al < bl ? al : bl;
+  uint64_t i = 0;
+  while (i + 8 <= m) {
+    const uint64_t x = *reinterpret_cast<const u64u*>(a + i), y = *reinterpret_cast<const u64u*>(b + i);
+    if (x != y) {
+      i += (uint64_t)(__builtin_ctzll(x ^ y) >> 3);
+      cmp = a[i] < b[i] ? -1 : 1;
+      return i;
+    }
+    i += 8;
+  }
+  while (i < m && a[i] == b[i]) ++i;
+  cmp = (i < m) ? (a[i] < b[i] ? -1 : 1) : (al < bl ? -1 : (al > bl ? 1 : 0));
+  return i;
+}
+
+// restart bookkeeping of BlockBuilder::add (src/block_builder.rs:50-62) for entry p of a block:
+// counter < interval -> shared = LCP(last_key, key) (0 for the first entry: last_key is
+// empty); else push a restart and shared = 0.  With interval == 0 the first add pushes a
+// restart and the second add fails `assert!(counter <= interval)`.
+__device__ __forceinline__ bool pushes_restart(uint64_t p, uint32_t iv) {
+  return iv == 0 ? p == 0 : (p > 0 && p % iv == 0);
+}
+__device__ __forceinline__ bool shares(uint64_t p, uint32_t iv) { return p > 0 && !pushes_restart(p, iv); }
+
+__device__ __forceinline__ uint64_t entry_bytes(uint64_t sh, uint64_t kl, uint64_t vl) {
+  return vlen32(sh) + vlen32(kl - sh) + vlen32(vl) + (kl - sh) + vl;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T x, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const T y = __shfl_up(x, d, kWave);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// ---------------------------------------------------------------------------------
+// k_plan: Writer::insert's flush rule per shard
+// ---------------------------------------------------------------------------------
+struct PlanArgs {
+  Recs R;
+  const uint64_t* shard_rec;   // [nshard + 1]
+  uint32_t nshard;
+  uint32_t interval;
+  uint64_t block_size;
+  uint64_t* shard_nblk;        // pass 0 output
+  const uint64_t* shard_blk0;  // pass 1 input
+  uint64_t* blk_rec;           // pass 1 output
+  uint32_t* flags;             // MTBLX_PLAN_*
+  int write;
+};
+
+__global__ void __launch_bounds__(kWave) k_plan(PlanArgs a) {
+  const uint32_t s = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (s >= a.nshard) return;
+  const uint64_t rb = a.shard_rec[s], re = a.shard_rec[s + 1];
+  const uint64_t out0 = a.write ? a.shard_blk0[s] : 0;
+  uint64_t nb = 0, bstart = rb, buf = 0, nrest = 1, r0 = rb;
+  uint32_t fl = 0;
+  if (rb < re) {
+    nb = 1;
+    if (a.write && lane == 0) a.blk_rec[out0] = rb;
+  }
+  while (r0 < re) {
+    const uint64_t r = r0 + (uint64_t)lane;
+    const bool v = r < re;
+    uint64_t k0 = 0, kl = 0, v0 = 0, vl = 0, sz = 0, push = 0;
+    if (v) {
+      rec_of(a.R, r, k0, kl, v0, vl);
+      if (kl > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) fl |= MTBLX_PLAN_TOO_LONG;
+      const uint64_t p = r - bstart;
+      uint64_t sh = 0;
+      if (r > rb) {   // Writer::insert: key must be > the previous key (src/writer.rs:119-123)
+        uint64_t pk0, pkl, pv0, pvl;
+        rec_of(a.R, r - 1, pk0, pkl, pv0, pvl);
+        int c = 0;
+        const uint64_t l = lcp_cmp(a.R.keys + pk0, pkl, a.R.keys + k0, kl, c);
+        if (c >= 0) fl |= MTBLX_PLAN_OUT_OF_ORDER;
+        if (shares(p, a.interval)) sh = l;
+      }
+      if (a.interval == 0 && p > 0) fl |= MTBLX_PLAN_PANIC;
+      push = pushes_restart(p, a.interval) ? 1 : 0;
+      sz = entry_bytes(sh, kl, vl);
+    }
+    const uint64_t isz = wave_incl_scan<uint64_t>(sz, lane);
+    const uint64_t ipu = wave_incl_scan<uint64_t>(push, lane);
+    // current_size_estimate before record r (src/block_builder.rs:40-47) + 15 + |k| + |v|
+    const uint64_t bb = buf + isz - sz, nr = nrest + ipu - push;
+    const uint64_t est = bb + nr * (bb > 0xFFFFFFFFull ? 8u : 4u) + 4u;
+    const bool flush = v && r > bstart && est + 15 + kl + vl >= a.block_size;
+    const uint64_t fm = __ballot(flush);
+    if (fm) {
+      const int f = __builtin_ctzll(fm);
+      bstart = r0 + (uint64_t)f;
+      r0 = bstart;
+      buf = 0;
+      nrest = 1;
+      if (a.write && lane == 0) a.blk_rec[out0 + nb] = bstart;
+      ++nb;
+    } else {
+      const int last = (int)(re - r0 < (uint64_t)kWave ? re - r0 : (uint64_t)kWave) - 1;
+      buf += __shfl(isz, last, kWave);
+      nrest += __shfl(ipu, last, kWave);
+      r0 += kWave;
+    }
+  }
+  // wave-uniform: OR of the lanes' flags
+  uint32_t f = fl;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) f |= (uint32_t)__shfl_xor((int)f, d, kWave);
+  if (lane == 0) {
+    if (!a.write) a.shard_nblk[s] = nb;
+    if (f) atomicOr(a.flags, f);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// k_encode: BlockBuilder per block + Writer framing, decoupled look-back for offsets
+// ---------------------------------------------------------------------------------
+struct X8Tab {
+  uint32_t p[64];   // x^(8 t) mod P, t < 64 (reflected, x^0 = bit 31)
+  constexpr X8Tab() : p() {
+    uint32_t x = 0x80000000u;
+    for (int t = 0; t < 64; ++t) {
+      p[t] = x;
+      for (int k = 0; k < 8; ++k) x = (x & 1u) ? (x >> 1) ^ mtblx_crc::kPoly : x >> 1;
+    }
+  }
+};
+static __constant__ X8Tab kX8 = X8Tab();
+
+struct EncArgs {
+  Recs R;
+  const uint64_t* blk_rec;   // [nblk + 1]
+  uint32_t nblk;
+  uint32_t interval;
+  int framed;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* blk_off;
+  uint32_t* blk_len;
+  int32_t* status;
+  uint64_t* totals;          // [2]: bytes written, flags
+  uint32_t* ticket;
+  uint64_t* lbw;             // [nblk] look-back words
+};
+
+struct alignas(16) EncLds {
+  uint8_t ob[kLdsBlock];
+  uint32_t T[256];
+  uint64_t red[kWaves];
+  uint32_t redf[kWaves];
+  uint64_t sh_u64[4];
+  uint32_t sh_u32[4];
+};
+
+// block-wide exclusive scan of a u64 (all threads); returns the exclusive prefix, total in `tot`
+__device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t& tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl_scan<uint64_t>(x, lane);
+  if (lane == kWave - 1) S.red[w] = inc;
+  __syncthreads();
+  uint64_t before = 0;
+  tot = 0;
+#pragma unroll
+  for (int k = 0; k < kWaves; ++k) {
+    const uint64_t v = S.red[k];
+    if (k < w) before += v;
+    tot += v;
+  }
+  __syncthreads();
+  return before + inc - x;
+}
+
+// copy n bytes from global src to dst (LDS or global, generic pointer)
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  uint64_t o = 0;
+  for (; o + 16 <= n; o += 16) {
+    const v4u w = *reinterpret_cast<const v4u*>(src + o);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[o + k] = (uint8_t)(ws[k >> 2] >> (8 * (k & 3)));
+  }
+  for (; o < n; ++o) dst[o] = src[o];
+}
+
+__device__ __forceinline__ void put32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+
+// CRC-32C of d[0..L) by the workgroup (crate crc32c 0.4).  64-byte chunks counted from the
+// START (16-byte aligned for the LDS buffer); chunk j's raw CRC is shifted by the bytes after
+// it: x^(512 (nfull-1-j)) * x^(8 tail).  The 0xFFFFFFFF init is folded into the first 4 bytes.
+__device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t acc = 0;
+  if (L >= 4) {
+    const uint64_t nfull = L / 64, tail = L - 64 * nfull;
+    for (uint64_t j = tid; j <= nfull; j += kThreads) {
+      const uint64_t lo = 64 * j;
+      const uint32_t n = j < nfull ? 64u : (uint32_t)tail;
+      if (n == 0) continue;
+      uint32_t c = 0;
+      if (n == 64) {
+        uint32_t wd[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
+          wd[4 * q] = x.x; wd[4 * q + 1] = x.y; wd[4 * q + 2] = x.z; wd[4 * q + 3] = x.w;
+        }
+        if (lo == 0) wd[0] ^= 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+          const uint32_t byte = (wd[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          c = S.T[(c ^ byte) & 0xFFu] ^ (c >> 8);
+        }
+        c = mtblx_crc::dmultmodp(mtblx_crc::xpow512(nfull - 1 - j), c);
+        if (tail) c = mtblx_crc::dmultmodp(kX8.p[tail], c);
+      } else {   // the tail chunk (< 64 bytes, byte loads: never past the content)
+        for (uint32_t k = 0; k < n; ++k) {
+          uint32_t byte = d[lo + k];
+          if (lo + k < 4) byte ^= 0xFFu;
+          c = S.T[(c ^ byte) & 0xFFu] ^ (c >> 8);
+        }
+      }
+      acc ^= c;
+    }
+  } else if (tid == 0) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = 0; i < L; ++i) c = S.T[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+    acc = c ^ 0xFFFFFFFFu ^ 0xFFFFFFFFu;   // complemented again below
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, s, kWave);
+  if (lane == 0) S.redf[w] = acc;
+  __syncthreads();
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < kWaves; ++k) r ^= S.redf[k];
+  __syncthreads();
+  return r ^ 0xFFFFFFFFu;
+}
+
+// entry i of the block starting at record r0: fields and encoded size
+struct Ent {
+  uint64_t k0, kl, v0, vl, sh;
+};
+__device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, uint32_t iv) {
+  Ent e;
+  rec_of(R, r0 + i, e.k0, e.kl, e.v0, e.vl);
+  e.sh = 0;
+  if (shares(i, iv)) {
+    uint64_t pk0, pkl, pv0, pvl;
+    rec_of(R, r0 + i - 1, pk0, pkl, pv0, pvl);
+    int c;
+    e.sh = lcp_cmp(R.keys + pk0, pkl, R.keys + e.k0, e.kl, c);
+  }
+  return e;
+}
+
+// write entry e at dst (header varints, key suffix, value): src/block_builder.rs:69-77
+__device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent& e) {
+  uint8_t h[15];
+  uint32_t n = venc(h, e.sh);
+  n += venc(h + n, e.kl - e.sh);
+  n += venc(h + n, e.vl);
+  for (uint32_t k = 0; k < n; ++k) dst[k] = h[k];
+  copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh);
+  copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl);
+}
+
+__device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
+  uint64_t excl = 0;
+  int64_t j = (int64_t)b - 1;
+  while (j >= 0) {
+    const int64_t idx = j - lane;
+    uint64_t w = idx >= 0 ? __hip_atomic_load(a.lbw + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kIncl;
+    uint32_t spins = 0;
+    while (__ballot(!(w & (kIncl | kAgg))) != 0ull) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!(w & (kIncl | kAgg))) w = __hip_atomic_load(a.lbw + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > (1u << 22)) { timeout = true; w |= kIncl; }
+    }
+    const uint64_t im = __ballot((w & kIncl) != 0ull);
+    const int first = im ? __builtin_ctzll(im) : kWave;
+    uint64_t v = (lane <= first) ? (w & kVal) : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+    excl += v;
+    if (im) break;
+    j -= kWave;
+  }
+  return excl;
+}
+
+__global__ void __launch_bounds__(kThreads, 2) k_encode(EncArgs a) {
+  __shared__ EncLds S;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < 256; i += kThreads) S.T[i] = mtblx_crc::kTab.byte[i];
+  if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  const uint32_t b = S.sh_u32[0];
+  if (b >= a.nblk) return;
+  const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
+  const uint32_t iv = a.interval;
+
+  // ---- phase A: the content length (entries + restart array + count) ----
+  uint64_t part = 0;
+  for (uint64_t i = tid; i < n; i += kThreads) {
+    const Ent e = entry_of(a.R, r0, i, iv);
+    part += entry_bytes(e.sh, e.kl, e.vl);
+  }
+  uint64_t entries = 0;
+  (void)wg_excl_scan(S, part, entries);
+  // restarts: [0] + one push per restart entry (src/block_builder.rs:21, :60)
+  const uint64_t nrest = n == 0 ? 1 : (iv == 0 ? 2 : 1 + (n - 1) / iv);
+  int32_t st = MTBLX_ST_OK;
+  if (iv == 0 && n > 1) st = MTBLX_ST_CORRUPT;            // assert!(counter <= interval) (:50)
+  if (entries > 0xFFFFFFFFull) st = MTBLX_ST_UNSUPPORTED;  // u64 restart arrays: blocks >= 4 GiB
+  const uint64_t L = entries + 4 * nrest + 4;
+  const uint64_t F = a.framed ? vlen64(L) + 4 + L : L;
+  if (tid == 0) {   // publish this block's framed size as early as possible
+    __hip_atomic_store(a.lbw + b, (b == 0 ? kIncl : kAgg) | F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const bool in_lds = L <= kLdsBlock && st == MTBLX_ST_OK;
+
+  // ---- phase B (LDS path): assemble the block ----
+  const uint64_t R = entries;   // restart array offset
+  auto assemble = [&](uint8_t* dst) {
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < n; base += kThreads) {
+      const uint64_t i = base + tid;
+      Ent e{};
+      uint64_t sz = 0;
+      if (i < n) {
+        e = entry_of(a.R, r0, i, iv);
+        sz = entry_bytes(e.sh, e.kl, e.vl);
+      }
+      uint64_t tot = 0;
+      const uint64_t eo = carry + wg_excl_scan(S, sz, tot);
+      if (i < n) {
+        put_entry(dst + eo, a.R, e);
+        if (iv > 0 && i % iv == 0) put32(dst + R + 4 * (i / iv), (uint32_t)eo);
+      }
+      carry += tot;
+    }
+    if (tid == 0) {
+      if (n == 0 || iv == 0) put32(dst + R, 0u);      // restarts[0] = 0 (entry 0 writes it otherwise)
+      if (iv == 0 && n > 0) put32(dst + R + 4, 0u);   // the push of entry 0 (buf.len() == 0)
+      put32(dst + L - 4, (uint32_t)nrest);            // restart count
+    }
+  };
+  if (in_lds) assemble(S.ob);
+
+  // ---- look-back: this block's offset in the output ----
+  if (w == 0) {
+    bool to = false;
+    const uint64_t excl = b == 0 ? 0 : lookback(a, b, lane, to);
+    if (lane == 0) {
+      if (b != 0) __hip_atomic_store(a.lbw + b, kIncl | (excl + F), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      S.sh_u64[0] = excl;
+      if (to) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 1), 2ull);
+    }
+  }
+  __syncthreads();
+  const uint64_t pre = S.sh_u64[0];
+  const uint64_t coff = pre + (a.framed ? vlen64(L) + 4 : 0);
+  if (st == MTBLX_ST_OK && pre + F > a.out_cap) st = MTBLX_ST_OVERFLOW;
+  if (st == MTBLX_ST_OK) {
+    uint8_t* dst = a.out + coff;
+    const uint8_t* src = S.ob;
+    if (!in_lds) {   // large block: assemble in place in HBM
+      assemble(dst);
+      __threadfence_block();
+      __syncthreads();
+      src = dst;
+    }
+    if (a.framed) {
+      const uint32_t crc = wg_crc32c(S, src, L);
+      if (tid == 0) {
+        uint8_t h[10];
+        const uint32_t hl = venc(h, L);
+        for (uint32_t k = 0; k < hl; ++k) a.out[pre + k] = h[k];
+        put32(a.out + pre + hl, crc);
+      }
+    }
+    if (in_lds) {   // stream the block out: aligned 16 B LDS reads, unaligned 16 B stores
+      const uint64_t nch = L / 16;
+      for (uint64_t c = tid; c < nch; c += kThreads) {
+        const v4a x = *reinterpret_cast<const v4a*>(S.ob + 16 * c);
+        *reinterpret_cast<v4u*>(dst + 16 * c) = v4u{x.x, x.y, x.z, x.w};
+      }
+      for (uint64_t o = 16 * nch + tid; o < L; o += kThreads) dst[o] = S.ob[o];
+    }
+  }
+  if (tid == 0) {
+    a.blk_off[b] = st == MTBLX_ST_OK ? coff : 0;
+    a.blk_len[b] = st == MTBLX_ST_OK ? (uint32_t)L : 0u;
+    a.status[b] = st;
+    if (st != MTBLX_ST_OK) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 1), 1ull);
+    if (b == a.nblk - 1) a.totals[0] = pre + F;
+  }
+}
+
+}  // namespace mtblx_enc
+
+using namespace mtblx_enc;
+
+extern "C" size_t mtblx_encode_workspace_bytes(uint32_t nblk) { return 256u + 8ull * (uint64_t)nblk; }
+
+extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
+                                 uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
+                                 uint64_t* nblk_out, uint32_t* flags_out, void* stream) {
+  if (!rec || !shard_rec || !nblk_out || nshard == 0) return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (block_size < 1024) block_size = 1024;   // WriterBuilder::block_size clamp (src/writer.rs:43-46)
+  uint64_t* d = nullptr;   // [nshard] counts | [nshard] firsts | flags
+  if (hipMalloc(reinterpret_cast<void**>(&d), 16ull * nshard + 16) != hipSuccess) return MTBLX_E_HIP;
+  uint32_t* dflags = reinterpret_cast<uint32_t*>(d + 2 * nshard);
+  int rc = MTBLX_OK;
+  std::vector<uint64_t> cnt(nshard), first(nshard);
+  uint32_t fl = 0;
+  PlanArgs a{{rec->keys, rec->key_end, rec->vals, rec->val_end}, shard_rec, nshard, restart_interval, block_size,
+             d, d + nshard, blk_rec, dflags, 0};
+  if (hipMemsetAsync(dflags, 0, 16, s) != hipSuccess) rc = MTBLX_E_HIP;
+  if (rc == MTBLX_OK) {
+    hipLaunchKernelGGL(k_plan, dim3(nshard), dim3(kWave), 0, s, a);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(cnt.data(), d, 8ull * nshard, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&fl, dflags, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      rc = MTBLX_E_HIP;
+  }
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nshard; ++i) {
+    first[i] = total;
+    total += cnt[i];
+  }
+  *nblk_out = total;
+  if (flags_out) *flags_out = fl;
+  if (rc == MTBLX_OK && blk_rec && total + 1 <= blk_cap) {
+    a.write = 1;
+    if (hipMemcpyAsync(d + nshard, first.data(), 8ull * nshard, hipMemcpyHostToDevice, s) != hipSuccess) rc = MTBLX_E_HIP;
+    if (rc == MTBLX_OK) {
+      hipLaunchKernelGGL(k_plan, dim3(nshard), dim3(kWave), 0, s, a);
+      // blk_rec[total] = the end of the last shard
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(blk_rec + total, shard_rec + nshard, 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        rc = MTBLX_E_HIP;
+    }
+  } else if (rc == MTBLX_OK && blk_rec) {
+    rc = MTBLX_E_INVAL;   // blk_cap too small: *nblk_out says how many are needed
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) rc = MTBLX_E_HIP;
+  (void)hipFree(d);
+  if (rc == MTBLX_OK && (fl & (MTBLX_PLAN_OUT_OF_ORDER | MTBLX_PLAN_PANIC | MTBLX_PLAN_TOO_LONG))) rc = MTBLX_E_FORMAT;
+  return rc;
+}
+
+extern "C" int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk_rec, uint32_t nblk,
+                                   uint32_t restart_interval, int framed, uint8_t* out, uint64_t out_cap,
+                                   uint64_t* blk_off, uint32_t* blk_len, int32_t* status, uint64_t* totals,
+                                   void* workspace, size_t ws_bytes, void* stream) {
+  if (!rec || !blk_rec || !totals) return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(totals, 0, 16, s) != hipSuccess) return MTBLX_E_HIP;
+  if (nblk == 0) return MTBLX_OK;
+  if (!out || !blk_off || !blk_len || !status || !workspace || ws_bytes < mtblx_encode_workspace_bytes(nblk) ||
+      (reinterpret_cast<uintptr_t>(workspace) & 7u))
+    return MTBLX_E_INVAL;
+  // the look-back words and the ticket are polled: zero them every call
+  if (hipMemsetAsync(workspace, 0, mtblx_encode_workspace_bytes(nblk), s) != hipSuccess) return MTBLX_E_HIP;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(workspace);
+  EncArgs a{{rec->keys, rec->key_end, rec->vals, rec->val_end},
+            blk_rec,
+            nblk,
+            restart_interval,
+            framed ? 1 : 0,
+            out,
+            out_cap,
+            blk_off,
+            blk_len,
+            status,
+            totals,
+            reinterpret_cast<uint32_t*>(ws),
+            reinterpret_cast<uint64_t*>(ws + 256)};
+  hipLaunchKernelGGL(k_encode, dim3(nblk), dim3(kThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}

@@ -32,7 +32,9 @@ EXPORTS = [
     "mtblx_snappy_max_compressed_len", "mtblx_snappy_uncompressed_len", "mtblx_snappy_decompress",
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
     "mtblx_pipe_decode", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
+    "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
 ]
+PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
 
 class BlockBatch(C.Structure):
@@ -45,6 +47,11 @@ class Decoded(C.Structure):
                 ("status", C.c_void_p), ("key_end", C.c_void_p), ("val_end", C.c_void_p), ("rec_cap", C.c_uint64),
                 ("keys", C.c_void_p), ("keys_cap", C.c_uint64), ("vals", C.c_void_p), ("vals_cap", C.c_uint64),
                 ("totals", C.c_void_p)]
+
+
+class Records(C.Structure):
+    _fields_ = [("keys", C.c_void_p), ("key_end", C.c_void_p), ("vals", C.c_void_p), ("val_end", C.c_void_p),
+                ("n", C.c_uint64)]
 
 
 class PipeStats(C.Structure):
@@ -121,6 +128,15 @@ def lib() -> C.CDLL:
         L.mtblx_pipe_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_uint32, C.POINTER(Decoded), C.POINTER(PipeStats)]
         L.mtblx_pipe_decode.restype = C.c_int
+        L.mtblx_encode_plan.argtypes = [C.POINTER(Records), C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                        C.c_void_p, C.c_uint64, u64p, u32p, C.c_void_p]
+        L.mtblx_encode_plan.restype = C.c_int
+        L.mtblx_encode_workspace_bytes.argtypes = [C.c_uint32]
+        L.mtblx_encode_workspace_bytes.restype = C.c_size_t
+        L.mtblx_encode_blocks.argtypes = [C.POINTER(Records), C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p,
+                                          C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_size_t, C.c_void_p]
+        L.mtblx_encode_blocks.restype = C.c_int
         L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]
         L.mtblx_host_alloc.restype = C.c_int
         L.mtblx_host_free.argtypes = [C.c_void_p]

@@ -1,0 +1,133 @@
+"""Device encode side: the Writer's block cut + BlockBuilder + write_block framing.
+
+Python front-end of mtblx_encode_plan / mtblx_encode_blocks (include/mtblx.h, csrc/encode.hip):
+    Writer::insert flush rule   /root/reference/src/writer.rs:125-130
+    BlockBuilder::add / finish  src/block_builder.rs:49-104
+    write_block framing + crc   src/writer.rs:203-237
+Records stay on the device (torch tensors as plumbing); the kernels do the work.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib, codec
+from ._lib import Records
+
+
+class WriterPanic(RuntimeError):
+    """Where Writer::insert / BlockBuilder::add panic (flags: _lib.PLAN_*)."""
+
+    def __init__(self, flags: int):
+        super().__init__(f"writer panic flags={flags}")
+        self.flags = flags
+
+
+@dataclass
+class DeviceRecords:
+    """keys/vals: uint8; key_end/val_end: int64 END offsets (u64) from record 0."""
+    keys: torch.Tensor
+    key_end: torch.Tensor
+    vals: torch.Tensor
+    val_end: torch.Tensor
+
+    @property
+    def n(self) -> int:
+        return int(self.key_end.numel())
+
+    def cstruct(self) -> Records:
+        u = codec._u
+        return Records(u(self.keys), u(self.key_end), u(self.vals), u(self.val_end), self.n)
+
+    @staticmethod
+    def from_list(records, device="cuda") -> "DeviceRecords":
+        import numpy as np
+        ks = b"".join(bytes(k) for k, _ in records)
+        vs = b"".join(bytes(v) for _, v in records)
+        ke = np.cumsum([len(k) for k, _ in records], dtype=np.int64) if records else np.zeros(0, np.int64)
+        ve = np.cumsum([len(v) for _, v in records], dtype=np.int64) if records else np.zeros(0, np.int64)
+        t = lambda b: torch.frombuffer(bytearray(b or b"\0"), dtype=torch.uint8).to(device)  # noqa: E731
+        return DeviceRecords(t(ks), torch.from_numpy(ke).to(device), t(vs), torch.from_numpy(ve).to(device))
+
+
+def plan(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16, shard_rec=None,
+         stream=None) -> torch.Tensor:
+    """-> blk_rec (device int64 [nblk + 1]): block b = records [blk_rec[b], blk_rec[b+1]).
+    shard_rec: record boundaries of independent Writers (default: one Writer over all)."""
+    L = codec._require_device()
+    dev = recs.key_end.device
+    if shard_rec is None:
+        shard_rec = torch.tensor([0, recs.n], dtype=torch.int64, device=dev)
+    nsh = int(shard_rec.numel()) - 1
+    rc_ = recs.cstruct()
+    nb = C.c_uint64(0)
+    fl = C.c_uint32(0)
+    st = C.c_void_p(codec._stream_handle(stream))
+    rc = L.mtblx_encode_plan(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size),
+                             int(restart_interval), None, 0, C.byref(nb), C.byref(fl), st)
+    if rc == _lib.MTBLX_E_FORMAT:
+        raise WriterPanic(int(fl.value))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_encode_plan (count) failed: {rc}")
+    blk = torch.empty(int(nb.value) + 1, dtype=torch.int64, device=dev)
+    rc = L.mtblx_encode_plan(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size),
+                             int(restart_interval), C.c_void_p(blk.data_ptr()), blk.numel(), C.byref(nb), C.byref(fl),
+                             st)
+    if rc != 0:
+        raise RuntimeError(f"mtblx_encode_plan failed: {rc}")
+    return blk
+
+
+@dataclass
+class Encoded:
+    out: torch.Tensor       # uint8: blocks (framed: back to back from 0)
+    blk_off: torch.Tensor   # int64 content offsets
+    blk_len: torch.Tensor   # int32 content lengths
+    status: torch.Tensor    # int32 MTBLX_ST_*
+    totals: torch.Tensor    # int64 [2]: bytes, flags
+
+    def batch(self) -> codec.DeviceBatch:
+        """the encoded blocks as a decode batch (mtblx_decode_blocks input)"""
+        ml = int(self.blk_len.max().item()) if self.blk_len.numel() else 0
+        return codec.DeviceBatch(self.out, self.blk_off, self.blk_len, ml)
+
+
+class EncodeBuffers:
+    """Output + workspace of mtblx_encode_blocks, sized once for a record set and plan."""
+
+    def __init__(self, recs: DeviceRecords, nblk: int, device="cuda"):
+        L = _lib.lib()
+        n = recs.n
+        cap = int(recs.keys.numel()) + int(recs.vals.numel()) + 19 * n + 30 * nblk + 64
+        self.out = torch.empty(cap, dtype=torch.uint8, device=device)
+        m = max(nblk, 1)
+        self.blk_off = torch.empty(m, dtype=torch.int64, device=device)
+        self.blk_len = torch.empty(m, dtype=torch.int32, device=device)
+        self.status = torch.empty(m, dtype=torch.int32, device=device)
+        self.totals = torch.zeros(2, dtype=torch.int64, device=device)
+        self.ws_bytes = int(L.mtblx_encode_workspace_bytes(m))
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+        self.nblk = nblk
+
+
+def encode_into(recs: DeviceRecords, blk_rec: torch.Tensor, bufs: EncodeBuffers, restart_interval: int = 16,
+                framed: bool = True, stream=None) -> Encoded:
+    L = codec._require_device()
+    nblk = int(blk_rec.numel()) - 1
+    rc_ = recs.cstruct()
+    rc = L.mtblx_encode_blocks(C.byref(rc_), C.c_void_p(blk_rec.data_ptr()), nblk, int(restart_interval),
+                               1 if framed else 0, C.c_void_p(bufs.out.data_ptr()), bufs.out.numel(),
+                               C.c_void_p(bufs.blk_off.data_ptr()), C.c_void_p(bufs.blk_len.data_ptr()),
+                               C.c_void_p(bufs.status.data_ptr()), C.c_void_p(bufs.totals.data_ptr()),
+                               C.c_void_p(bufs.ws.data_ptr()), bufs.ws_bytes, C.c_void_p(codec._stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_encode_blocks failed: {rc}")
+    return Encoded(bufs.out, bufs.blk_off[:nblk], bufs.blk_len[:nblk], bufs.status[:nblk], bufs.totals)
+
+
+def encode_blocks(recs: DeviceRecords, blk_rec: torch.Tensor, restart_interval: int = 16, framed: bool = True,
+                  stream=None) -> Encoded:
+    bufs = EncodeBuffers(recs, int(blk_rec.numel()) - 1, device=recs.key_end.device)
+    return encode_into(recs, blk_rec, bufs, restart_interval, framed, stream)

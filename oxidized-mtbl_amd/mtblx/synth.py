@@ -1,6 +1,9 @@
 """Deterministic synthetic workloads for BASELINE.json's configs.
 
 cfg1  10 k keys "{:010}" / value "{:010}" * (1 + i % 8), 4 KiB blocks (examples/dump.rs plumbing)
+cfg3  64 KiB blocks, key length 8 + k with P(k) ~ (k+1)^-1.1, k = 0..248 (mean ~40 B), keys =
+      be64(c_i) || random tail (c_i = sum of gaps ~ U[1, 2^20)), 64 random value bytes,
+      restart interval 16, seed 0x6d74626c03; generated on the device (cfg3_records_device)
 cfg2  4 KiB blocks, 16 B keys = be64(c_i) || 8 random bytes with c_i = sum of gaps ~ U[1, 2^20)
       (strictly increasing, neighbours share ~5 B), 64 random value bytes, restart interval 16,
       CompressionType::None, seed 0x6d74626c02.
@@ -62,3 +65,33 @@ def cfg2_file(nblocks: int = 100_000, block_size: int = 4096, seed: int = SEED_C
         data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
     cfg2_file.last_block_nrec = write_arrays.last_block_nrec[:nblocks].copy()
     return data, off[:nblocks].copy(), ln[:nblocks].copy()
+
+
+def cfg3_key_len_probs():
+    """P(key length = 8 + k) for k = 0..248, proportional to (k + 1)^-1.1"""
+    w = (np.arange(249, dtype=np.float64) + 1.0) ** -1.1
+    return w / w.sum()
+
+
+def cfg3_records_device(nrec: int, seed: int = SEED_CFG3, c0: int = 0, device="cuda"):
+    """cfg3 records on the device (torch as plumbing): -> (DeviceRecords, c_last).  c0 continues
+    the key counter of a previous chunk so consecutive chunks stay strictly increasing."""
+    import torch
+
+    from .encode import DeviceRecords
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed) & ((1 << 63) - 1))
+    probs = torch.tensor(cfg3_key_len_probs(), dtype=torch.float32, device=device)
+    klen = torch.multinomial(probs, nrec, replacement=True, generator=g).to(torch.int64) + 8
+    gaps = torch.randint(1, 1 << 20, (nrec,), generator=g, device=device, dtype=torch.int64)
+    c = torch.cumsum(gaps, 0) + int(c0)
+    key_end = torch.cumsum(klen, 0)
+    total = int(key_end[-1].item())
+    keys = torch.randint(0, 256, (total,), generator=g, device=device, dtype=torch.uint8)
+    start = key_end - klen
+    be = torch.stack([(c >> (8 * (7 - j))) & 0xFF for j in range(8)], 1).to(torch.uint8)   # big-endian c
+    for j in range(8):
+        keys[start + j] = be[:, j]
+    vals = torch.randint(0, 256, (nrec * 64,), generator=g, device=device, dtype=torch.uint8)
+    val_end = torch.arange(1, nrec + 1, device=device, dtype=torch.int64) * 64
+    return DeviceRecords(keys, key_end, vals, val_end), int(c[-1].item())

@@ -1,0 +1,154 @@
+"""Device encode (Writer block cut + BlockBuilder + write_block framing) vs the oracle and
+the product host Writer (itself byte-identical to the oracle Writer, which the golden files pin).
+
+- framed blocks == the data-block region of the file the Writer writes, byte for byte
+- unframed block contents == oracle_build_block (src/block_builder.rs restated) per block
+- decode(encode(x)) == x on the cfg3 scheme (Zipf 8..256 B keys, 64 KiB blocks)
+- Writer panics (out-of-order key, interval 0) are reported, never produced
+"""
+import numpy as np
+import pytest
+
+import corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def _enc():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mtblx import encode
+    return encode
+
+
+def _writer_file(recs, block_size, interval):
+    from mtblx.writer import Writer
+    w = Writer(block_size, interval)
+    for k, v in recs:
+        w.insert(k, v)
+    data = w.into_inner()
+    off, ln = w.block_dir
+    return data, off, ln, w.block_nrec
+
+
+def test_framed_equals_writer_file(oracle):
+    enc = _enc()
+    rng = np.random.default_rng(61)
+    cases = [(1024, 16, 300, 0, 30, 0, 40), (4096, 16, 3000, 0, 80, 0, 200), (8192, 3, 2000, 0, 300, 0, 50),
+             (65536, 16, 6000, 8, 256, 64, 64), (2000, 1, 800, 0, 20, 0, 10), (4096, 40, 2500, 1, 60, 0, 120)]
+    for bs, iv, n, kmin, kmax, vmin, vmax in cases:
+        recs = corpus.random_records(rng, n, kmin, kmax, vmin, vmax)
+        data, off, ln, nrec = _writer_file(recs, bs, iv)
+        d = enc.DeviceRecords.from_list(recs)
+        blk = enc.plan(d, bs, iv).cpu().numpy()
+        assert blk.size - 1 == off.size, (bs, iv, blk.size - 1, off.size)
+        assert np.array_equal(np.diff(blk), nrec.astype(np.int64))
+        e = enc.encode_blocks(d, enc.plan(d, bs, iv), iv, framed=True)
+        total = int(e.totals[0].item())
+        assert int(e.totals[1].item()) == 0 and (e.status.cpu().numpy() == 0).all()
+        idx_off = int(np.frombuffer(data[-512:-504], np.uint64)[0])
+        assert total == idx_off
+        assert e.out[:total].cpu().numpy().tobytes() == data[:idx_off]
+        assert np.array_equal(e.blk_off.cpu().numpy().astype(np.uint64), off)
+        assert np.array_equal(e.blk_len.cpu().numpy().astype(np.uint32), ln)
+        # the oracle reads the device-written blocks back (its own CRC + decode)
+        orc = oracle.decode_blocks(e.out[:total].cpu().numpy(), off, ln)
+        assert (orc.status == 0).all() and int(orc.nrec.sum()) == n
+
+
+def test_unframed_blocks_equal_oracle_builder(oracle):
+    enc = _enc()
+    import torch
+    rng = np.random.default_rng(62)
+    for iv in (1, 2, 5, 16, 17, 40):
+        recs = corpus.random_records(rng, 1500, 0, 120, 0, 90)
+        d = enc.DeviceRecords.from_list(recs)
+        # arbitrary block cuts (not the Writer's): 0-record blocks included
+        cuts = np.sort(rng.integers(0, len(recs) + 1, 40))
+        blk = torch.tensor(np.concatenate([[0], cuts, [len(recs)]]), dtype=torch.int64, device="cuda")
+        e = enc.encode_blocks(d, blk, iv, framed=False)
+        out = e.out.cpu().numpy()
+        bo, bl = e.blk_off.cpu().numpy(), e.blk_len.cpu().numpy()
+        b = blk.cpu().numpy()
+        for j in range(b.size - 1):
+            exp = oracle.build_block(recs[b[j]: b[j + 1]], restart_interval=iv)
+            assert out[bo[j]: bo[j] + bl[j]].tobytes() == exp, (iv, j)
+    # interval 0: one-record blocks encode ([0, 0] restarts), two-record blocks panic
+    recs = corpus.random_records(rng, 10, 1, 10, 0, 10)
+    d = enc.DeviceRecords.from_list(recs)
+    blk = torch.tensor([0, 1, 2, 4, 5], dtype=torch.int64, device="cuda")
+    e = enc.encode_blocks(d, blk, 0, framed=False)
+    st = e.status.cpu().numpy()
+    assert st.tolist() == [0, 0, 2, 0]
+    out = e.out.cpu().numpy()
+    for j in (0, 1, 3):
+        o, n_ = int(e.blk_off[j].item()), int(e.blk_len[j].item())
+        assert out[o: o + n_].tobytes() == oracle.build_block(recs[int(blk[j]): int(blk[j + 1])], restart_interval=0)
+
+
+def test_writer_panics_reported():
+    enc = _enc()
+    import torch
+    recs = [(b"b", b"1"), (b"a", b"2")]
+    with pytest.raises(enc.WriterPanic) as ei:
+        enc.plan(enc.DeviceRecords.from_list(recs), 4096, 16)
+    assert ei.value.flags & 1
+    recs = [(bytes([i]), b"x") for i in range(1, 50)]
+    with pytest.raises(enc.WriterPanic) as ei:
+        enc.plan(enc.DeviceRecords.from_list(recs), 4096, 0)
+    assert ei.value.flags & 2
+    # equal keys are out of order too (key <= last_key)
+    with pytest.raises(enc.WriterPanic):
+        enc.plan(enc.DeviceRecords.from_list([(b"a", b""), (b"a", b"")]), 4096, 16)
+    del torch
+
+
+def test_shards_are_independent_writers():
+    enc = _enc()
+    import torch
+    rng = np.random.default_rng(63)
+    recs = corpus.random_records(rng, 4000, 0, 50, 0, 100)
+    cuts = [0, 700, 701, 2500, 2500, 4000]
+    d = enc.DeviceRecords.from_list(recs)
+    blk = enc.plan(d, 2048, 8, shard_rec=torch.tensor(cuts, dtype=torch.int64, device="cuda")).cpu().numpy()
+    exp = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if b > a:
+            _, _, _, nrec = _writer_file(recs[a:b], 2048, 8)
+            exp.append(a + np.concatenate([[0], np.cumsum(nrec)[:-1]]))
+    assert np.array_equal(blk[:-1], np.concatenate(exp)) and blk[-1] == 4000
+
+
+def test_cfg3_roundtrip_sample(oracle):
+    """cfg3 scheme on the device: plan -> encode -> decode == the generated records; a sample of
+    blocks against the oracle builder and decoder"""
+    enc = _enc()
+    import torch
+    from mtblx import codec, synth
+    recs, _ = synth.cfg3_records_device(300_000)
+    blk = enc.plan(recs, 65536, 16, shard_rec=torch.tensor([0, 100_000, 300_000], dtype=torch.int64, device="cuda"))
+    e = enc.encode_blocks(recs, blk, 16, framed=True)
+    assert int(e.totals[1].item()) == 0
+    assert int(e.blk_len.max().item()) <= 65536
+    out = codec.decode_blocks(e.batch())
+    torch.cuda.synchronize()
+    nr, kb, vb, fl = out.totals_host()
+    assert fl == 0 and nr == recs.n and (out.status[: out.nblk] == 0).all().item()
+    assert torch.equal(out.keys[:kb], recs.keys) and torch.equal(out.vals[:vb], recs.vals)
+    # key_end is block-relative u32: rebuild global ends and compare
+    nrec = out.nrec[: out.nblk].to(torch.int64)
+    blk_of = torch.repeat_interleave(torch.arange(out.nblk, device="cuda"), nrec)
+    ke = out.key_base[: out.nblk][blk_of] + (out.key_end[:nr].to(torch.int64) & 0xFFFFFFFF)
+    assert torch.equal(ke, recs.key_end)
+    # oracle sample: a few blocks' bytes == oracle builder over the same records
+    b = blk.cpu().numpy()
+    ho = e.out.cpu().numpy()
+    bo, bl = e.blk_off.cpu().numpy(), e.blk_len.cpu().numpy()
+    keys, ke_h = recs.keys.cpu().numpy(), recs.key_end.cpu().numpy()
+    vals, ve_h = recs.vals.cpu().numpy(), recs.val_end.cpu().numpy()
+    for j in (0, 1, b.size // 2, b.size - 2):
+        r0, r1 = int(b[j]), int(b[j + 1])
+        rr = [(keys[(ke_h[r - 1] if r else 0): ke_h[r]].tobytes(), vals[(ve_h[r - 1] if r else 0): ve_h[r]].tobytes())
+              for r in range(r0, r1)]
+        assert ho[bo[j]: bo[j] + bl[j]].tobytes() == oracle.build_block(rr, 16)

@@ -216,6 +216,229 @@ def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
     return res
 
 
+def _timed(fn, stream, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _max_over_ranks(x, dist):
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_cfg3(args, dist, world, rank):
+    """BASELINE configs[2]: 1 M blocks x 64 KiB per GPU, Zipf 8..256 B keys, 64 B values,
+    restart interval 16 -- device encode (Writer block cut + BlockBuilder + framing, src/writer.rs,
+    src/block_builder.rs) and decode round trip, bit-exact (every record compared on the device).
+    Generated and processed in chunks of `--cfg3-chunk` blocks (HBM holds records, blocks and
+    decoded outputs of one chunk at a time); kernel times are summed over chunks."""
+    from mtblx import codec, encode, synth
+    s = torch.cuda.Stream()
+    total_blocks = args.cfg3_blocks
+    per_chunk = args.cfg3_chunk
+    rec_per_blk = 640   # ~637 records per 64 KiB block at this key/value mix (SURVEY §8a)
+    c0 = 0
+    acc = dict(blocks=0, records=0, block_bytes=0, key_bytes=0, val_bytes=0, enc_ms=0.0, dec_ms=0.0, plan_ms=0.0,
+               file_bytes=0, mismatches=0, chunks=0)
+    done = 0
+    ci = 0
+    while done < total_blocks:
+        want = min(per_chunk, total_blocks - done)
+        nrec = int(want * rec_per_blk * 1.03) + 1024
+        recs, c_last = synth.cfg3_records_device(nrec, seed=synth.SEED_CFG3 + 1000 * rank + ci, c0=c0)
+        c0 = c_last
+        nsh = 64
+        cuts = torch.linspace(0, nrec, nsh + 1, device="cuda").to(torch.int64)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        blk = encode.plan(recs, 65536, 16, shard_rec=cuts)
+        acc["plan_ms"] += (time.perf_counter() - t0) * 1e3
+        blk = blk[: want + 1].contiguous()
+        nb = int(blk.numel()) - 1
+        bufs = encode.EncodeBuffers(recs, nb)
+        with torch.cuda.stream(s):
+            encode.encode_into(recs, blk, bufs, 16, True, s)      # warm-up
+            enc_ms = _timed(lambda: encode.encode_into(recs, blk, bufs, 16, True, s), s, 3)
+        e = encode.Encoded(bufs.out, bufs.blk_off[:nb], bufs.blk_len[:nb], bufs.status[:nb], bufs.totals)
+        if int(e.totals[1].item()) != 0:
+            raise RuntimeError("cfg3: encode reported a failed block")
+        batch = e.batch()
+        with torch.cuda.stream(s):
+            ws = codec.Workspace(nb)
+            probe = codec.DecodedBlocks(nb, 0, 0, 0)
+            codec.count_blocks(batch, probe, ws, s)
+        torch.cuda.synchronize()
+        nr, kb, vb, _ = probe.totals_host()
+        with torch.cuda.stream(s):
+            out = codec.DecodedBlocks(nb, nr, kb, vb)
+            codec.decode_into(batch, out, ws, s)
+            dec_ms = _timed(lambda: codec.decode_into(batch, out, ws, s), s, 5)
+        # round trip: every decoded record == the generated record
+        r_used = int(blk[-1].item())
+        ke_used = int(recs.key_end[r_used - 1].item())
+        ok = nr == r_used and kb == ke_used and vb == 64 * r_used and out.totals_host()[3] == 0
+        ok = ok and bool((out.status[:nb] == 0).all().item())
+        ok = ok and torch.equal(out.keys[:kb], recs.keys[:kb]) and torch.equal(out.vals[:vb], recs.vals[:vb])
+        if ok:
+            nrb = out.nrec[:nb].to(torch.int64)
+            blk_of = torch.repeat_interleave(torch.arange(nb, device="cuda"), nrb)
+            ke = out.key_base[:nb][blk_of] + (out.key_end[:nr].to(torch.int64) & 0xFFFFFFFF)
+            ok = torch.equal(ke, recs.key_end[:nr])
+        acc["mismatches"] += 0 if ok else 1
+        acc["blocks"] += nb
+        acc["records"] += nr
+        acc["block_bytes"] += int(e.blk_len.to(torch.int64).sum().item())
+        acc["file_bytes"] += int(e.totals[0].item())
+        acc["key_bytes"] += kb
+        acc["val_bytes"] += vb
+        acc["enc_ms"] += enc_ms
+        acc["dec_ms"] += dec_ms
+        acc["chunks"] += 1
+        done += nb
+        ci += 1
+        log(f"[rank {rank}] cfg3 chunk {ci}: {nb} blocks, enc {enc_ms:.2f} ms, dec {dec_ms:.2f} ms, ok={ok}")
+        del recs, blk, bufs, e, batch, ws, probe, out
+        torch.cuda.empty_cache()
+    if acc["mismatches"]:
+        raise RuntimeError(f"cfg3 round trip failed in {acc['mismatches']} chunk(s)")
+    dec_ms = _max_over_ranks(acc["dec_ms"], dist)
+    enc_ms = _max_over_ranks(acc["enc_ms"], dist)
+    bb = acc["block_bytes"] * world
+    alg_dec = acc["block_bytes"] + acc["key_bytes"] + acc["val_bytes"] + 8 * acc["records"] + 24 * acc["blocks"]
+    alg_enc = acc["key_bytes"] + acc["val_bytes"] + 16 * acc["records"] + acc["file_bytes"] + 8 * acc["blocks"]
+    return {
+        "metric": "cfg3 round trip: GiB/s of block bytes decoded / encoded, device-resident",
+        "value": round(bb / (dec_ms * 1e-3) / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+        "decode_records_per_s": round(acc["records"] * world / (dec_ms * 1e-3), 1),
+        "encode_GiB_per_s": round(bb / (enc_ms * 1e-3) / 2**30, 2),
+        "encode_records_per_s": round(acc["records"] * world / (enc_ms * 1e-3), 1),
+        "plan_ms_total": round(acc["plan_ms"], 1), "scaling": "weak", "dtype": "u8",
+        "data": "synthetic (device generator: Zipf 8..256 B keys = be64(counter) || random tail, 64 B random values)",
+        "config": {"workload": "cfg3: 64 KiB blocks, restart_interval=16, compression=none, encode (framed) + decode",
+                   "blocks_per_gpu": acc["blocks"], "records_per_gpu": acc["records"],
+                   "block_bytes_per_gpu": acc["block_bytes"], "chunks": acc["chunks"]},
+        "round_trip": "bit-exact (keys, values, key END offsets of every record; all statuses OK)",
+        "roofline": {"decode": {"kernel": "k_decode_pipe<PipeLarge>", "achieved_GBs":
+                                round(alg_dec / (acc["dec_ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                "alg_bytes": alg_dec},
+                     "encode": {"kernel": "k_encode", "achieved_GBs": round(alg_enc / (acc["enc_ms"] * 1e-3) / 1e9, 1),
+                                "peak": HBM_PEAK_GBS, "alg_bytes": alg_enc}},
+    }
+
+
+def run_cfg4(args, dist, world, rank):
+    """BASELINE configs[3]: 10 GiB of blocks in equal byte thirds of 4, 16 and 64 KiB blocks
+    (three files, cfg2 key/value scheme), sharded evenly over the ranks (10 GiB / world each);
+    device-resident decode of all three per step, plus the end-to-end pipe (pinned host file
+    in, pinned host outputs out) per leg.  Files are written on the device by the encode path
+    (byte-identical to the Writer, tests/test_encode_gpu.py)."""
+    from mtblx import codec, encode, pipe
+    s = torch.cuda.Stream()
+    per_leg = int(args.cfg4_gib * 2**30 / 3 / world)
+    legs = []
+    for li, bs in enumerate((4096, 16384, 65536)):
+        nrec = per_leg // 83 + 1024     # ~80 B of payload + header per record
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0x6D74626C04 + 100 * rank + li)
+        gaps = torch.randint(1, 1 << 20, (nrec,), generator=g, device="cuda", dtype=torch.int64)
+        c = torch.cumsum(gaps, 0)
+        keys = torch.randint(0, 256, (nrec, 16), generator=g, device="cuda", dtype=torch.uint8)
+        for j in range(8):
+            keys[:, j] = ((c >> (8 * (7 - j))) & 0xFF).to(torch.uint8)
+        vals = torch.randint(0, 256, (nrec * 64,), generator=g, device="cuda", dtype=torch.uint8)
+        recs = encode.DeviceRecords(keys.reshape(-1), torch.arange(1, nrec + 1, device="cuda") * 16, vals,
+                                    torch.arange(1, nrec + 1, device="cuda") * 64)
+        blk = encode.plan(recs, bs, 16)
+        # trim to the leg's byte budget (whole blocks)
+        e = encode.encode_blocks(recs, blk, 16, framed=True)
+        ends = torch.cumsum(e.blk_len.to(torch.int64), 0)
+        nb = int((ends <= per_leg).sum().item())
+        nr = int(blk[nb].item())
+        file_len = int(e.blk_off[nb - 1].item()) + int(e.blk_len[nb - 1].item())
+        data = e.out[:file_len]
+        batch = codec.DeviceBatch(data, e.blk_off[:nb].clone(), e.blk_len[:nb].clone(), int(e.blk_len[:nb].max().item()))
+        with torch.cuda.stream(s):
+            ws = codec.Workspace(nb)
+            out = codec.DecodedBlocks(nb, nr, 16 * nr, 64 * nr)
+        torch.cuda.synchronize()
+        legs.append(dict(bs=bs, nb=nb, nr=nr, bytes=int(ends[nb - 1].item()), batch=batch, ws=ws, out=out,
+                         host=data.cpu().numpy(), off=e.blk_off[:nb].cpu().numpy().astype(np.uint64),
+                         ln=e.blk_len[:nb].cpu().numpy().astype(np.uint32)))
+        del recs, keys, vals, gaps, c, blk, e
+        torch.cuda.empty_cache()
+
+    def step():
+        for L in legs:
+            codec.decode_into(L["batch"], L["out"], L["ws"], s)
+    with torch.cuda.stream(s):
+        for _ in range(args.warmup):
+            step()
+    torch.cuda.synchronize()
+    for L in legs:
+        h = L["out"].totals_host()
+        if h != (L["nr"], 16 * L["nr"], 64 * L["nr"], 0) or not bool((L["out"].status[: L["nb"]] == 0).all().item()):
+            raise RuntimeError(f"cfg4 leg {L['bs']}: decode mismatch {h}")
+    per_leg_ms = {}
+    with torch.cuda.stream(s):
+        for L in legs:
+            per_leg_ms[L["bs"]] = _timed(lambda: codec.decode_into(L["batch"], L["out"], L["ws"], s), s, 10)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        for _ in range(args.steps):
+            step()
+    torch.cuda.synchronize()
+    el = _max_over_ranks(time.perf_counter() - t0, dist)
+    tot_bytes = sum(L["bytes"] for L in legs)
+    tot_recs = sum(L["nr"] for L in legs)
+    res = {"metric": "cfg4: GiB/s of block bytes decoded, device-resident (mixed 4/16/64 KiB)",
+           "value": round(tot_bytes * world / (el / args.steps) / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+           "records_per_s": round(tot_recs * world / (el / args.steps), 1), "steps": args.steps,
+           "ms_per_step": round(el * 1e3 / args.steps, 3), "scaling": "weak (10 GiB / n_gpus per rank: strong over "
+                                                                      "the 10 GiB total)",
+           "dtype": "u8", "data": "synthetic cfg2 scheme, written on the device by the encode path",
+           "config": {"workload": "cfg4: 10 GiB total, equal byte thirds of 4/16/64 KiB blocks, sharded evenly",
+                      "total_GiB": args.cfg4_gib, "bytes_per_gpu": tot_bytes, "records_per_gpu": tot_recs},
+           "legs": {str(L["bs"]): {"blocks": L["nb"], "bytes": L["bytes"], "decode_ms": round(per_leg_ms[L["bs"]], 3),
+                                   "GiB_per_s": round(L["bytes"] / (per_leg_ms[L["bs"]] * 1e-3) / 2**30, 1)}
+                    for L in legs}}
+    # end-to-end per leg: pinned host file in, pinned host outputs out
+    if not args.no_e2e:
+        for L in legs:
+            del L["batch"], L["ws"], L["out"]
+        torch.cuda.empty_cache()
+        p = pipe.HostPipe(chunk_bytes=64 << 20, threads=16)
+        e2e_t = 0.0
+        for L in legs:
+            out = pipe.HostOutputs(L["nb"], L["nr"], 16 * L["nr"], 64 * L["nr"])
+            pipe.register(L["host"])
+            try:
+                p.decode(L["host"], L["off"], L["ln"], out)
+                if dist is not None:
+                    dist.barrier()
+                t0 = time.perf_counter()
+                p.decode(L["host"], L["off"], L["ln"], out)
+                dt = _max_over_ranks(time.perf_counter() - t0, dist)
+            finally:
+                pipe.unregister(L["host"])
+            if tuple(int(x) for x in out.totals) != (L["nr"], 16 * L["nr"], 64 * L["nr"], 0):
+                raise RuntimeError("cfg4 end-to-end decode mismatch")
+            e2e_t += dt
+            res["legs"][str(L["bs"])]["end_to_end_GiB_per_s"] = round(L["bytes"] * world / dt / 2**30, 2)
+        res["end_to_end_GiB_per_s"] = round(tot_bytes * world / e2e_t / 2**30, 2)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +453,11 @@ def main():
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32C verify measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host in, host out) measurement")
     ap.add_argument("--e2e-passes", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4"],
+                    help="cfg2 (default, BASELINE configs[1]: the metric's workload); cfg3 / cfg4 print their own line")
+    ap.add_argument("--cfg3-blocks", type=int, default=1_000_000)
+    ap.add_argument("--cfg3-chunk", type=int, default=100_000)
+    ap.add_argument("--cfg4-gib", type=float, default=10.0)
     ap.add_argument("--lib", default=None, help="diagnostic: alternative libmtblx build (ablations)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load libmtblx_stamps.so and report per-phase cycles per tile (not a measurement)")
@@ -252,6 +480,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mtblx import codec, synth
+
+    if args.config in ("cfg3", "cfg4"):
+        res = (run_cfg3 if args.config == "cfg3" else run_cfg4)(args, dist, world, rank)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     t = time.time()
     data, off, ln = synth.cfg2_file(args.blocks, block_size=args.block_size, seed=synth.SEED_CFG2 + rank)

@@ -1114,6 +1114,46 @@ __device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, ui
   return p == e && (orf & 0x808080u) == 0u && badsh == 0u;
 }
 
+// Walk of [s, e) that also accepts 2-byte varints (values < 16384: cfg3's long key suffixes).
+// Same deferred-check structure as walk_pos; an 8-byte window per header; rejects (-> the
+// exact walk_careful_pos) any varint of 3+ bytes, shared > previous key length, an overshoot
+// or more than 16 entries.  Reads past R land inside the LDS allocation or return 0 and are
+// never used when the walk is rejected (p is monotonic; the result requires p == e <= R).
+__device__ __forceinline__ bool walk_pos2(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t s, uint32_t e,
+                                          uint32_t slot0, uint32_t& cnt, uint32_t& kb, uint32_t& vb) {
+  cnt = kb = vb = 0;
+  if (!(s < e)) return false;
+  uint32_t p = s, prevlen = 0, bad = 0, ssh = 0, svl = 0, shl = 0, c = 0;
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
+  do {
+    const uint32_t ad = bo + p, q = ad >> 2, sft = (ad & 3u) * 8u;
+    const uint32_t w0 = st32[q], w1 = st32[q + 1], w2 = st32[q + 2];
+    uint64_t x = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sft) |
+                 ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sft) << 32);
+    uint32_t f[3], hl = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t b0 = (uint32_t)x & 0xffu, b1 = (uint32_t)(x >> 8) & 0xffu, two = b0 >> 7;
+      f[k] = (b0 & 0x7fu) | (two ? (b1 & 0x7fu) << 7 : 0u);
+      bad |= two & (b1 >> 7);                    // a 3+ byte varint
+      x >>= 8u * (1u + two);
+      hl += 1u + two;
+    }
+    pos[slot0 + c] = (uint16_t)p;
+    bad |= (uint32_t)(f[0] > prevlen);
+    prevlen = f[0] + f[1];
+    ssh += f[0];
+    svl += f[2];
+    shl += hl;
+    c += 1;
+    p += hl + f[1] + f[2];
+  } while (p < e && c < (uint32_t)kP2Spi);
+  cnt = c;
+  vb = svl;
+  kb = ssh + (p - s) - shl - svl;   // sum(shared + non_shared): p - s = sum(header + ns + vl)
+  return p == e && bad == 0u;
+}
+
 // exact walk (multi-byte varint headers allowed) recording header offsets; same checks as
 // walk_interval
 __device__ __forceinline__ bool walk_careful_pos(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t L, uint32_t R,
@@ -1259,6 +1299,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
     ST.hit(10);
     const uint32_t slot0 = (uint32_t)lane * kP2Spi;
     wok = e <= jR && walk_pos(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb);
+    if (!wok) wok = e <= jR && walk_pos2(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb);
     if (!wok) wok = walk_careful_pos(B.stage, B.pos, jbo, jL, jR, s, e, slot0, cnt, kb, vb);
     B.iraw[lane] = (uint8_t)(cnt < 255u ? cnt : 255u);
     B.iblk[lane] = (uint8_t)j;
@@ -1533,6 +1574,15 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
   uint8_t* kd = a.keys + pk + r.ks;
   if (live && r.klen > 0u) store_bytes(kd, r.W0, r.klen < 16u ? r.klen : 16u);
   for (uint32_t q0 = 16; __ballot(live && r.klen > q0) != 0ull; q0 += 16) {   // further planes (keys > 16 B)
+    if (__ballot(live && r.sh > q0 && q0 < r.klen) == 0ull) {
+      // no live entry inherits a byte of this plane from an earlier key: every byte is the
+      // entry's own suffix (typical for long keys with short shared prefixes), copy it directly
+      if (live && q0 < r.klen) {
+        const uint32_t n = r.klen - q0;
+        store_bytes(kd + q0, lds_win16(B.stage, r.sp - r.sh + q0), n < 16 ? n : 16);
+      }
+      continue;
+    }
     const bool own = live && r.sh < q0 + 16u && q0 < r.klen;
     uint4 W = own ? lds_win16(B.stage, r.sp - r.sh + q0) : make_uint4(0, 0, 0, 0);
     uint32_t m = r.sh;

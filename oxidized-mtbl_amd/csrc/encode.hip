@@ -30,9 +30,10 @@
 namespace mtblx_enc {
 
 constexpr int kWave = 64;
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / kWave;
 constexpr uint32_t kLdsBlock = 65536 + 1024;   // contents up to this many bytes are assembled in LDS
+constexpr uint32_t kShCache = 2048;            // entries whose `shared` phase A keeps for phase B
 constexpr uint64_t kIncl = 1ull << 63, kAgg = 1ull << 62, kVal = kAgg - 1;
 
 typedef uint64_t __attribute__((aligned(1))) u64u;
@@ -225,7 +226,8 @@ struct EncArgs {
 
 struct alignas(16) EncLds {
   uint8_t ob[kLdsBlock];
-  uint32_t T[256];
+  uint32_t T[4][256];        // slicing-by-4 CRC-32C tables
+  uint16_t shc[kShCache];    // phase A's `shared` of the first entries (0xFFFF: recompute)
   uint64_t red[kWaves];
   uint32_t redf[kWaves];
   uint64_t sh_u64[4];
@@ -266,46 +268,46 @@ __device__ __forceinline__ void put32(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
 
-// CRC-32C of d[0..L) by the workgroup (crate crc32c 0.4).  64-byte chunks counted from the
-// START (16-byte aligned for the LDS buffer); chunk j's raw CRC is shifted by the bytes after
-// it: x^(512 (nfull-1-j)) * x^(8 tail).  The 0xFFFFFFFF init is folded into the first 4 bytes.
+// CRC-32C of d[0..L) by the workgroup (crate crc32c 0.4).  Thread t takes the contiguous span
+// [t S, (t+1) S) (S a multiple of 16: aligned 16 B reads of the LDS buffer), computes its raw
+// CRC with slicing-by-4, and shifts it by the bytes after the span, x^(8 m) = x^(512 (m / 64))
+// * x^(8 (m % 64)); the spans are XOR-combined.  The 0xFFFFFFFF init is folded into the first
+// 4 bytes; the final complement is the xorout.
+__device__ __forceinline__ uint32_t crc_word(const EncLds& S, uint32_t c, uint32_t w) {
+  c ^= w;
+  return S.T[3][c & 0xffu] ^ S.T[2][(c >> 8) & 0xffu] ^ S.T[1][(c >> 16) & 0xffu] ^ S.T[0][c >> 24];
+}
+
 __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t acc = 0;
   if (L >= 4) {
-    const uint64_t nfull = L / 64, tail = L - 64 * nfull;
-    for (uint64_t j = tid; j <= nfull; j += kThreads) {
-      const uint64_t lo = 64 * j;
-      const uint32_t n = j < nfull ? 64u : (uint32_t)tail;
-      if (n == 0) continue;
+    const uint64_t per = (L + kThreads - 1) / kThreads;
+    const uint64_t span = ((per + 15) / 16) * 16;
+    const uint64_t a0 = (uint64_t)tid * span;
+    const uint64_t a1 = a0 + span < L ? a0 + span : L;
+    if (a0 < a1) {
       uint32_t c = 0;
-      if (n == 64) {
-        uint32_t wd[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
-          wd[4 * q] = x.x; wd[4 * q + 1] = x.y; wd[4 * q + 2] = x.z; wd[4 * q + 3] = x.w;
-        }
-        if (lo == 0) wd[0] ^= 0xFFFFFFFFu;
-#pragma unroll
-        for (int k = 0; k < 64; ++k) {
-          const uint32_t byte = (wd[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-          c = S.T[(c ^ byte) & 0xFFu] ^ (c >> 8);
-        }
-        c = mtblx_crc::dmultmodp(mtblx_crc::xpow512(nfull - 1 - j), c);
-        if (tail) c = mtblx_crc::dmultmodp(kX8.p[tail], c);
-      } else {   // the tail chunk (< 64 bytes, byte loads: never past the content)
-        for (uint32_t k = 0; k < n; ++k) {
-          uint32_t byte = d[lo + k];
-          if (lo + k < 4) byte ^= 0xFFu;
-          c = S.T[(c ^ byte) & 0xFFu] ^ (c >> 8);
-        }
+      uint64_t o = a0;
+      for (; o + 16 <= a1; o += 16) {
+        const v4u x = *reinterpret_cast<const v4u*>(d + o);
+        c = crc_word(S, c, o == 0 ? x.x ^ 0xFFFFFFFFu : x.x);
+        c = crc_word(S, c, x.y);
+        c = crc_word(S, c, x.z);
+        c = crc_word(S, c, x.w);
       }
-      acc ^= c;
+      for (; o < a1; ++o) {   // tail bytes (byte loads: never past the content)
+        uint32_t byte = d[o];
+        if (o < 4) byte ^= 0xFFu;
+        c = S.T[0][(c ^ byte) & 0xFFu] ^ (c >> 8);
+      }
+      const uint64_t m = L - a1;
+      if (m) c = mtblx_crc::dmultmodp(mtblx_crc::dmultmodp(mtblx_crc::xpow512(m / 64), kX8.p[m % 64]), c);
+      acc = c;
     }
   } else if (tid == 0) {
     uint32_t c = 0xFFFFFFFFu;
-    for (uint64_t i = 0; i < L; ++i) c = S.T[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+    for (uint64_t i = 0; i < L; ++i) c = S.T[0][(c ^ d[i]) & 0xFFu] ^ (c >> 8);
     acc = c ^ 0xFFFFFFFFu ^ 0xFFFFFFFFu;   // complemented again below
   }
 #pragma unroll
@@ -323,11 +325,14 @@ __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
 struct Ent {
   uint64_t k0, kl, v0, vl, sh;
 };
-__device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, uint32_t iv) {
+__device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, uint32_t iv,
+                                        const uint16_t* shc = nullptr) {
   Ent e;
   rec_of(R, r0 + i, e.k0, e.kl, e.v0, e.vl);
   e.sh = 0;
-  if (shares(i, iv)) {
+  if (shc && i < kShCache && shc[i] != 0xFFFFu) {
+    e.sh = shc[i];
+  } else if (shares(i, iv)) {
     uint64_t pk0, pkl, pv0, pvl;
     rec_of(R, r0 + i - 1, pk0, pkl, pv0, pvl);
     int c;
@@ -371,10 +376,18 @@ __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeo
   return excl;
 }
 
-__global__ void __launch_bounds__(kThreads, 2) k_encode(EncArgs a) {
+__global__ void __launch_bounds__(kThreads) k_encode(EncArgs a) {
   __shared__ EncLds S;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < 256; i += kThreads) S.T[i] = mtblx_crc::kTab.byte[i];
+  for (int i = tid; i < 256; i += kThreads) {   // slicing-by-4 tables from the byte table
+    uint32_t t = mtblx_crc::kTab.byte[i];
+    S.T[0][i] = t;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
+      S.T[k][i] = t;
+    }
+  }
   if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
   __syncthreads();
   const uint32_t b = S.sh_u32[0];
@@ -387,6 +400,7 @@ __global__ void __launch_bounds__(kThreads, 2) k_encode(EncArgs a) {
   for (uint64_t i = tid; i < n; i += kThreads) {
     const Ent e = entry_of(a.R, r0, i, iv);
     part += entry_bytes(e.sh, e.kl, e.vl);
+    if (i < kShCache) S.shc[i] = e.sh < 0xFFFFu ? (uint16_t)e.sh : (uint16_t)0xFFFFu;
   }
   uint64_t entries = 0;
   (void)wg_excl_scan(S, part, entries);
@@ -411,7 +425,7 @@ __global__ void __launch_bounds__(kThreads, 2) k_encode(EncArgs a) {
       Ent e{};
       uint64_t sz = 0;
       if (i < n) {
-        e = entry_of(a.R, r0, i, iv);
+        e = entry_of(a.R, r0, i, iv, S.shc);
         sz = entry_bytes(e.sh, e.kl, e.vl);
       }
       uint64_t tot = 0;

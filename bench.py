@@ -603,9 +603,23 @@ def main():
             c1.record(stream)
         torch.cuda.synchronize()
         crc_ms = c0.elapsed_time(c1) / 10
+        # f1 fused: decode + checksum in one launch (the Reader's default verify_checksums path)
+        vbad = torch.zeros(batch.nblk, dtype=torch.uint8, device="cuda")
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=True)
+            v_ms = _timed(lambda: codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=True),
+                          stream, 20)
+        hv = out.totals_host()
+        if hv[:3] != h[:3] or hv[3] != 0 or int(vbad.sum().item()) != 0:
+            raise RuntimeError(f"fused verify decode mismatch: {hv}")
         crc_info = {"kernel": "k_crc32c_blocks", "ms": round(crc_ms, 4),
                     "GiB_per_s": round(block_bytes / (crc_ms * 1e-3) / 2**30, 1),
-                    "bad_blocks": int(bad.sum().item())}
+                    "bad_blocks": int(bad.sum().item()),
+                    "fused_decode_verify": {"kernel": "k_decode_pipe<PipeSmallV>", "ms": round(v_ms, 4),
+                                            "GiB_per_s": round(block_bytes / (v_ms * 1e-3) / 2**30, 1),
+                                            "vs_decode_then_crc_GiB_per_s":
+                                                round(block_bytes / ((k_decode_ms + crc_ms) * 1e-3) / 2**30, 1)}}
 
     res = {
         "metric": "KV records/s + GiB/s of block bytes decoded, device-resident",

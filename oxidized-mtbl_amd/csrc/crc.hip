@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data,
     const uint8_t* d = data + off;
     const uint32_t acc = wave_crc32c(d, L, T, lane);
     if (lane == 0) {
-      crc_out[b] = acc;
+      if (crc_out) crc_out[b] = acc;
       if (bad) {
         uint32_t stored = 0;
         if (framed && off >= 4)
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data,
 
 extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed,
                                    void* stream) {
-  if (!in || (!crc && in->nblk)) return MTBLX_E_INVAL;
+  if (!in || (!crc && !bad && in->nblk)) return MTBLX_E_INVAL;
   if (in->nblk == 0) return MTBLX_OK;
   if (!in->data || !in->blk_off || !in->blk_len) return MTBLX_E_INVAL;
   static int grid = 0;

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 
+#include "crc_dev.h"
 #include "mtblx.h"
 
 namespace mtblx {
@@ -319,6 +320,9 @@ struct TileArgs {
   struct WsHdr* hdr;
   uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
   int write;
+  uint32_t* crc;     // VERIFY kernels: crc32c of every block's content (may be NULL)
+  uint8_t* crc_bad;  // VERIFY kernels: 1 where the stored checksum differs (may be NULL)
+  int crc_framed;    // the u32 before each content is its stored checksum (an mtbl file)
   // set at kernel start from the workspace header (ws_begin)
   uint32_t wscap;   // tile entries the workspace holds (from workspace_bytes)
   uint32_t par;     // launch parity: aggregates live in slot `par` of each tile entry
@@ -987,13 +991,16 @@ constexpr int kP2Spi = 16;                                               // slot
 // LDS (3: DMA / walk / copy of three tiles overlap; 2: DMA of the next tile overlaps the
 // walk + copy of this one), MAXBLK blocks and MAXINT (<= 64: one walk lane each) restart
 // intervals per tile.
-template <int TB_, int NBUF_, int MAXBLK_, int MAXINT_>
+template <int TB_, int NBUF_, int MAXBLK_, int MAXINT_, bool VERIFY_ = false>
 struct PipeCfg {
   static constexpr int TB = TB_, NBUF = NBUF_, MAXBLK = MAXBLK_, MAXINT = MAXINT_;
   static constexpr int SLOTS = MAXINT * kP2Spi;
+  static constexpr bool VERIFY = VERIFY_;   // fused CRC-32C of every staged block (f1)
 };
 using PipeSmall = PipeCfg<49152, 3, 16, 56>;   // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
 using PipeLarge = PipeCfg<65664, 2, 2, 64>;    // blocks up to ~64 KiB (cfg3, cfg4 64 KiB)
+using PipeSmallV = PipeCfg<49152, 3, 16, 56, true>;
+using PipeLargeV = PipeCfg<65664, 2, 2, 64, true>;
 
 template <class P>
 struct alignas(16) PipeBuf {
@@ -1019,6 +1026,11 @@ struct alignas(16) PipeLds {
   uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
   uint32_t pub;      // wave 0 sets after publishing the aggregate of the tile it walked
   uint32_t cdone;    // copy waves that finished their copy (monotonic)
+  // VERIFY: slicing-by-4 CRC-32C tables, per-block XOR accumulators (by tile parity), and
+  // the count of CRC waves done (monotonic; the last of a tile finalises it)
+  uint32_t crcT[P::VERIFY ? 4 : 1][P::VERIFY ? 256 : 1];
+  uint32_t cacc[2][P::VERIFY ? P::MAXBLK : 1];
+  uint32_t crcdone;
 };
 
 __device__ __forceinline__ void raw_barrier() {
@@ -1636,6 +1648,130 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
   }
 }
 
+// ---------------------------------------------------------------------------------
+// fused CRC-32C verify (VERIFY kernels): the checksum Reader::block asserts
+// before it decodes a block (src/reader.rs:159-164, crate crc32c 0.4), computed from the tile
+// already staged in LDS by the waves that otherwise idle there: the look-back wave after its
+// look-back and the two loader waves after issuing their DMA.  64-byte chunks counted from
+// each block's END (chunk k is shifted by x^(512 k), a table lookup + one GF(2) multiply),
+// slicing-by-4 over 16 words, 4 chunks in flight per lane; contributions are XORed into a
+// per-block LDS accumulator; the last of the three waves to finish a tile finalises it.
+// ---------------------------------------------------------------------------------
+constexpr int kCrcWaves = 3;   // the look-back wave + the two loader waves
+
+template <class P>
+__device__ __forceinline__ uint32_t crc_word4(const PipeLds<P>& S, uint32_t c, uint32_t w) {
+  c ^= w;   // slicing-by-4 (measured 0.62 ms vs 0.74 ms byte-at-a-time in this kernel, cfg2)
+  return S.crcT[3][c & 0xffu] ^ S.crcT[2][(c >> 8) & 0xffu] ^ S.crcT[1][(c >> 16) & 0xffu] ^ S.crcT[0][c >> 24];
+}
+
+template <class P>
+__device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, int cw, int lane, uint32_t par) {
+  const uint32_t nb = B.nb, b0 = B.b0;
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(B.stage);
+  const uint32_t gl = (uint32_t)cw * kWave + (uint32_t)lane;
+  // chunks of staged blocks of >= 4 bytes, numbered across the tile
+  uint32_t total = 0;
+  for (uint32_t j = 0; j < nb; ++j) {
+    const uint32_t L = B.blen[j];
+    total += (B.boff[j] != kNotStaged && L >= 4u) ? (L + 63u) / 64u : 0u;
+  }
+  // per-lane chunk prefix of the tile's blocks (lane j < nb holds the first chunk of block j)
+  uint32_t mych = 0, myL = 0, mybo = 0;
+  if (lane < (int)nb) {
+    myL = B.blen[lane];
+    mybo = B.boff[lane];
+    mych = (mybo != kNotStaged && myL >= 4u) ? (myL + 63u) / 64u : 0u;
+  }
+  const uint32_t incl = wave_incl_scan(mych), excl = incl - mych;
+  constexpr int kCh = 2;   // chunks in flight per lane (register budget: 128 VGPRs at 16 waves/CU)
+  for (uint32_t base = 0; base < total; base += kCh * kCrcWaves * kWave) {
+    uint32_t c[kCh], d0[kCh], jk[kCh], sft[kCh];   // jk = block << 16 | chunk
+    int32_t q[kCh], p0[kCh];   // first dword index; block position of the window's first byte
+#pragma unroll
+    for (int i = 0; i < kCh; ++i) {
+      const uint32_t ch = base + (uint32_t)i * kCrcWaves * kWave + gl;
+      uint32_t j0 = 0;
+      for (uint32_t j = 1; j < nb; ++j) j0 += ((uint32_t)__shfl((int)excl, (int)j, kWave) <= ch) ? 1u : 0u;
+      const uint32_t e0 = (uint32_t)__shfl((int)excl, (int)j0, kWave);
+      const uint32_t L = (uint32_t)__shfl((int)myL, (int)j0, kWave), bo = (uint32_t)__shfl((int)mybo, (int)j0, kWave);
+      const bool on = ch < total;
+      const uint32_t k0 = on ? ch - e0 : 0xFFFFu;
+      jk[i] = j0 << 16 | k0;
+      // window [L - 64 (k0 + 1), L - 64 k0): bytes before the block start read as 0 (leading
+      // zeros leave a zero-init CRC unchanged), so every chunk is 16 word steps
+      p0[i] = on ? (int32_t)L - 64 * (int32_t)k0 - 64 : (1 << 20);   // off: never masked, result dropped
+      const int32_t A = on ? (int32_t)bo + p0[i] : 0;               // stage address (< 0 possible)
+      q[i] = A >> 2;                                                // floor
+      sft[i] = (uint32_t)(A & 3) * 8u;
+      d0[i] = q[i] >= 0 ? st32[q[i]] : 0u;
+      c[i] = 0;
+    }
+#pragma unroll 2
+    for (int m = 0; m < 16; ++m) {
+#pragma unroll
+      for (int i = 0; i < kCh; ++i) {
+        const int32_t pos = p0[i] + 4 * m;           // block position of the word's first byte
+        const int32_t qa = q[i] + m + 1;
+        const uint32_t d1 = qa >= 0 ? st32[qa] : 0u;
+        uint32_t w = __builtin_amdgcn_alignbit(d1, d0[i], sft[i]);
+        d0[i] = d1;
+        if (pos < 4) {   // leading zeros (pos < 0) and the 0xFFFFFFFF init folded into bytes 0..3
+          const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8u * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+          const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8u * (uint32_t)pos);
+          w = (w & keep) ^ fold;
+        }
+        c[i] = crc_word4(S, c[i], w);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kCh; ++i) {
+      const uint32_t k0 = jk[i] & 0xFFFFu;
+      if (k0 != 0xFFFFu) atomicXor(&S.cacc[par][jk[i] >> 16], mtblx_crc::dmultmodp(mtblx_crc::xpow512(k0), c[i]));
+    }
+  }
+  // the last CRC wave of this tile finalises it
+  uint32_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(&S.crcdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+  if (old % kCrcWaves != kCrcWaves - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint32_t crc = 0, L = 0, o = kNotStaged;
+  if (lane < (int)nb) {
+    L = B.blen[lane];
+    o = B.boff[lane];
+    if (o != kNotStaged && L >= 4u) {
+      crc = S.cacc[par][lane] ^ 0xFFFFFFFFu;
+    } else if (o != kNotStaged) {   // < 4 bytes: byte-wise with the init
+      uint32_t x = 0xFFFFFFFFu;
+      for (uint32_t t = 0; t < L; ++t) x = S.crcT[0][(x ^ B.stage[o + t]) & 0xffu] ^ (x >> 8);
+      crc = x ^ 0xFFFFFFFFu;
+    }
+    S.cacc[par][lane] = 0;
+  }
+  // blocks that were not staged (larger than a slot): from HBM, the wave together
+  for (uint32_t j = 0; j < nb; ++j) {
+    if (B.boff[j] != kNotStaged) continue;
+    const uint64_t off = a.blk_off[b0 + j];
+    const uint32_t x = mtblx_crc::wave_crc32c(a.data + off, B.blen[j], &S.crcT[0][0], lane);
+    if (lane == (int)j) crc = x;
+  }
+  if (lane < (int)nb) {
+    const uint32_t b = b0 + lane;
+    if (a.crc) a.crc[b] = crc;
+    if (a.crc_bad) {
+      uint8_t bad = 0;
+      const uint64_t off = a.blk_off[b];
+      if (a.crc_framed && off >= 4) {
+        const uint8_t* d = a.data + off;
+        const uint32_t stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
+        bad = stored != crc;
+      }
+      a.crc_bad[b] = bad;
+    }
+  }
+}
+
 template <class P>
 __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   __shared__ PipeLds<P> S;
@@ -1645,7 +1781,19 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   Stamps ST;
   ST.init();
   ws_begin(a);
-  if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; }
+  if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; }
+  if constexpr (P::VERIFY) {
+    for (int i = tid; i < 256; i += kPipeThreads) {   // slicing-by-4 tables from the byte table
+      uint32_t t = mtblx_crc::kTab.byte[i];
+      S.crcT[0][i] = t;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
+        S.crcT[k][i] = t;
+      }
+    }
+    for (int i = tid; i < 2 * P::MAXBLK; i += kPipeThreads) S.cacc[i / P::MAXBLK][i % P::MAXBLK] = 0;
+  }
 
   uint64_t tinc[3] = {0, 0, 0};           // wave 1
   uint64_t lbv[kMaxLookbackLoads];        // wave 1: look-back words of the next tile to copy
@@ -1690,6 +1838,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           load_info(it + 2);
         }
         ST.hit(4);
+        if constexpr (P::VERIFY) pipe_crc(C, a, S, 1 + (int)part, lane, it & 1u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+1 (read next phase)
         ST.hit(6);
       } else if (wv == 1) {
@@ -1699,6 +1848,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&S.ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(1);
+        if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
         wait_flag(&S.pub, it + 1);
         pipe_copy(C, a, wv - kPipeCopyWave0, lane, &S.ready, it + 1, ST);
@@ -1726,6 +1876,9 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         load_info(k2 + 1);
       }
       ST.hit(4);
+      if constexpr (P::VERIFY) {
+        if (it >= 0) pipe_crc(S.buf[(uint32_t)it % P::NBUF], a, S, 1 + (int)part, lane, (uint32_t)it & 1u);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+2 (read next phase)
       ST.hit(6);
     } else if (it >= 0) {
@@ -1736,6 +1889,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&S.ready, (uint32_t)it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(1);
+        // CRC of tile it while lbv is dead (its words were consumed above): lower register pressure
+        if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, (uint32_t)it & 1u);
         if (k1 < nloc) {
           // the other workgroups publish A(tile it+1's predecessors) about when this
           // workgroup's wave 0 publishes A(tile it+1): issue the look-back loads after that
@@ -1856,8 +2011,11 @@ int resident_grid(uint32_t ntiles) {
 // Zero-filled once by the caller; every launch leaves it ready for the next (ws_end).
 extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
 
+extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed,
+                                   void* stream);
+
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t ws_bytes,
-                              int write, hipStream_t s) {
+                              int write, hipStream_t s, int verify, uint32_t* crc, uint8_t* crc_bad, int framed) {
   const uint32_t nblk = in->nblk;
   const uint64_t cap64 = ws_bytes > 320u ? (ws_bytes - 320u) / 24u : 0u;
   const uint32_t wscap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;
@@ -1868,13 +2026,22 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
   TileArgs a{in->data,     in->data_len,  in->blk_off,  in->blk_len,   nblk,         p.bpt,         p.slot,
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
-             lbw,          hdr,           dbg,          write ? 1 : 0, wscap,       0,             0};
+             lbw,          hdr,           dbg,          write ? 1 : 0, crc,         crc_bad,       framed ? 1 : 0,
+             wscap,        0,             0};
   if (p.kind == 0) {
-    hipLaunchKernelGGL(k_decode_pipe<PipeSmall>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+    if (verify)
+      hipLaunchKernelGGL(k_decode_pipe<PipeSmallV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_decode_pipe<PipeSmall>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   } else if (p.kind == 1) {
-    hipLaunchKernelGGL(k_decode_pipe<PipeLarge>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+    if (verify)
+      hipLaunchKernelGGL(k_decode_pipe<PipeLargeV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_decode_pipe<PipeLarge>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   } else {
     hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
+    // blocks above ~64 KiB: the checksum is a separate launch (k_crc32c_blocks)
+    if (verify && hipGetLastError() == hipSuccess) return mtblx_crc32c_blocks(in, crc, crc_bad, framed, s);
   }
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -10,7 +10,10 @@
 
 extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk);
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t ws_bytes,
-                              int write, hipStream_t s);
+                              int write, hipStream_t s, int verify, uint32_t* crc, uint8_t* crc_bad, int framed);
+
+extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed,
+                                   void* stream);
 
 extern "C" int mtblx_abi_version(void) { return MTBLX_ABI_VERSION; }
 
@@ -45,7 +48,7 @@ extern "C" int mtblx_count_blocks(const mtblx_block_batch* in, const mtblx_decod
                                   void* stream) {
   int c = check_common(in, out, ws, wsb, stream);
   if (c != 1) return c;
-  return mtblx_impl_run(in, out, ws, wsb, 0, reinterpret_cast<hipStream_t>(stream));
+  return mtblx_impl_run(in, out, ws, wsb, 0, reinterpret_cast<hipStream_t>(stream), 0, nullptr, nullptr, 0);
 }
 
 extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
@@ -56,7 +59,7 @@ extern "C" int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_dec
       (!out->val_end && out->rec_cap))
     return MTBLX_E_INVAL;
   // single-pass kernel: counting is fused into the decode, so this is a full decode
-  return mtblx_impl_run(in, out, ws, wsb, 1, reinterpret_cast<hipStream_t>(stream));
+  return mtblx_impl_run(in, out, ws, wsb, 1, reinterpret_cast<hipStream_t>(stream), 0, nullptr, nullptr, 0);
 }
 
 extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t wsb,
@@ -66,5 +69,21 @@ extern "C" int mtblx_decode_blocks(const mtblx_block_batch* in, const mtblx_deco
   if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
       (!out->val_end && out->rec_cap))
     return MTBLX_E_INVAL;
-  return mtblx_impl_run(in, out, ws, wsb, 1, reinterpret_cast<hipStream_t>(stream));
+  return mtblx_impl_run(in, out, ws, wsb, 1, reinterpret_cast<hipStream_t>(stream), 0, nullptr, nullptr, 0);
+}
+
+extern "C" int mtblx_decode_blocks_verify(const mtblx_block_batch* in, const mtblx_decoded* out, uint32_t* crc,
+                                          uint8_t* crc_bad, int framed, void* ws, size_t wsb, void* stream) {
+  int c = check_common(in, out, ws, wsb, stream);
+  if (c != 1) return c;
+  if ((!out->keys && out->keys_cap) || (!out->vals && out->vals_cap) || (!out->key_end && out->rec_cap) ||
+      (!out->val_end && out->rec_cap) || (!crc && !crc_bad))
+    return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (framed & MTBLX_VERIFY_FUSED)   // one launch: the CRC from the LDS-staged tiles
+    return mtblx_impl_run(in, out, ws, wsb, 1, s, 1, crc, crc_bad, framed & 1);
+  // default: the decode, then k_crc32c_blocks on the same stream (faster on gfx950)
+  const int rc = mtblx_impl_run(in, out, ws, wsb, 1, s, 0, nullptr, nullptr, 0);
+  if (rc != MTBLX_OK) return rc;
+  return mtblx_crc32c_blocks(in, crc, crc_bad, framed & 1, stream);
 }

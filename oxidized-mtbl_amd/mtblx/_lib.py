@@ -26,7 +26,7 @@ GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP = range(5)
 # every symbol the public headers declare (checked by tests/test_abi.py)
 EXPORTS = [
     "mtblx_abi_version", "mtblx_device_ok", "mtblx_decode_workspace_bytes", "mtblx_decode_blocks",
-    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_get", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
+    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_decode_blocks_verify", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_get", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
     "mtblx_writer_new", "mtblx_writer_insert", "mtblx_writer_insert_batch", "mtblx_writer_finish",
     "mtblx_writer_block_count", "mtblx_writer_block_dir", "mtblx_writer_free", "mtblx_free",
     "mtblx_snappy_max_compressed_len", "mtblx_snappy_uncompressed_len", "mtblx_snappy_decompress",
@@ -81,6 +81,9 @@ def lib() -> C.CDLL:
         for f in (L.mtblx_decode_blocks, L.mtblx_count_blocks, L.mtblx_decode_counted):
             f.argtypes = [C.POINTER(BlockBatch), C.POINTER(Decoded), C.c_void_p, C.c_size_t, C.c_void_p]
             f.restype = C.c_int
+        L.mtblx_decode_blocks_verify.argtypes = [C.POINTER(BlockBatch), C.POINTER(Decoded), C.c_void_p, C.c_void_p,
+                                                 C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.mtblx_decode_blocks_verify.restype = C.c_int
         L.mtblx_crc32c_blocks.argtypes = [C.POINTER(BlockBatch), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.mtblx_crc32c_blocks.restype = C.c_int
         L.mtblx_block_dir.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,

@@ -173,6 +173,40 @@ def decode_into(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=No
         raise RuntimeError(f"mtblx_decode_blocks failed: {rc}")
 
 
+VERIFY_FUSED = 2
+
+
+def decode_verify_into(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, crc=None, bad=None, framed=True,
+                       stream=None, fused=False) -> None:
+    """decode_into + the CRC-32C of every block (mtblx_decode_blocks_verify, f1): crc (int32
+    [nblk]) and/or bad (uint8 [nblk]) device tensors.  fused=True: one launch (checksum from
+    the LDS-staged tiles); default: decode then k_crc32c_blocks."""
+    L = _require_device()
+    b, o = batch.cstruct(), out.cstruct()
+    flags = (1 if framed else 0) | (VERIFY_FUSED if fused else 0)
+    rc = L.mtblx_decode_blocks_verify(C.byref(b), C.byref(o), C.c_void_p(_u(crc)), C.c_void_p(_u(bad)),
+                                      flags, C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
+                                      C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_decode_blocks_verify failed: {rc}")
+
+
+def decode_verify(batch: DeviceBatch, framed: bool = True, stream=None, fused=False):
+    """Size exactly, allocate, decode + checksum in one launch -> (DecodedBlocks, crc, bad)."""
+    _require_device()
+    ws = Workspace(batch.nblk)
+    probe = DecodedBlocks(batch.nblk, 0, 0, 0)
+    count_blocks(batch, probe, ws, stream)
+    torch.cuda.synchronize()
+    nr, kb, vb, _ = probe.totals_host()
+    out = DecodedBlocks(batch.nblk, nr, kb, vb)
+    n = max(batch.nblk, 1)
+    crc = torch.zeros(n, dtype=torch.int32, device=batch.data.device)
+    bad = torch.zeros(n, dtype=torch.uint8, device=batch.data.device)
+    decode_verify_into(batch, out, ws, crc, bad, framed, stream, fused)
+    return out, crc[: batch.nblk], bad[: batch.nblk]
+
+
 def decode_counted(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=None) -> None:
     """Decode using the counts a previous count_blocks(batch, out, ws) left behind."""
     L = _require_device()

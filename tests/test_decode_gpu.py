@@ -231,3 +231,45 @@ def test_crc32c_blocks_vs_oracle(oracle):
     _, bad = codec.crc32c_blocks(batch, framed=True)
     torch.cuda.synchronize()
     assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == [5, 77, 1234, 2999]
+
+
+def test_fused_verify_decode(oracle):
+    """f1 fused: decode + CRC-32C in one launch == the plain decode (all outputs) and the
+    oracle's crc32c of every block; the framed check flags exactly the corrupted checksums.
+    Shapes: cfg2 (PipeSmall), builder / quirk / mutated blocks incl. < 4 B and < 64 B blocks,
+    blocks too large for a staging slot (HBM path), 64 KiB blocks (PipeLarge), > 64 KiB
+    blocks (separate-launch fallback)."""
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    rng = np.random.default_rng(77)
+    cases = []
+    data, off, ln = synth.cfg2_file(3000)
+    d2 = data.copy()
+    for b in (0, 7, 1500, 2999):
+        d2[int(off[b]) - 1] ^= 0x08
+    cases.append((d2, off, ln, True, [0, 7, 1500, 2999]))
+    blocks = corpus.builder_blocks(oracle, seed=71, count=120, max_bytes=9000) + \
+        [b for _, b, _ in corpus.quirk_blocks()] + corpus.mutated_blocks(oracle, seed=72, count=150)
+    blocks += [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in (0, 1, 2, 3, 4, 5, 63, 64, 65, 127, 128)]
+    for n in (400, 700):   # > the PipeSmall slot of this batch's mix: unstaged, CRC from HBM
+        blocks.append(oracle.build_block(corpus.random_records(rng, n, 4, 60, 10, 120)))
+    d, o, l = corpus.pack(blocks, rng=rng, lead=3)
+    cases.append((d, o, l, False, []))
+    d, o, l = synth.cfg2_file(200, block_size=65536)
+    cases.append((d, o, l, True, []))
+    big = [oracle.build_block(corpus.random_records(rng, 1400, 8, 60, 40, 60)) for _ in range(3)]
+    assert max(len(b) for b in big) > 70000
+    d, o, l = corpus.pack(big, rng=rng)
+    cases.append((d, o, l, False, []))
+    for (d_, o_, l_, framed, bad_exp), fused in [(c, f) for c in cases for f in (True, False)]:
+        batch = codec.DeviceBatch.from_host(d_, o_, l_)
+        out, crc, bad = codec.decode_verify(batch, framed=framed, fused=fused)
+        torch.cuda.synchronize()
+        dev = out.to_host()
+        orc = oracle.decode_blocks(d_, o_, l_)
+        assert_same(dev, orc, o_.size) if (orc.status != 5).all() else None
+        got = crc.cpu().numpy().view(np.uint32)
+        exp = np.array([oracle.crc32c(bytes(d_[int(a): int(a) + int(n)])) for a, n in zip(o_, l_)], np.uint32)
+        assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+        assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == (bad_exp if framed else [])

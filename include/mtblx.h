@@ -210,6 +210,33 @@ int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk_rec, uint3
                         int framed, uint8_t* out, uint64_t out_cap, uint64_t* blk_off, uint32_t* blk_len,
                         int32_t* status, uint64_t* totals, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- snappy raw decompression on the device (f4) ----
+ * Reader::block's decompression step for CompressionType::Snappy (src/reader.rs:166-170 ->
+ * src/compression.rs:57-68, :116-119, snap::raw::Decoder::decompress_vec), for a batch of
+ * blocks at once.  Block b's STORED bytes are src[src_off[b] .. + src_len[b]) (device).
+ * Status codes are mtblx_host.h's MTBLX_SNAPPY_*: OK, CORRUPT (snap errors -> Err(Error::Io)),
+ * TOO_SMALL (the preamble length exceeds dst_len[b]).
+ *
+ * mtblx_snappy_dir: the output layout from the preambles: dst_len[b] = the stored
+ * uncompressed length (0 if the preamble is corrupt, status[b] = CORRUPT), dst_off[b] = the
+ * exclusive prefix of dst_len rounded up to 16 bytes; totals (device [3]) = bytes of the
+ * layout, max dst_len, corrupt preambles.  workspace: mtblx_snappy_workspace_bytes(nblk)
+ * bytes of device memory (no fill needed).
+ *
+ * mtblx_snappy_decompress_dev: decompresses block b into dst[dst_off[b] .. + its length)
+ * (dst_len[b] = capacity); status[b]; dec_len[b] (device [nblk], may be NULL) = the
+ * decompressed length, or 0 if the block failed -- i.e. {dst, dst_off, dec_len} is directly
+ * the mtblx_block_batch directory of the decompressed blocks.  max_dst_len: host hint (max
+ * of dst_len; 0 = unknown) selecting the kernel variant.  Both calls are asynchronous on
+ * `stream`. */
+size_t mtblx_snappy_workspace_bytes(uint32_t nblk);
+int mtblx_snappy_dir(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint32_t nblk,
+                     uint64_t* dst_off, uint32_t* dst_len, int32_t* status, uint64_t* totals, void* workspace,
+                     size_t workspace_bytes, void* stream);
+int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint32_t nblk,
+                                uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_len, uint32_t max_dst_len,
+                                int32_t* status, uint32_t* dec_len, void* stream);
+
 /* ---- end-to-end decode from host memory (the PCIe-inclusive path of the north star) ----
  * An mtbl file in host memory in (mmap'd or read), the caller's host byte slices out:
  * for every data block, Reader::block's decompression (src/reader.rs:166-170, host: the

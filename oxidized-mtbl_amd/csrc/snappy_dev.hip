@@ -1,0 +1,436 @@
+// snappy_dev.hip — snappy raw decompression of mtbl data blocks on the device (SURVEY.md
+// §8(f) f4).
+//
+// Reference path it replaces: Reader::block decompresses every data block after its checksum
+// (/root/reference/src/reader.rs:166-170) via decompress -> snappy_decompress
+// (src/compression.rs:57-68, :116-119: snap::raw::Decoder::decompress_vec, crate snap 1.x,
+// which is not in /root/reference).  Decompression is format-defined (snappy
+// format_description.txt), so the checks below are the host codec's (csrc/snappy_host.cpp)
+// and the oracle's (oracle/mtbl_oracle.c oracle_snappy_decompress):
+//   preamble  varint32 uncompressed length (unterminated in 5 bytes or > u32: corrupt)
+//   literal   tag&3 == 0: len-1 = tag>>2 (< 60) or the next 1..4 LE bytes; the bytes follow
+//   copy-1    tag&3 == 1: len = 4 + ((tag>>2)&7), offset = (tag>>5)<<8 | next byte
+//   copy-2/4  tag&3 == 2/3: len = 1 + (tag>>2), offset = next 2/4 LE bytes
+//   a copy's offset is 1 .. bytes produced so far; nothing may run past the input or the
+//   stated length; the output must be exactly the stated length.
+//
+// Design (one wave per block; blocks are independent, so no cross-wave state):
+//  - the block's stored bytes are staged through an LDS window (coalesced 16-byte loads);
+//    the output is assembled in LDS (Small: <= 4.5 KiB out, 16 waves per CU; Large: <= 65 KiB
+//    out, 2 waves per CU) and streamed to HBM with 16-byte stores; larger outputs are
+//    assembled in place in HBM;
+//  - the tag stream is a serial chain, parsed with wave-uniform (scalar) arithmetic from LDS;
+//    parsed elements are parked one per lane (up to 64);
+//  - a RUN is a sequence of elements whose copy sources all lie before the run's first output
+//    byte: its bytes are independent, so the wave writes them all at once (lane = output byte,
+//    element found by a 6-step binary search over the parked starts).  A copy that reads bytes
+//    of the current run (short offsets, overlapping copies) closes the run first.  A run that
+//    is a single literal is copied 4 bytes per lane (aligned dword stores).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mtblx.h"
+#include "mtblx_host.h"
+
+namespace mtblx_snap {
+
+constexpr int kWave = 64;
+// No stream of n bytes decodes to more than 64/3 * n bytes (a 3-byte copy-2 yields at most 64),
+// so a longer preamble length can never be met: snap fails on it (Err(Io)) after allocating;
+// here it is CORRUPT up front, which also bounds the layout a corrupt preamble can ask for.
+constexpr uint64_t kMaxExpand = 22;
+
+template <int W_, int OUT_, int WAVES_>
+struct Cfg {
+  static constexpr int W = W_, OUT = OUT_, WAVES = WAVES_;
+};
+using Small = Cfg<4608, 4608, 4>;   // 4 x 9.25 KiB per workgroup, 4 workgroups per CU
+using Large = Cfg<8192, 66560, 1>;  // 73 KiB per workgroup, 2 workgroups per CU
+
+template <class C>
+struct alignas(16) WaveLds {
+  uint8_t win[C::W + 16];   // stored bytes of the block at positions [wstart, wstart + W); 16 B slack
+  uint8_t out[C::OUT + 16];
+};
+
+__device__ __forceinline__ void lds_fence() { __asm__ volatile("" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+template <class C>
+__device__ __forceinline__ void snap_block(WaveLds<C>& S, const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ dg,
+                           uint32_t cap, int lane, int32_t* st_out, uint32_t* dec_len) {
+  // ---- LDS window over the stored bytes ----
+  int32_t wstart = 0;   // block position of window byte 0 (16-byte aligned in memory; may be < 0)
+  uint32_t whi = 0;     // window holds block positions [max(wstart, 0), whi)
+  auto restage = [&](uint32_t p0) {
+    const uint32_t r = (uint32_t)(((uintptr_t)s + p0) & 15u);
+    wstart = (int32_t)p0 - (int32_t)r;
+    const int32_t e = wstart + C::W;
+    whi = (e > (int32_t)n) ? n : (uint32_t)e;
+    const uint32_t nch = (uint32_t)((int32_t)whi - wstart + 15) / 16u;
+    lds_fence();
+    for (uint32_t c = (uint32_t)lane; c < nch; c += kWave) {
+      const int32_t bp = wstart + 16 * (int32_t)c;
+      uint4 v;
+      if (bp >= 0 && bp + 16 <= (int32_t)n) {
+        v = *reinterpret_cast<const uint4*>(s + bp);
+      } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16; ++k) {
+          const int32_t q = bp + k;
+          if (q >= 0 && q < (int32_t)n) w[k >> 2] |= (uint32_t)s[q] << (8 * (k & 3));
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *reinterpret_cast<uint4*>(S.win + 16 * c) = v;
+    }
+    lds_fence();
+  };
+  const uint32_t* w32 = reinterpret_cast<const uint32_t*>(S.win);
+  // 8 bytes at block position p (p in the window), wave-uniform
+  auto hdr8 = [&](uint32_t p, uint32_t& lo, uint32_t& hi) {
+    const uint32_t wi = (uint32_t)((int32_t)p - wstart), q = wi >> 2, sh = (wi & 3u) * 8u;
+    const uint32_t a = ufl(w32[q]), b = ufl(w32[q + 1]), c = ufl(w32[q + 2]);
+    lo = __builtin_amdgcn_alignbit(b, a, sh);
+    hi = __builtin_amdgcn_alignbit(c, b, sh);
+  };
+
+  restage(0);
+  // ---- preamble: varint32 uncompressed length ----
+  uint32_t lo, hi;
+  hdr8(0, lo, hi);
+  uint64_t want = 0;
+  uint32_t pos = 0;
+  bool term = false;
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+    const uint32_t byte = (i < 4 ? lo >> (8 * i) : hi) & 0xffu;
+    want |= (uint64_t)(byte & 0x7fu) << (7 * i);
+    if (!(byte & 0x80u)) {
+      term = true;
+      pos = i + 1;
+      break;
+    }
+  }
+  int32_t st = MTBLX_SNAPPY_OK;
+  if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
+  else if (want > cap) st = MTBLX_SNAPPY_TOO_SMALL;
+  const uint32_t W = (uint32_t)want;
+  const bool glob = W > (uint32_t)C::OUT;   // assemble in place in HBM
+
+  // ---- element runs ----
+  uint32_t e_d = 0xFFFFFFFFu, e_len = 0, e_x = 0;   // lane k: parked element k (start, len | lit<<31, x)
+  uint32_t ne = 0, D = 0, d = 0;                    // parked count, run start, output position
+  // every byte of the run [D, d): lane = output byte, element by binary search over the starts
+  auto run_bytes = [&](auto* out) {
+    const uint32_t T = d - D;
+    for (uint32_t base = 0; base < T; base += kWave) {
+      const uint32_t i = min(base + (uint32_t)lane, T - 1u), p = D + i;
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t stp = 32; stp; stp >>= 1) {
+        const uint32_t kk = k + stp;
+        if ((uint32_t)__shfl((int)e_d, (int)kk, kWave) <= p) k = kk;   // lanes >= ne hold ~0
+      }
+      const uint32_t ed = (uint32_t)__shfl((int)e_d, (int)k, kWave);
+      const uint32_t el = (uint32_t)__shfl((int)e_len, (int)k, kWave);
+      const uint32_t ex = (uint32_t)__shfl((int)e_x, (int)k, kWave);
+      const uint32_t r = p - ed;
+      uint8_t v;
+      if (el >> 31) {
+        v = S.win[ex + r];
+      } else {
+        const uint32_t rr = ex >= (el & 0x7FFFFFFFu) ? r : r % ex;   // overlapping copy: period `off`
+        v = out[ed - ex + rr];
+      }
+      if (base + (uint32_t)lane < T) out[p] = v;
+    }
+  };
+  auto flush = [&]() {
+    if (ne == 0) return;
+    const uint32_t T = d - D;
+    lds_fence();
+    if (glob) {
+      run_bytes(dg);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this run's HBM bytes before the next run's reads
+    } else if (ne == 1 && (ufl(e_len) >> 31)) {
+      // one literal: 4 bytes per lane, aligned dword stores into the output
+      const uint32_t ex = ufl(e_x);
+      const uint32_t h = min((4u - (D & 3u)) & 3u, T);
+      if ((uint32_t)lane < h) S.out[D + lane] = S.win[ex + lane];
+      const uint32_t nd = (T - h) / 4u, sp0 = ex + h, sh = (sp0 & 3u) * 8u;
+      uint32_t* o32 = reinterpret_cast<uint32_t*>(S.out + D + h);
+      for (uint32_t j = (uint32_t)lane; j < nd; j += kWave) {
+        const uint32_t q = (sp0 >> 2) + j;
+        o32[j] = __builtin_amdgcn_alignbit(w32[q + 1], w32[q], sh);
+      }
+      const uint32_t t0 = h + 4u * nd;
+      if ((uint32_t)lane < T - t0) S.out[D + t0 + lane] = S.win[ex + t0 + lane];
+    } else {
+      run_bytes(S.out);
+    }
+    lds_fence();
+    ne = 0;
+    D = d;
+    e_d = 0xFFFFFFFFu;
+  };
+  auto park = [&](uint32_t len, uint32_t lit, uint32_t x) {
+    if ((uint32_t)lane == ne) {
+      e_d = d;
+      e_len = len | (lit << 31);
+      e_x = x;
+    }
+    ++ne;
+    d += len;
+    if (ne == (uint32_t)kWave) flush();
+  };
+
+  while (st == MTBLX_SNAPPY_OK && pos < n) {
+    const uint32_t need = min(pos + 5u, n);
+    if (need > whi) {
+      flush();
+      restage(pos);
+    }
+    hdr8(pos, lo, hi);
+    const uint32_t tag = lo & 0xffu, kind = tag & 3u;
+    const uint32_t avail = n - pos - 1u;   // stored bytes after the tag
+    if (kind == 0) {
+      uint64_t len = (tag >> 2) + 1u;
+      uint32_t hl = 1;
+      if (len > 60) {
+        const uint32_t nb = (uint32_t)len - 60u;
+        if (avail < nb) { st = MTBLX_SNAPPY_CORRUPT; break; }
+        const uint64_t raw = ((uint64_t)hi << 32 | lo) >> 8;
+        len = (raw & ((1ull << (8 * nb)) - 1ull)) + 1ull;
+        hl += nb;
+      }
+      const uint32_t src = pos + hl;
+      if ((uint64_t)(n - src) < len || (uint64_t)(W - d) < len) { st = MTBLX_SNAPPY_CORRUPT; break; }
+      const uint32_t L = (uint32_t)len;
+      if (src + L > whi) {   // literal bytes not in the window
+        flush();
+        if (L <= (uint32_t)C::W - 32u) {
+          restage(src);
+        } else {   // longer than a window: piece by piece, each a one-literal run
+          for (uint32_t o = 0; o < L; o += (uint32_t)C::W - 32u) {
+            const uint32_t piece = min((uint32_t)C::W - 32u, L - o);
+            restage(src + o);
+            park(piece, 1u, (uint32_t)((int32_t)(src + o) - wstart));
+            flush();
+          }
+          pos = src + L;
+          continue;
+        }
+      }
+      park(L, 1u, (uint32_t)((int32_t)src - wstart));
+      pos = src + L;
+      continue;
+    }
+    uint32_t len, off, hl;
+    if (kind == 1) {
+      if (avail < 1) { st = MTBLX_SNAPPY_CORRUPT; break; }
+      len = 4u + ((tag >> 2) & 7u);
+      off = ((tag >> 5) << 8) | ((lo >> 8) & 0xffu);
+      hl = 2;
+    } else if (kind == 2) {
+      if (avail < 2) { st = MTBLX_SNAPPY_CORRUPT; break; }
+      len = 1u + (tag >> 2);
+      off = (lo >> 8) & 0xffffu;
+      hl = 3;
+    } else {
+      if (avail < 4) { st = MTBLX_SNAPPY_CORRUPT; break; }
+      len = 1u + (tag >> 2);
+      off = (lo >> 8) | (hi << 24);
+      hl = 5;
+    }
+    if (off == 0 || off > d || W - d < len) { st = MTBLX_SNAPPY_CORRUPT; break; }
+    // its source must precede the run (the first bytes of the pattern for an overlapping copy)
+    if (d - off + min(len, off) > D) flush();
+    park(len, 0u, off);
+    pos += hl;
+  }
+  if (st == MTBLX_SNAPPY_OK) {
+    flush();
+    if (d != W) st = MTBLX_SNAPPY_CORRUPT;
+  }
+  // ---- LDS output -> HBM ----
+  if (st == MTBLX_SNAPPY_OK && !glob) {
+    lds_fence();
+    if (((uintptr_t)dg & 15u) == 0) {
+      const uint32_t n16 = W / 16u;
+      for (uint32_t j = (uint32_t)lane; j < n16; j += kWave)
+        reinterpret_cast<uint4*>(dg)[j] = reinterpret_cast<const uint4*>(S.out)[j];
+      if ((uint32_t)lane < W - 16u * n16) dg[16u * n16 + lane] = S.out[16u * n16 + lane];
+    } else {
+      for (uint32_t j = (uint32_t)lane; j < W; j += kWave) dg[j] = S.out[j];
+    }
+  }
+  if (lane == 0) {
+    st_out[0] = st;
+    if (dec_len) dec_len[0] = st == MTBLX_SNAPPY_OK ? W : 0u;
+  }
+  lds_fence();
+}
+
+template <class C>
+__global__ void __launch_bounds__(C::WAVES * kWave) k_snappy_blocks(const uint8_t* src, const uint64_t* src_off,
+                                                                     const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                                     const uint64_t* dst_off, const uint32_t* dst_len,
+                                                                     int32_t* status, uint32_t* dec_len) {
+  __shared__ WaveLds<C> S[C::WAVES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * C::WAVES;
+  for (uint32_t b = blockIdx.x * C::WAVES + wv; b < nblk; b += nw)
+    snap_block<C>(S[wv], src + src_off[b], src_len[b], dst + dst_off[b], dst_len[b], lane, status + b,
+                  dec_len ? dec_len + b : nullptr);
+}
+
+// ---- directory: preamble lengths, 16-byte aligned exclusive prefix ----
+constexpr int kDirThreads = 256, kDirPer = 8, kDirSpan = kDirThreads * kDirPer;
+
+__device__ __forceinline__ uint32_t preamble(const uint8_t* s, uint32_t n, bool& ok) {
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+    const uint32_t byte = s[i];
+    v |= (uint64_t)(byte & 0x7fu) << (7 * i);
+    if (!(byte & 0x80u)) {
+      ok = v <= 0xFFFFFFFFull && v <= kMaxExpand * (uint64_t)n;
+      return ok ? (uint32_t)v : 0u;
+    }
+  }
+  ok = false;
+  return 0;
+}
+
+__device__ __forceinline__ uint64_t pad16(uint32_t x) { return ((uint64_t)x + 15u) & ~15ull; }
+
+// per-thread sums -> workgroup exclusive scan (in `sh`), returns the thread's exclusive base
+__device__ uint64_t wg_excl_scan(uint64_t v, uint64_t* sh, uint64_t& total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < kDirThreads; o <<= 1) {
+    const uint64_t a = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += a;
+    __syncthreads();
+  }
+  total = sh[kDirThreads - 1];
+  const uint64_t r = sh[t] - v;
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(kDirThreads) k_snap_len(const uint8_t* src, const uint64_t* src_off,
+                                                          const uint32_t* src_len, uint32_t nblk, uint32_t* dst_len,
+                                                          int32_t* status, uint64_t* wsum, uint64_t* totals) {
+  __shared__ uint64_t sh[kDirThreads];
+  const uint32_t b0 = blockIdx.x * kDirSpan + threadIdx.x * kDirPer;
+  uint64_t sum = 0;
+  uint32_t mx = 0, bad = 0;
+  for (int j = 0; j < kDirPer; ++j) {
+    const uint32_t b = b0 + j;
+    if (b >= nblk) break;
+    bool ok = false;
+    const uint32_t u = preamble(src + src_off[b], src_len[b], ok);
+    dst_len[b] = u;
+    status[b] = ok ? MTBLX_SNAPPY_OK : MTBLX_SNAPPY_CORRUPT;
+    sum += pad16(u);
+    mx = max(mx, u);
+    bad += ok ? 0u : 1u;
+  }
+  uint64_t tot = 0;
+  (void)wg_excl_scan(sum, sh, tot);
+  if (threadIdx.x == 0) wsum[blockIdx.x] = tot;
+  if (mx) atomicMax(reinterpret_cast<unsigned long long*>(totals + 1), (unsigned long long)mx);
+  if (bad) atomicAdd(reinterpret_cast<unsigned long long*>(totals + 2), (unsigned long long)bad);
+}
+
+__global__ void __launch_bounds__(kDirThreads) k_snap_scan(uint64_t* wsum, uint32_t nwg, uint64_t* totals) {
+  __shared__ uint64_t sh[kDirThreads];
+  uint64_t carry = 0;
+  for (uint32_t c = 0; c < nwg; c += kDirThreads) {
+    const uint32_t i = c + threadIdx.x;
+    const uint64_t v = i < nwg ? wsum[i] : 0;
+    uint64_t tot = 0;
+    const uint64_t e = wg_excl_scan(v, sh, tot);
+    if (i < nwg) wsum[i] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) totals[0] = carry;
+}
+
+__global__ void __launch_bounds__(kDirThreads) k_snap_off(const uint32_t* dst_len, uint32_t nblk, const uint64_t* wsum,
+                                                          uint64_t* dst_off) {
+  __shared__ uint64_t sh[kDirThreads];
+  const uint32_t b0 = blockIdx.x * kDirSpan + threadIdx.x * kDirPer;
+  uint64_t sum = 0;
+  uint32_t u[kDirPer];
+  for (int j = 0; j < kDirPer; ++j) {
+    u[j] = b0 + j < nblk ? dst_len[b0 + j] : 0u;
+    sum += pad16(u[j]);
+  }
+  uint64_t tot = 0;
+  uint64_t base = wg_excl_scan(sum, sh, tot) + wsum[blockIdx.x];
+  for (int j = 0; j < kDirPer; ++j) {
+    if (b0 + j >= nblk) break;
+    dst_off[b0 + j] = base;
+    base += pad16(u[j]);
+  }
+}
+
+int grid_for(int per_cu, uint32_t units) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const uint32_t g = (uint32_t)(ncu * per_cu);
+  return (int)(units < g ? (units ? units : 1u) : g);
+}
+
+}  // namespace mtblx_snap
+
+using namespace mtblx_snap;
+
+extern "C" size_t mtblx_snappy_workspace_bytes(uint32_t nblk) {
+  return 8u * ((size_t)(nblk + kDirSpan - 1) / kDirSpan + 1);
+}
+
+extern "C" int mtblx_snappy_dir(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint32_t nblk,
+                                uint64_t* dst_off, uint32_t* dst_len, int32_t* status, uint64_t* totals,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  if (!totals || (nblk && (!src || !src_off || !src_len || !dst_off || !dst_len || !status || !workspace)))
+    return MTBLX_E_INVAL;
+  if (workspace_bytes < mtblx_snappy_workspace_bytes(nblk)) return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(totals, 0, 3 * sizeof(uint64_t), s) != hipSuccess) return MTBLX_E_HIP;
+  if (nblk == 0) return MTBLX_OK;
+  const uint32_t nwg = (nblk + kDirSpan - 1) / kDirSpan;
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(workspace);
+  hipLaunchKernelGGL(k_snap_len, dim3(nwg), dim3(kDirThreads), 0, s, src, src_off, src_len, nblk, dst_len, status,
+                     wsum, totals);
+  hipLaunchKernelGGL(k_snap_scan, dim3(1), dim3(kDirThreads), 0, s, wsum, nwg, totals);
+  hipLaunchKernelGGL(k_snap_off, dim3(nwg), dim3(kDirThreads), 0, s, dst_len, nblk, wsum, dst_off);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                                           uint32_t nblk, uint8_t* dst, const uint64_t* dst_off,
+                                           const uint32_t* dst_len, uint32_t max_dst_len, int32_t* status,
+                                           uint32_t* dec_len, void* stream) {
+  if (nblk == 0) return MTBLX_OK;
+  if (!src || !src_off || !src_len || !dst || !dst_off || !dst_len || !status) return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (max_dst_len != 0 && max_dst_len <= (uint32_t)Small::OUT) {
+    hipLaunchKernelGGL(k_snappy_blocks<Small>, dim3(grid_for(4, (nblk + Small::WAVES - 1) / Small::WAVES)),
+                       dim3(Small::WAVES * kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, status,
+                       dec_len);
+  } else {
+    hipLaunchKernelGGL(k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,
+                       src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
+  }
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}

@@ -33,6 +33,7 @@ EXPORTS = [
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
     "mtblx_pipe_decode", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
+    "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
@@ -140,6 +141,15 @@ def lib() -> C.CDLL:
                                           C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_size_t, C.c_void_p]
         L.mtblx_encode_blocks.restype = C.c_int
+        L.mtblx_snappy_workspace_bytes.argtypes = [C.c_uint32]
+        L.mtblx_snappy_workspace_bytes.restype = C.c_size_t
+        L.mtblx_snappy_dir.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.mtblx_snappy_dir.restype = C.c_int
+        L.mtblx_snappy_decompress_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                                  C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                                  C.c_void_p]
+        L.mtblx_snappy_decompress_dev.restype = C.c_int
         L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]
         L.mtblx_host_alloc.restype = C.c_int
         L.mtblx_host_free.argtypes = [C.c_void_p]

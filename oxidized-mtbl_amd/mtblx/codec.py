@@ -245,3 +245,78 @@ def crc32c_blocks(batch: DeviceBatch, framed: bool = False, stream=None):
     if rc != 0:
         raise RuntimeError(f"mtblx_crc32c_blocks failed: {rc}")
     return crc[: batch.nblk], (bad[: batch.nblk] if framed else None)
+
+
+# ---------------- snappy raw decompression on the device (f4) ----------------
+class SnappyBatch:
+    """Snappy-compressed (stored) block bytes resident in HBM: block b = data[src_off[b] .. + src_len[b])."""
+
+    def __init__(self, data: torch.Tensor, src_off: torch.Tensor, src_len: torch.Tensor):
+        self.data, self.src_off, self.src_len = data, src_off, src_len
+
+    @property
+    def nblk(self) -> int:
+        return int(self.src_off.numel())
+
+    @staticmethod
+    def from_host(data: np.ndarray, src_off: np.ndarray, src_len: np.ndarray, device="cuda") -> "SnappyBatch":
+        d = torch.from_numpy(np.ascontiguousarray(data, np.uint8)).to(device)
+        o = torch.from_numpy(np.ascontiguousarray(src_off, np.uint64).view(np.int64)).to(device)
+        n = torch.from_numpy(np.ascontiguousarray(src_len, np.uint32).view(np.int32)).to(device)
+        return SnappyBatch(d, o, n)
+
+
+class SnappyLayout:
+    """Output layout of a SnappyBatch (mtblx_snappy_dir): dst_off (16-byte aligned), dst_len,
+    per-block status (MTBLX_SNAPPY_*) and totals (layout bytes, max length, corrupt preambles)."""
+
+    def __init__(self, nblk: int, device="cuda"):
+        n = max(nblk, 1)
+        self.nblk = nblk
+        self.dst_off = torch.zeros(n, dtype=torch.int64, device=device)
+        self.dst_len = torch.zeros(n, dtype=torch.int32, device=device)
+        self.status = torch.zeros(n, dtype=torch.int32, device=device)
+        self.totals = torch.zeros(3, dtype=torch.int64, device=device)
+        L = _lib.lib()
+        self.ws_bytes = int(L.mtblx_snappy_workspace_bytes(nblk))
+        self.ws = torch.empty(max(self.ws_bytes, 8), dtype=torch.uint8, device=device)
+
+
+def snappy_dir(batch: SnappyBatch, layout: SnappyLayout, stream=None) -> None:
+    L = _require_device()
+    rc = L.mtblx_snappy_dir(C.c_void_p(_u(batch.data)), C.c_void_p(_u(batch.src_off)), C.c_void_p(_u(batch.src_len)),
+                            batch.nblk, C.c_void_p(_u(layout.dst_off)), C.c_void_p(_u(layout.dst_len)),
+                            C.c_void_p(_u(layout.status)), C.c_void_p(_u(layout.totals)),
+                            C.c_void_p(_u(layout.ws)), layout.ws_bytes, C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_snappy_dir failed: {rc}")
+
+
+def snappy_decompress_into(batch: SnappyBatch, layout: SnappyLayout, dst: torch.Tensor, status: torch.Tensor,
+                           dec_len: torch.Tensor | None, max_len: int, stream=None) -> None:
+    """Asynchronous device decompression of every block into dst at layout.dst_off."""
+    L = _require_device()
+    rc = L.mtblx_snappy_decompress_dev(C.c_void_p(_u(batch.data)), C.c_void_p(_u(batch.src_off)),
+                                       C.c_void_p(_u(batch.src_len)), batch.nblk, C.c_void_p(_u(dst)),
+                                       C.c_void_p(_u(layout.dst_off)), C.c_void_p(_u(layout.dst_len)), int(max_len),
+                                       C.c_void_p(_u(status)), C.c_void_p(_u(dec_len)),
+                                       C.c_void_p(_stream_handle(stream)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_snappy_decompress_dev failed: {rc}")
+
+
+def snappy_decompress(batch: SnappyBatch, stream=None):
+    """Layout + decompress -> (DeviceBatch of the decompressed blocks, status int32 [nblk]).
+    The DeviceBatch feeds decode_blocks directly (a failed block has length 0)."""
+    _require_device()
+    lay = SnappyLayout(batch.nblk, batch.data.device)
+    snappy_dir(batch, lay, stream)
+    torch.cuda.synchronize()
+    t = lay.totals.cpu().numpy().view(np.uint64)
+    total, mx = int(t[0]), int(t[1])
+    dst = torch.zeros(max(total, 16), dtype=torch.uint8, device=batch.data.device)
+    status = torch.zeros(max(batch.nblk, 1), dtype=torch.int32, device=batch.data.device)
+    dec_len = torch.zeros(max(batch.nblk, 1), dtype=torch.int32, device=batch.data.device)
+    snappy_decompress_into(batch, lay, dst, status, dec_len, mx, stream)
+    out = DeviceBatch(dst, lay.dst_off[: batch.nblk], dec_len[: batch.nblk], mx)
+    return out, status[: batch.nblk]

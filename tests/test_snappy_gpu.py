@@ -1,0 +1,189 @@
+"""Device snappy raw decompression (f4, include/mtblx.h mtblx_snappy_dir /
+mtblx_snappy_decompress_dev) against the oracle's independent byte-at-a-time restatement
+(oracle/mtbl_oracle.c oracle_snappy_decompress; Reader::block -> src/compression.rs:116-119).
+
+Streams come from the product compressor and, where this image has it, libsnappy 1.1.8 (a
+different encoder: different element mixes).  Compressed bytes are parity-unpinned (SURVEY.md
+§8c); decoded bytes and the error/ok verdict per block are compared.  Shapes cover both kernel
+variants (<= 4.5 KiB outputs: Small; larger: Large, with outputs above 65 KiB assembled in HBM),
+overlapping copies (period 1..4), literals longer than a staging window, empty streams and
+mutated streams.
+"""
+import numpy as np
+import pytest
+
+import corpus
+from test_snappy import _inputs, _libsnappy
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mtblx import codec
+    return codec
+
+
+def _streams(xs, lib=None):
+    from mtblx import pipe
+    out = []
+    for x in xs:
+        out.append(pipe.snappy_compress(x))
+        if lib is not None:
+            import ctypes as C
+            cap = lib.snappy_max_compressed_length(len(x))
+            buf = C.create_string_buffer(cap)
+            n = C.c_size_t(cap)
+            assert lib.snappy_compress(x, len(x), buf, C.byref(n)) == 0
+            out.append(buf.raw[: n.value])
+    return out
+
+
+def _device(codec, streams, rng, lead=0):
+    data, off, ln = corpus.pack(streams, rng=rng, lead=lead)
+    batch = codec.SnappyBatch.from_host(data, off, ln)
+    dec, st = codec.snappy_decompress(batch)
+    import torch
+    torch.cuda.synchronize()
+    host = dec.data.cpu().numpy()
+    o = dec.blk_off.cpu().numpy().view(np.uint64)
+    n = dec.blk_len.cpu().numpy().view(np.uint32)
+    got = [bytes(host[int(a): int(a) + int(b)]) for a, b in zip(o, n)]
+    return got, st.cpu().numpy(), o
+
+
+def _check(oracle, streams, got, st):
+    for i, z in enumerate(streams):
+        exp = oracle.snappy_decompress(z)
+        if exp is None:
+            assert st[i] == 1, i
+        else:
+            assert st[i] == 0, (i, st[i])
+            assert got[i] == exp, i
+
+
+def _compressible(rng):
+    xs = [b"", b"x", b"ab" * 2000, b"\0" * 4500, bytes(range(256)) * 17, b"abc" * 1500, b"abcd" * 16_000]
+    xs += [b"".join(rng.choice([b"alpha", b"beta", b"gamma", b"delta"], 2000).tolist())]
+    from mtblx import synth
+    xs += [b"".join(v for _, v in synth.cfg1_records(400))]
+    recs = corpus.random_records(rng, 300, 0, 40, 0, 20)
+    xs.append(b"".join(k + v for k, v in recs))
+    return xs
+
+
+def test_small_blocks_vs_oracle(oracle):
+    """every output <= 4.5 KiB: the Small variant (16 waves per CU, LDS output)"""
+    codec = _dev()
+    rng = np.random.default_rng(1)
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(300)
+    xs = [bytes(data[int(a): int(a) + int(n)]) for a, n in zip(off, ln)]
+    xs += [x for x in _compressible(rng) if len(x) <= 4608]
+    xs += [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in (1, 2, 3, 15, 16, 17, 59, 60, 61, 4608)]
+    streams = _streams(xs, _libsnappy())
+    got, st, o = _device(codec, streams, rng, lead=3)
+    _check(oracle, streams, got, st)
+    assert (o % 16 == 0).all()
+
+
+def test_mixed_and_large_blocks_vs_oracle(oracle):
+    """outputs up to 200 KB: the Large variant, in-HBM assembly above 65 KiB, long literals
+    crossing staging windows, overlapping copies"""
+    codec = _dev()
+    rng = np.random.default_rng(2)
+    xs = _inputs() + _compressible(rng)
+    xs += [rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes(), b"q" * 66_000, b"xy" * 40_000]
+    streams = _streams(xs, _libsnappy())
+    got, st, _ = _device(codec, streams, rng, lead=1)
+    _check(oracle, streams, got, st)
+
+
+def test_corrupt_streams_vs_oracle(oracle):
+    """mutated streams (bit flips, truncations, preamble rewrites, random bytes): the device
+    flags exactly the streams the oracle rejects and decodes the rest identically"""
+    codec = _dev()
+    from mtblx import pipe
+    rng = np.random.default_rng(11)
+    base = [pipe.snappy_compress(x) for x in _inputs() + _compressible(rng) if len(x) < 70_000]
+    streams = []
+    for i in range(3000):
+        z = bytearray(base[i % len(base)])
+        if not z:
+            streams.append(bytes(z))
+            continue
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            z[int(rng.integers(0, len(z)))] ^= 1 << int(rng.integers(0, 8))
+        elif k == 1:
+            z = z[: int(rng.integers(0, len(z)))]
+        elif k == 2:
+            z[0] = int(rng.integers(0, 256))
+        else:
+            z[int(rng.integers(0, len(z)))] = int(rng.integers(0, 256))
+        streams.append(bytes(z))
+    got, st, _ = _device(codec, streams, rng)
+    _check(oracle, streams, got, st)
+    assert (st == 1).sum() > 300 and (st == 0).sum() > 300
+
+
+def test_too_small_capacity():
+    """a block whose preamble length exceeds its dst_len capacity -> MTBLX_SNAPPY_TOO_SMALL"""
+    codec = _dev()
+    import torch
+    from mtblx import pipe
+    xs = [b"a" * 100, b"b" * 300, b"c" * 50]
+    zs = [pipe.snappy_compress(x) for x in xs]
+    data, off, ln = corpus.pack(zs)
+    batch = codec.SnappyBatch.from_host(data, off, ln)
+    lay = codec.SnappyLayout(3)
+    codec.snappy_dir(batch, lay)
+    torch.cuda.synchronize()
+    assert lay.dst_len.cpu().tolist() == [100, 300, 50]
+    assert lay.dst_off.cpu().tolist() == [0, 112, 416]
+    assert lay.totals.cpu().tolist() == [416 + 64, 300, 0]
+    lay.dst_len[1] = 299
+    dst = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    st = torch.full((3,), -1, dtype=torch.int32, device="cuda")
+    dl = torch.full((3,), -1, dtype=torch.int32, device="cuda")
+    codec.snappy_decompress_into(batch, lay, dst, st, dl, 300)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0, 2, 0] and dl.cpu().tolist() == [100, 0, 50]
+    h = dst.cpu().numpy().tobytes()
+    assert h[:100] == xs[0] and h[416:466] == xs[2]
+
+
+def test_snappy_file_device_decompress_then_decode(oracle):
+    """a CompressionType::Snappy file: device decompression feeds the device decode directly
+    ({dst, dst_off, dec_len} is the decode batch); records == the None file's decode by the
+    oracle, with one corrupted block reported CORRUPT and decoded as empty (INVALID_BLOCK)"""
+    codec = _dev()
+    from mtblx.writer import Writer
+    rng = np.random.default_rng(9)
+    recs = corpus.random_records(rng, 6000, 1, 40, 0, 120)
+    files = {}
+    for comp in (0, 1):
+        w = Writer(4096, 16, comp)
+        for k, v in recs:
+            w.insert(k, v)
+        files[comp] = (np.frombuffer(w.into_inner(), np.uint8).copy(), *w.block_dir)
+    d0, o0, l0 = files[0]
+    d1, o1, l1 = files[1]
+    exp = oracle.decode_blocks(d0, o0, l0)
+    d1 = d1.copy()
+    d1[int(o1[7])] ^= 0x01   # preamble length off by one -> snap error
+    batch = codec.SnappyBatch.from_host(d1, o1, l1)
+    dec, st = codec.snappy_decompress(batch)
+    out = codec.decode_blocks(dec)
+    import torch
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert st[7] == 1 and (np.delete(st, 7) == 0).all()
+    h = out.to_host()
+    for b in range(o0.size):
+        if b == 7:
+            assert h.status[b] == 1 and h.nrec[b] == 0
+        else:
+            assert h.status[b] == 0 and h.records(b) == exp.records(b)

@@ -118,15 +118,16 @@ def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
     out = pipe.HostOutputs(off.size, nrec, kbytes, vbytes)
     p = pipe.HostPipe(chunk_bytes=64 << 20, max_blocks=1 << 16, threads=16)
 
-    def run(d, o, l, comp, tag, extra=None):
-        p.decode(d, o, l, out, compression=comp)    # warm-up (first-touch of pinned pages, slots)
+    def run(d, o, l, comp, tag, extra=None, pp=None):
+        pp = pp or p
+        pp.decode(d, o, l, out, compression=comp)    # warm-up (first-touch of pinned pages, slots)
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
         st = None
         h2d = d2h = stage = dec = 0.0
         for _ in range(reps):
-            st = p.decode(d, o, l, out, compression=comp)
+            st = pp.decode(d, o, l, out, compression=comp)
             h2d += st.h2d_bytes
             d2h += st.d2h_bytes
             stage += st.stage_seconds
@@ -202,12 +203,45 @@ def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
     dev_ms = e0.elapsed_time(e1) / 20
     if dout.totals_host()[:3] != (nrec, kbytes, vbytes):
         raise RuntimeError("cfg5: device-resident decode of the decompressed blocks failed")
+    # f4: device snappy decompression of the same stored blocks (device-resident), then the
+    # decode of its output: the same totals
+    zb = codec.SnappyBatch.from_host(zdata, zoff, zln)
+    lay = codec.SnappyLayout(zb.nblk)
+    codec.snappy_dir(zb, lay)
+    torch.cuda.synchronize()
+    zt = lay.totals.cpu().numpy().view(np.uint64)
+    with torch.cuda.stream(s):
+        zdst = torch.zeros(int(zt[0]) + 16, dtype=torch.uint8, device="cuda")
+        zst_d = torch.zeros(zb.nblk, dtype=torch.int32, device="cuda")
+        zdl = torch.zeros(zb.nblk, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dz = lambda: codec.snappy_decompress_into(zb, lay, zdst, zst_d, zdl, int(zt[1]), s)  # noqa: E731
+    for _ in range(3):
+        dz()
+    dz_ms = _timed(dz, s, 20)
+    zbatch = codec.DeviceBatch(zdst, lay.dst_off[: zb.nblk], zdl, int(zt[1]))
+    with torch.cuda.stream(s):
+        zws = codec.Workspace(zbatch.nblk)
+    torch.cuda.synchronize()
+    both = lambda: (dz(), codec.decode_into(zbatch, dout, zws, s))  # noqa: E731
+    for _ in range(3):
+        both()
+    both_ms = _timed(both, s, 20)
+    if dout.totals_host()[:3] != (nrec, kbytes, vbytes) or int((zst_d != 0).sum().item()) != 0:
+        raise RuntimeError("cfg5: device snappy decompression + decode failed")
+    pz = pipe.HostPipe(chunk_bytes=64 << 20, max_blocks=1 << 16, threads=16, device_snappy=True)
     pipe.register(zdata)
     try:
         res["cfg5_snappy"] = run(zdata, zoff, zln, 1, "cfg5", {
             "stored_bytes": int(zln.sum(dtype=np.uint64)),
             "host_decompress_GiB_per_s_16_threads": round(block_bytes / t_dz / 2**30, 2),
             "device_resident_GiB_per_s": round(block_bytes / (dev_ms * 1e-3) / 2**30, 1)})
+        res["cfg5_snappy_device_decompress"] = run(zdata, zoff, zln, 1, "cfg5-dz", {
+            "mode": "MTBLX_PIPE_DEVICE_SNAPPY: stored bytes H2D, k_snappy_blocks + decode on the device",
+            "device_resident_decompress_ms": round(dz_ms, 4),
+            "device_resident_decompress_GiB_per_s": round(block_bytes / (dz_ms * 1e-3) / 2**30, 1),
+            "device_resident_decompress_plus_decode_GiB_per_s": round(block_bytes / (both_ms * 1e-3) / 2**30, 1)},
+            pp=pz)
     finally:
         pipe.unregister(zdata)
     res["note"] = ("pinned host file in -> pinned host outputs (keys, values, u32 end offsets, per-block arrays) out; "

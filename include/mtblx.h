@@ -271,6 +271,11 @@ void mtblx_pipe_free(mtblx_pipe* p);
 int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t file_len, uint32_t compression,
                       const uint64_t* blk_off, const uint32_t* blk_len, uint32_t nblk, const mtblx_decoded* out,
                       mtblx_pipe_stats* stats);
+/* pipe options.  MTBLX_PIPE_DEVICE_SNAPPY (value 1 = on, 0 = off, default off): snappy files
+ * cross PCIe as stored and are decompressed on the device (mtblx_snappy_decompress_dev) right
+ * before the decode; off = host decompression in the staging stage.  Same outputs either way. */
+#define MTBLX_PIPE_DEVICE_SNAPPY 1
+int mtblx_pipe_set(mtblx_pipe* p, int option, int64_t value);
 /* pinned host memory for the pipe's inputs / outputs */
 int mtblx_host_alloc(void** p, uint64_t bytes);
 int mtblx_host_free(void* p);

@@ -17,6 +17,9 @@
 //          decompression for CompressionType::Snappy
 //   s_h2d  directory + bytes, host -> device
 //   s_dec  mtblx_decode_blocks, then the chunk totals -> pinned host
+// With MTBLX_PIPE_DEVICE_SNAPPY a snappy file crosses PCIe as stored (compressed) and is
+// decompressed on the device (mtblx_snappy_decompress_dev, snappy_dev.hip) right before the
+// decode, on s_dec: the host stage is then the same as for an uncompressed file.
 //   s_d2h  rebase of the chunk's per-block bases to file-global ones, then every output ->
 //          the caller's host arrays at the running offsets
 // with kSlots chunks in flight, so the host stage of chunk i+1, the H2D and decode of chunk i
@@ -124,8 +127,11 @@ Caps caps_for(uint64_t in, uint64_t blocks) {
 }
 
 struct Slot {
-  uint8_t* h = nullptr;       // pinned staging: dir (off u64[blocks] | len u32[blocks]) | data
+  uint8_t* h = nullptr;       // pinned staging: dir (off u64[blocks] | len u32[blocks]) | dir2 | data
   uint8_t* d = nullptr;       // device copy of the staging layout
+  uint8_t* du = nullptr;      // device snappy: decompressed blocks (16-byte aligned starts)
+  uint8_t* dz = nullptr;      // device snappy: dec_len u32[blocks] | status i32[blocks]
+  int32_t* hz = nullptr;      // device snappy: pinned copy of the status
   uint8_t* dout = nullptr;    // device outputs
   uint64_t* htot = nullptr;   // pinned chunk totals [4]
   Caps cap;
@@ -133,6 +139,9 @@ struct Slot {
   hipEvent_t e_h2d = nullptr, e_dec0 = nullptr, e_dec = nullptr, e_d2h = nullptr;
   bool busy = false;          // e_d2h pending for a previous chunk
   uint64_t dir_bytes() const { return up256(cap.blocks * 12); }
+  // dir2 (device snappy): decompressed layout dst_off u64[blocks] | dst_len u32[blocks]
+  uint64_t data_at() const { return 2 * dir_bytes(); }
+  uint64_t du_bytes() const { return cap.in + 16 * cap.blocks + 64; }
 };
 
 __global__ void k_rebase(uint64_t* rb, uint64_t* kb, uint64_t* vb, uint32_t n, uint64_t r0, uint64_t k0,
@@ -158,6 +167,7 @@ struct mtblx_pipe {
   uint64_t chunk_bytes = 64ull << 20;
   uint32_t max_blocks = 1u << 16;
   int dev = 0;
+  bool dev_snappy = false;   // MTBLX_PIPE_DEVICE_SNAPPY
   hipStream_t s_h2d = nullptr, s_dec = nullptr, s_d2h = nullptr;
   Slot slot[kSlots];
   void* ws = nullptr;
@@ -210,6 +220,9 @@ void free_slot(Slot& s) {
   if (s.d) (void)hipFree(s.d);
   free_outputs(s);
   if (s.htot) (void)hipHostFree(s.htot);
+  if (s.hz) (void)hipHostFree(s.hz);
+  if (s.du) (void)hipFree(s.du);
+  if (s.dz) (void)hipFree(s.dz);
   for (hipEvent_t* e : {&s.e_h2d, &s.e_dec0, &s.e_dec, &s.e_d2h})
     if (*e) (void)hipEventDestroy(*e);
   s = Slot();
@@ -218,10 +231,14 @@ void free_slot(Slot& s) {
 int alloc_slot(Slot& s, const Caps& c) {
   free_slot(s);
   s.cap = c;
-  const uint64_t inb = s.dir_bytes() + c.in + 64;
+  const uint64_t inb = s.data_at() + c.in + 64;
   if (hipHostMalloc(reinterpret_cast<void**>(&s.h), inb, hipHostMallocDefault) != hipSuccess) return MTBLX_E_HIP;
   if (hipMalloc(reinterpret_cast<void**>(&s.d), inb) != hipSuccess) return MTBLX_E_HIP;
   if (hipHostMalloc(reinterpret_cast<void**>(&s.htot), 32, hipHostMallocDefault) != hipSuccess) return MTBLX_E_HIP;
+  if (hipHostMalloc(reinterpret_cast<void**>(&s.hz), 4 * c.blocks + 4, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&s.du), s.du_bytes()) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&s.dz), 8 * c.blocks + 8) != hipSuccess)
+    return MTBLX_E_HIP;
   if (hipEventCreateWithFlags(&s.e_h2d, hipEventDisableTiming) != hipSuccess) return MTBLX_E_HIP;
   if (hipEventCreateWithFlags(&s.e_d2h, hipEventDisableTiming) != hipSuccess) return MTBLX_E_HIP;
   if (hipEventCreate(&s.e_dec0) != hipSuccess || hipEventCreate(&s.e_dec) != hipSuccess) return MTBLX_E_HIP;
@@ -298,6 +315,8 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
       ulen[b] = u;
     }
   }
+  const bool dz_mode = compression == 1 && p->dev_snappy;   // stored bytes H2D, device decompression
+  const bool ranged = compression == 0 || dz_mode;
   std::vector<Chunk> chunks;
   Caps need;
   for (uint32_t b = 0; b < nblk;) {
@@ -305,10 +324,13 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     while (b < nblk && c.nb < p->max_blocks) {
       const uint64_t u = ulen[b];
       const uint64_t nhi = std::max(c.hi, blk_off[b] + blk_len[b]);
-      const uint64_t span = compression == 0 ? nhi - std::min(c.lo, blk_off[b]) : c.ubytes + u;
+      const uint64_t range = nhi - std::min(c.lo, blk_off[b]);
+      const uint64_t span = compression == 0 ? range
+                            : dz_mode   ? std::max<uint64_t>(range, c.ubytes + u + 16ull * (c.nb + 1))
+                                        : c.ubytes + u;
       if (c.nb > 0 && span > p->chunk_bytes) break;
-      // uncompressed chunks are one contiguous file range: blocks must be in file order
-      if (compression == 0 && c.nb > 0 && blk_off[b] < c.hi) break;
+      // chunks shipped as stored are one contiguous file range: blocks must be in file order
+      if (ranged && c.nb > 0 && blk_off[b] < c.hi) break;
       c.lo = std::min(c.lo, blk_off[b]);
       c.hi = nhi;
       c.ubytes += u;
@@ -316,7 +338,9 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
       ++c.nb;
       ++b;
     }
-    const uint64_t in = compression == 0 ? c.hi - c.lo : c.ubytes;
+    const uint64_t in = compression == 0 ? c.hi - c.lo
+                        : dz_mode   ? std::max<uint64_t>(c.hi - c.lo, c.ubytes + 16ull * c.nb)
+                                    : c.ubytes;
     need.in = std::max(need.in, in);
     st.block_bytes += c.ubytes;
     chunks.push_back(c);
@@ -328,7 +352,7 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     for (auto& s : p->slot)
       if (alloc_slot(s, c) != MTBLX_OK) return MTBLX_E_HIP;
   }
-  const bool pinned_src = compression == 0 && nblk && host_pinned(file);
+  const bool pinned_src = ranged && nblk && host_pinned(file);
 
   uint64_t R = 0, K = 0, V = 0, flags = 0;
   std::vector<std::pair<uint32_t, uint32_t>> skipped;   // chunks whose outputs did not fit `out`
@@ -345,13 +369,24 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     const double t0 = now_s();
     uint64_t* doff = reinterpret_cast<uint64_t*>(s.h);
     uint32_t* dlen = reinterpret_cast<uint32_t*>(s.h + 8 * s.cap.blocks);
-    uint8_t* hdata = s.h + s.dir_bytes();
+    uint8_t* hdata = s.h + s.data_at();
+    uint64_t* zoff = reinterpret_cast<uint64_t*>(s.h + s.dir_bytes());            // dz_mode: dst_off
+    uint32_t* zlen = reinterpret_cast<uint32_t*>(s.h + s.dir_bytes() + 8 * s.cap.blocks);   // dst_len
+    uint64_t ubytes = 0;
     const uint8_t* src = hdata;
     uint64_t bytes;
-    if (compression == 0) {
+    if (ranged) {
       for (uint32_t j = 0; j < c.nb; ++j) {
         doff[j] = blk_off[c.b0 + j] - c.lo;
         dlen[j] = blk_len[c.b0 + j];
+      }
+      if (dz_mode) {   // the decompressed layout: 16-byte aligned starts, lengths from the preambles
+        for (uint32_t j = 0; j < c.nb; ++j) {
+          const uint32_t u = zerr[c.b0 + j] ? 0u : (uint32_t)ulen[c.b0 + j];
+          zoff[j] = ubytes;
+          zlen[j] = u;
+          ubytes += (u + 15ull) & ~15ull;
+        }
       }
       bytes = c.hi - c.lo;
       if (pinned_src) {
@@ -387,17 +422,32 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     st.stage_seconds += now_s() - t0;
     hipStream_t sh = p->s_h2d, sd = p->s_dec;
     const uint64_t lens_at = 8 * s.cap.blocks;
-    if (hipMemcpyAsync(s.d, s.h, 8ull * c.nb, hipMemcpyHostToDevice, sh) != hipSuccess ||
-        hipMemcpyAsync(s.d + lens_at, s.h + lens_at, 4ull * c.nb, hipMemcpyHostToDevice, sh) != hipSuccess)
+    for (int half = 0; half < (dz_mode ? 2 : 1); ++half) {
+      const uint64_t h0 = half * s.dir_bytes();
+      if (hipMemcpyAsync(s.d + h0, s.h + h0, 8ull * c.nb, hipMemcpyHostToDevice, sh) != hipSuccess ||
+          hipMemcpyAsync(s.d + h0 + lens_at, s.h + h0 + lens_at, 4ull * c.nb, hipMemcpyHostToDevice, sh) != hipSuccess)
+        return MTBLX_E_HIP;
+      st.h2d_bytes += 12ull * c.nb;
+    }
+    if (bytes && hipMemcpyAsync(s.d + s.data_at(), src, bytes, hipMemcpyHostToDevice, sh) != hipSuccess)
       return MTBLX_E_HIP;
-    if (bytes && hipMemcpyAsync(s.d + s.dir_bytes(), src, bytes, hipMemcpyHostToDevice, sh) != hipSuccess)
-      return MTBLX_E_HIP;
-    st.h2d_bytes += 12ull * c.nb + bytes;
+    st.h2d_bytes += bytes;
     if (hipEventRecord(s.e_h2d, sh) != hipSuccess || hipStreamWaitEvent(sd, s.e_h2d, 0) != hipSuccess)
       return MTBLX_E_HIP;
-    mtblx_block_batch in{s.d + s.dir_bytes(), bytes ? bytes : 1, reinterpret_cast<const uint64_t*>(s.d),
+    mtblx_block_batch in{s.d + s.data_at(), bytes ? bytes : 1, reinterpret_cast<const uint64_t*>(s.d),
                          reinterpret_cast<const uint32_t*>(s.d + 8 * s.cap.blocks), c.nb, c.maxlen};
     (void)hipEventRecord(s.e_dec0, sd);
+    if (dz_mode) {   // Reader::block's decompression (src/reader.rs:166-170) on the device
+      uint32_t* dec_len = reinterpret_cast<uint32_t*>(s.dz);
+      int32_t* zst = reinterpret_cast<int32_t*>(s.dz + 4 * s.cap.blocks);
+      const uint64_t* d_zoff = reinterpret_cast<const uint64_t*>(s.d + s.dir_bytes());
+      const uint32_t* d_zlen = reinterpret_cast<const uint32_t*>(s.d + s.dir_bytes() + lens_at);
+      int rz = mtblx_snappy_decompress_dev(s.d + s.data_at(), in.blk_off, in.blk_len, c.nb, s.du, d_zoff, d_zlen,
+                                           c.maxlen, zst, dec_len, sd);
+      if (rz != MTBLX_OK) return rz;
+      if (hipMemcpyAsync(s.hz, zst, 4ull * c.nb, hipMemcpyDeviceToHost, sd) != hipSuccess) return MTBLX_E_HIP;
+      in = mtblx_block_batch{s.du, std::max<uint64_t>(ubytes, 1), d_zoff, dec_len, c.nb, c.maxlen};
+    }
     int r = mtblx_decode_blocks(&in, &s.o, p->ws, p->ws_bytes, sd);
     if (r != MTBLX_OK) return r;
     if (hipMemcpyAsync(s.htot, s.o.totals, 32, hipMemcpyDeviceToHost, sd) != hipSuccess) return MTBLX_E_HIP;
@@ -412,6 +462,9 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     if (hipEventSynchronize(s.e_dec) != hipSuccess) return MTBLX_E_HIP;
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s.e_dec0, s.e_dec) == hipSuccess) st.decode_ms += ms;
+    if (dz_mode)   // device decompression failures: Err(Error::Io), the block decoded as empty
+      for (uint32_t j = 0; j < c.nb; ++j)
+        if (s.hz[j] != MTBLX_SNAPPY_OK) zerr[c.b0 + j] = 1;
     uint64_t nr = s.htot[0], kb = s.htot[1], vb = s.htot[2];
     if (s.htot[3] & 1ull) {
       // the slot's output capacity was too small (keys far longer than the block bytes):
@@ -421,9 +474,12 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
       c2.keys = std::max(c2.keys, kb + 64);
       c2.vals = std::max(c2.vals, vb + 64);
       if (hipStreamSynchronize(p->s_d2h) != hipSuccess || alloc_outputs(s, c2) != MTBLX_OK) return MTBLX_E_HIP;
-      mtblx_block_batch in{s.d + s.dir_bytes(), std::max<uint64_t>(compression == 0 ? c.hi - c.lo : c.ubytes, 1),
+      mtblx_block_batch in{s.d + s.data_at(), std::max<uint64_t>(compression == 0 ? c.hi - c.lo : c.ubytes, 1),
                            reinterpret_cast<const uint64_t*>(s.d),
                            reinterpret_cast<const uint32_t*>(s.d + 8 * s.cap.blocks), c.nb, c.maxlen};
+      if (dz_mode)
+        in = mtblx_block_batch{s.du, s.du_bytes(), reinterpret_cast<const uint64_t*>(s.d + s.dir_bytes()),
+                               reinterpret_cast<const uint32_t*>(s.dz), c.nb, c.maxlen};
       int r = mtblx_decode_blocks(&in, &s.o, p->ws, p->ws_bytes, p->s_dec);
       if (r != MTBLX_OK) return r;
       if (hipMemcpyAsync(s.htot, s.o.totals, 32, hipMemcpyDeviceToHost, p->s_dec) != hipSuccess ||
@@ -488,6 +544,15 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
   st.seconds = now_s() - t_start;
   if (stats) *stats = st;
   return MTBLX_OK;
+}
+
+extern "C" int mtblx_pipe_set(mtblx_pipe* p, int option, int64_t value) {
+  if (!p) return MTBLX_E_INVAL;
+  if (option == MTBLX_PIPE_DEVICE_SNAPPY) {
+    p->dev_snappy = value != 0;
+    return MTBLX_OK;
+  }
+  return MTBLX_E_INVAL;
 }
 
 extern "C" int mtblx_host_alloc(void** p, uint64_t bytes) {

@@ -24,8 +24,9 @@
 //  - a RUN is a sequence of elements whose copy sources all lie before the run's first output
 //    byte: its bytes are independent, so the wave writes them all at once (lane = output byte,
 //    element found by a 6-step binary search over the parked starts).  A copy that reads bytes
-//    of the current run (short offsets, overlapping copies) closes the run first.  A run that
-//    is a single literal is copied 4 bytes per lane (aligned dword stores).
+//    of the current run (short offsets, overlapping copies) closes the run first.  A run of
+//    long elements (>= 64 bytes on average) is instead copied element by element, 4 bytes per
+//    lane with aligned dword stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -57,35 +58,66 @@ __device__ __forceinline__ void lds_fence() { __asm__ volatile("" ::: "memory");
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
+// A window: the block's stored bytes at block positions [wstart, wstart + W) (wstart = p0
+// rounded down to a 16-byte address; bytes outside the block read as 0), loaded as 16-byte
+// chunks, up to NCH per lane, all loads in flight before the first LDS store.
 template <class C>
-__device__ __forceinline__ void snap_block(WaveLds<C>& S, const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ dg,
-                           uint32_t cap, int lane, int32_t* st_out, uint32_t* dec_len) {
-  // ---- LDS window over the stored bytes ----
-  int32_t wstart = 0;   // block position of window byte 0 (16-byte aligned in memory; may be < 0)
-  uint32_t whi = 0;     // window holds block positions [max(wstart, 0), whi)
-  auto restage = [&](uint32_t p0) {
+struct Window {
+  static constexpr int NCH = (C::W / 16 + kWave - 1) / kWave;
+  int32_t wstart;
+  uint32_t whi, nch;   // block positions [max(wstart, 0), whi) are valid; nch chunks
+  uint4 v[NCH];
+
+  __device__ __forceinline__ void load(const uint8_t* s, uint32_t n, uint32_t p0, int lane) {
     const uint32_t r = (uint32_t)(((uintptr_t)s + p0) & 15u);
     wstart = (int32_t)p0 - (int32_t)r;
     const int32_t e = wstart + C::W;
     whi = (e > (int32_t)n) ? n : (uint32_t)e;
-    const uint32_t nch = (uint32_t)((int32_t)whi - wstart + 15) / 16u;
-    lds_fence();
-    for (uint32_t c = (uint32_t)lane; c < nch; c += kWave) {
+    nch = (uint32_t)((int32_t)whi - wstart + 15) / 16u;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const uint32_t c = (uint32_t)lane + (uint32_t)k * kWave;
       const int32_t bp = wstart + 16 * (int32_t)c;
-      uint4 v;
-      if (bp >= 0 && bp + 16 <= (int32_t)n) {
-        v = *reinterpret_cast<const uint4*>(s + bp);
-      } else {
+      if (c < nch && bp >= 0 && bp + 16 <= (int32_t)n) {
+        v[k] = *reinterpret_cast<const uint4*>(s + bp);
+      } else if (c < nch) {
         uint32_t w[4] = {0, 0, 0, 0};
-        for (int k = 0; k < 16; ++k) {
-          const int32_t q = bp + k;
-          if (q >= 0 && q < (int32_t)n) w[k >> 2] |= (uint32_t)s[q] << (8 * (k & 3));
+        for (int t = 0; t < 16; ++t) {
+          const int32_t q = bp + t;
+          if (q >= 0 && q < (int32_t)n) w[t >> 2] |= (uint32_t)s[q] << (8 * (t & 3));
         }
-        v = make_uint4(w[0], w[1], w[2], w[3]);
+        v[k] = make_uint4(w[0], w[1], w[2], w[3]);
       }
-      *reinterpret_cast<uint4*>(S.win + 16 * c) = v;
+    }
+  }
+  __device__ __forceinline__ void store(uint8_t* win, int lane) const {
+    lds_fence();
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const uint32_t c = (uint32_t)lane + (uint32_t)k * kWave;
+      if (c < nch) *reinterpret_cast<uint4*>(win + 16 * c) = v[k];
     }
     lds_fence();
+  }
+};
+
+// pf: the first window of this block, loaded while the previous block ran; it is stored here
+// and refilled with the first window of the wave's next block (s2, n2) right away.
+template <class C>
+__device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const uint8_t* __restrict__ s, uint32_t n,
+                                           const uint8_t* s2, uint32_t n2, uint8_t* __restrict__ dg, uint32_t cap,
+                                           int lane, int32_t* st_out, uint32_t* dec_len) {
+  // ---- LDS window over the stored bytes ----
+  int32_t wstart = pf.wstart;   // block position of window byte 0 (16-byte aligned in memory; may be < 0)
+  uint32_t whi = pf.whi;        // window holds block positions [max(wstart, 0), whi)
+  pf.store(S.win, lane);
+  pf.load(s2, n2, 0, lane);
+  auto restage = [&](uint32_t p0) {
+    Window<C> w;
+    w.load(s, n, p0, lane);
+    w.store(S.win, lane);
+    wstart = w.wstart;
+    whi = w.whi;
   };
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(S.win);
   // 8 bytes at block position p (p in the window), wave-uniform
@@ -96,7 +128,6 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, const uint8_t* __restr
     hi = __builtin_amdgcn_alignbit(c, b, sh);
   };
 
-  restage(0);
   // ---- preamble: varint32 uncompressed length ----
   uint32_t lo, hi;
   hdr8(0, lo, hi);
@@ -121,20 +152,33 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, const uint8_t* __restr
   // ---- element runs ----
   uint32_t e_d = 0xFFFFFFFFu, e_len = 0, e_x = 0;   // lane k: parked element k (start, len | lit<<31, x)
   uint32_t ne = 0, D = 0, d = 0;                    // parked count, run start, output position
-  // every byte of the run [D, d): lane = output byte, element by binary search over the starts
+  // every byte of the run [D, d), 64 at a time (lane = output byte).  k0 = the element holding
+  // the first byte of the step (uniform, carried); the m elements starting inside the step are
+  // found with one ballot, and each lane binary-searches only those (none for long elements).
   auto run_bytes = [&](auto* out) {
     const uint32_t T = d - D;
+    uint32_t k0 = 0;
     for (uint32_t base = 0; base < T; base += kWave) {
+      const uint32_t B = D + base;
       const uint32_t i = min(base + (uint32_t)lane, T - 1u), p = D + i;
-      uint32_t k = 0;
-#pragma unroll
-      for (uint32_t stp = 32; stp; stp >>= 1) {
-        const uint32_t kk = k + stp;
-        if ((uint32_t)__shfl((int)e_d, (int)kk, kWave) <= p) k = kk;   // lanes >= ne hold ~0
+      const uint32_t m = (uint32_t)__popcll(__ballot(e_d > B && e_d <= B + (kWave - 1)));   // lanes >= ne: ~0
+      uint32_t k = k0, ed, el, ex;
+      if (m == 0) {
+        ed = (uint32_t)__builtin_amdgcn_readlane((int)e_d, (int)k0);
+        el = (uint32_t)__builtin_amdgcn_readlane((int)e_len, (int)k0);
+        ex = (uint32_t)__builtin_amdgcn_readlane((int)e_x, (int)k0);
+      } else {
+        for (uint32_t stp = 1u << (31 - __builtin_clz(m)); stp; stp >>= 1) {
+          const uint32_t kk = k + stp;
+          // the shuffle runs on every lane: a bpermute from a lane masked off by a branch reads garbage
+          const uint32_t v = (uint32_t)__shfl((int)e_d, (int)min(kk, 63u), kWave);
+          if (kk <= k0 + m && v <= p) k = kk;
+        }
+        ed = (uint32_t)__shfl((int)e_d, (int)k, kWave);
+        el = (uint32_t)__shfl((int)e_len, (int)k, kWave);
+        ex = (uint32_t)__shfl((int)e_x, (int)k, kWave);
       }
-      const uint32_t ed = (uint32_t)__shfl((int)e_d, (int)k, kWave);
-      const uint32_t el = (uint32_t)__shfl((int)e_len, (int)k, kWave);
-      const uint32_t ex = (uint32_t)__shfl((int)e_x, (int)k, kWave);
+      k0 += (uint32_t)__popcll(__ballot(e_d > B && e_d <= B + kWave));
       const uint32_t r = p - ed;
       uint8_t v;
       if (el >> 31) {
@@ -153,19 +197,35 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, const uint8_t* __restr
     if (glob) {
       run_bytes(dg);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this run's HBM bytes before the next run's reads
-    } else if (ne == 1 && (ufl(e_len) >> 31)) {
-      // one literal: 4 bytes per lane, aligned dword stores into the output
-      const uint32_t ex = ufl(e_x);
-      const uint32_t h = min((4u - (D & 3u)) & 3u, T);
-      if ((uint32_t)lane < h) S.out[D + lane] = S.win[ex + lane];
-      const uint32_t nd = (T - h) / 4u, sp0 = ex + h, sh = (sp0 & 3u) * 8u;
-      uint32_t* o32 = reinterpret_cast<uint32_t*>(S.out + D + h);
-      for (uint32_t j = (uint32_t)lane; j < nd; j += kWave) {
-        const uint32_t q = (sp0 >> 2) + j;
-        o32[j] = __builtin_amdgcn_alignbit(w32[q + 1], w32[q], sh);
+    } else if (T >= (uint32_t)kWave * ne) {
+      // long elements (>= 64 bytes on average): one at a time, 4 bytes per lane with aligned
+      // dword stores (literals, and copies that do not overlap themselves); self-overlapping
+      // copies byte by byte (their pattern repeats every `off` bytes)
+      const uint32_t* o32r = reinterpret_cast<const uint32_t*>(S.out);
+      for (uint32_t k = 0; k < ne; ++k) {
+        const uint32_t ed = (uint32_t)__builtin_amdgcn_readlane((int)e_d, (int)k);
+        const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)e_len, (int)k);
+        const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)e_x, (int)k);
+        const uint32_t len = el & 0x7FFFFFFFu;
+        const bool lit = (el >> 31) != 0;
+        if (!lit && ex < len) {
+          for (uint32_t j = (uint32_t)lane; j < len; j += kWave) S.out[ed + j] = S.out[ed - ex + j % ex];
+          continue;
+        }
+        const uint8_t* src = lit ? S.win : S.out;
+        const uint32_t* src32 = lit ? w32 : o32r;
+        const uint32_t s0 = lit ? ex : ed - ex;
+        const uint32_t h = min((4u - (ed & 3u)) & 3u, len);
+        if ((uint32_t)lane < h) S.out[ed + lane] = src[s0 + lane];
+        const uint32_t nd = (len - h) / 4u, sp0 = s0 + h, sh = (sp0 & 3u) * 8u;
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(S.out + ed + h);
+        for (uint32_t j = (uint32_t)lane; j < nd; j += kWave) {
+          const uint32_t q = (sp0 >> 2) + j;
+          o32[j] = __builtin_amdgcn_alignbit(src32[q + 1], src32[q], sh);
+        }
+        const uint32_t t0 = h + 4u * nd;
+        if ((uint32_t)lane < len - t0) S.out[ed + t0 + lane] = src[s0 + t0 + lane];
       }
-      const uint32_t t0 = h + 4u * nd;
-      if ((uint32_t)lane < T - t0) S.out[D + t0 + lane] = S.win[ex + t0 + lane];
     } else {
       run_bytes(S.out);
     }
@@ -244,8 +304,10 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, const uint8_t* __restr
       hl = 5;
     }
     if (off == 0 || off > d || W - d < len) { st = MTBLX_SNAPPY_CORRUPT; break; }
-    // its source must precede the run (the first bytes of the pattern for an overlapping copy)
-    if (d - off + min(len, off) > D) flush();
+    // its source must be written before the step that reads it: before the run (the first
+    // bytes of the pattern for an overlapping copy), or -- LDS output, 64-byte steps in order
+    // -- at least one step back (off >= 64)
+    if (d - off + min(len, off) > D && (glob || off < (uint32_t)kWave)) flush();
     park(len, 0u, off);
     pos += hl;
   }
@@ -280,9 +342,21 @@ __global__ void __launch_bounds__(C::WAVES * kWave) k_snappy_blocks(const uint8_
   __shared__ WaveLds<C> S[C::WAVES];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * C::WAVES;
-  for (uint32_t b = blockIdx.x * C::WAVES + wv; b < nblk; b += nw)
-    snap_block<C>(S[wv], src + src_off[b], src_len[b], dst + dst_off[b], dst_len[b], lane, status + b,
+  uint32_t b = blockIdx.x * C::WAVES + wv;
+  if (b >= nblk) return;
+  const uint8_t* s = src + src_off[b];
+  uint32_t n = src_len[b];
+  Window<C> pf;
+  pf.load(s, n, 0, lane);
+  for (; b < nblk; b += nw) {
+    const uint32_t b2 = b + nw;
+    const uint8_t* s2 = b2 < nblk ? src + src_off[b2] : s;
+    const uint32_t n2 = b2 < nblk ? src_len[b2] : 0u;
+    snap_block<C>(S[wv], pf, s, n, s2, n2, dst + dst_off[b], dst_len[b], lane, status + b,
                   dec_len ? dec_len + b : nullptr);
+    s = s2;
+    n = n2;
+  }
 }
 
 // ---- directory: preamble lengths, 16-byte aligned exclusive prefix ----

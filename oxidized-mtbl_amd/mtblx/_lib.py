@@ -31,7 +31,7 @@ EXPORTS = [
     "mtblx_writer_block_count", "mtblx_writer_block_dir", "mtblx_writer_free", "mtblx_free",
     "mtblx_snappy_max_compressed_len", "mtblx_snappy_uncompressed_len", "mtblx_snappy_decompress",
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
-    "mtblx_pipe_decode", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
+    "mtblx_pipe_decode", "mtblx_pipe_set", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev",
 ]
@@ -132,6 +132,8 @@ def lib() -> C.CDLL:
         L.mtblx_pipe_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_uint32, C.POINTER(Decoded), C.POINTER(PipeStats)]
         L.mtblx_pipe_decode.restype = C.c_int
+        L.mtblx_pipe_set.argtypes = [C.c_void_p, C.c_int, C.c_int64]
+        L.mtblx_pipe_set.restype = C.c_int
         L.mtblx_encode_plan.argtypes = [C.POINTER(Records), C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                         C.c_void_p, C.c_uint64, u64p, u32p, C.c_void_p]
         L.mtblx_encode_plan.restype = C.c_int

@@ -74,11 +74,15 @@ class _Plain:
 class HostPipe:
     """mtblx_pipe: chunked host -> device -> host decode with three chunks in flight."""
 
-    def __init__(self, chunk_bytes: int = 64 << 20, max_blocks: int = 1 << 16, threads: int = 16):
+    def __init__(self, chunk_bytes: int = 64 << 20, max_blocks: int = 1 << 16, threads: int = 16,
+                 device_snappy: bool = False):
         codec._require_device()
         self._p = _lib.lib().mtblx_pipe_new(int(chunk_bytes), int(max_blocks), int(threads))
         if not self._p:
             raise RuntimeError("mtblx_pipe_new failed")
+        # MTBLX_PIPE_DEVICE_SNAPPY: snappy blocks cross PCIe compressed, decompressed on the device
+        if _lib.lib().mtblx_pipe_set(self._p, 1, 1 if device_snappy else 0) != 0:
+            raise RuntimeError("mtblx_pipe_set failed")
         self.stats = PipeStats()
 
     def decode(self, file: np.ndarray, blk_off: np.ndarray, blk_len: np.ndarray, out: HostOutputs,

@@ -1,0 +1,65 @@
+"""Diagnostic: device snappy decompression of the cfg5 stored blocks (cfg2 records written with
+CompressionType::Snappy), timed with HIP events; run under rocprofv3 for kernel stats / PMC.
+    python scripts/snappy_probe.py [--blocks N] [--reps R]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "oxidized-mtbl_amd")]
+
+from mtblx import codec, synth  # noqa: E402
+from mtblx.writer import Writer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=100_000)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--compressible", action="store_true", help="cfg1-style repeated values instead")
+    a = ap.parse_args()
+    t0 = time.time()
+    w = Writer(4096, 16, 1)
+    if a.compressible:
+        for k, v in synth.cfg1_records(a.blocks * 20):
+            w.insert(k, v)
+        z = np.frombuffer(w.into_inner(), np.uint8).copy()
+    else:
+        per = (4096 - 64) // 79
+        n = a.blocks * per
+        keys, vals, kl, vl = synth.cfg2_arrays(n)
+        w.insert_batch(keys, np.arange(1, n + 1, dtype=np.uint64) * np.uint64(kl), vals,
+                       np.arange(1, n + 1, dtype=np.uint64) * np.uint64(vl))
+        z = w.into_inner_np()
+    zoff, zln = w.block_dir
+    print(f"generated {zoff.size} blocks, {int(zln.sum()) / 2**20:.1f} MiB stored in {time.time() - t0:.1f}s",
+          flush=True)
+    zb = codec.SnappyBatch.from_host(z, zoff, zln)
+    lay = codec.SnappyLayout(zb.nblk)
+    codec.snappy_dir(zb, lay)
+    torch.cuda.synchronize()
+    tot = lay.totals.cpu().numpy().view(np.uint64)
+    dst = torch.zeros(int(tot[0]) + 16, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(zb.nblk, dtype=torch.int32, device="cuda")
+    dl = torch.zeros(zb.nblk, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        codec.snappy_decompress_into(zb, lay, dst, st, dl, int(tot[1]), s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(a.reps):
+        codec.snappy_decompress_into(zb, lay, dst, st, dl, int(tot[1]), s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    out_bytes = int(dl.sum().item())
+    print(f"decompress {ms:.4f} ms  {out_bytes / ms / 1e6:.1f} GB/s out  stored {int(zln.sum()) / ms / 1e6:.1f} GB/s in"
+          f"  bad={int((st != 0).sum().item())}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -42,9 +42,10 @@ def _cfg2_records(nblk):
     return keys, ke, vals, ve
 
 
-def _pipe_decode(data, off, ln, comp, exp, chunk=1 << 20, max_blocks=1 << 16, pinned_src=False, caps=None):
+def _pipe_decode(data, off, ln, comp, exp, chunk=1 << 20, max_blocks=1 << 16, pinned_src=False, caps=None,
+                 device_snappy=False):
     from mtblx import pipe
-    p = pipe.HostPipe(chunk_bytes=chunk, max_blocks=max_blocks, threads=8)
+    p = pipe.HostPipe(chunk_bytes=chunk, max_blocks=max_blocks, threads=8, device_snappy=device_snappy)
     nr = int(exp.nrec.sum())
     caps = caps or (nr, exp.keys.size, exp.vals.size)
     out = pipe.HostOutputs(off.size, *caps)
@@ -131,9 +132,36 @@ def test_pipe_snappy_equals_uncompressed(oracle):
         assert st.block_bytes == int(l0.sum()) and st.decompress_errors == 0
 
 
+def test_pipe_device_snappy_equals_uncompressed(oracle):
+    """MTBLX_PIPE_DEVICE_SNAPPY: stored (compressed) bytes cross PCIe and are decompressed on
+    the device; same outputs as the None file, pageable and pinned sources, several chunkings;
+    plus a compressible file (repeated values, ratio well above 1)"""
+    _need_gpu()
+    from mtblx import pipe
+    f = _files(_cfg2_records(400))
+    d0, o0, l0 = f[0]
+    d1, o1, l1 = f[1]
+    exp = oracle.decode_blocks(d0, o0, l0)
+    for chunk, pinned in ((1 << 20, False), (100_000, True), (64 << 20, True)):
+        out, st = _pipe_decode(d1, o1, l1, 1, exp, chunk=chunk, pinned_src=pinned, device_snappy=True)
+        _assert_same(out, exp)
+        assert st.block_bytes == int(l0.sum()) and st.decompress_errors == 0
+        assert st.h2d_bytes < int(l1.sum()) + 40 * o1.size + 4096
+    from mtblx import synth
+    f = _files(list(synth.cfg1_records(20000)), block_size=8192)
+    d0, o0, l0 = f[0]
+    d1, o1, l1 = f[1]
+    assert int(l1.sum()) * 3 < int(l0.sum())
+    exp = oracle.decode_blocks(d0, o0, l0)
+    for chunk in (1 << 20, 200_000):
+        out, st = _pipe_decode(d1, o1, l1, 1, exp, chunk=chunk, device_snappy=True)
+        _assert_same(out, exp)
+        assert st.decompress_errors == 0 and st.h2d_bytes < int(l0.sum()) // 2
+
+
 def test_pipe_snappy_corrupt_block(oracle):
     """a block that fails decompression -> MTBLX_ST_DECOMPRESS (the reference: Err(Error::Io)),
-    every other block decoded"""
+    every other block decoded; host and device decompression alike"""
     _need_gpu()
     f = _files(_cfg2_records(60))
     d0, o0, l0 = f[0]
@@ -143,14 +171,21 @@ def test_pipe_snappy_corrupt_block(oracle):
     for b in bad:
         d1[int(o1[b]) + int(l1[b]) - 1] ^= 0xFF   # last literal byte flips: length still fine...
         d1[int(o1[b])] ^= 0x01                    # ...but the preamble length no longer matches
+    d1[int(o1[50]) + int(l1[50]) // 2] ^= 0x5A   # mid-stream damage: preamble intact
     exp = oracle.decode_blocks(d0, o0, l0)
-    out, st = _pipe_decode(d1, o1, l1, 1, exp)
-    assert st.decompress_errors == len(bad)
-    for b in range(o0.size):
-        if b in bad:
-            assert out.status[b] == 6 and out.nrec[b] == 0
-        else:
-            assert out.status[b] == 0 and out.nrec[b] == exp.nrec[b]
+    from mtblx import pipe
+    zbad = [b for b in range(o1.size) if pipe.snappy_decompress(d1[int(o1[b]): int(o1[b]) + int(l1[b])]) is None]
+    assert set(bad) <= set(zbad)
+    for dev in (False, True):
+        out, st = _pipe_decode(d1, o1, l1, 1, exp, device_snappy=dev)
+        assert st.decompress_errors == len(zbad)
+        for b in range(o0.size):
+            if b in zbad:
+                assert out.status[b] == 6 and out.nrec[b] == 0
+            elif b == 50:   # decompressed to other bytes of the right length: decoded as they are
+                assert out.status[b] != 6
+            else:
+                assert out.status[b] == 0 and out.nrec[b] == exp.nrec[b]
 
 
 def test_pipe_capacity_overflow_reports_sizes(oracle):

@@ -693,7 +693,8 @@ def main():
         d = ws.buf[:128].cpu().numpy().view(np.uint64).astype(np.float64)
         names = ["copy:wait-ready", "w1:lookback+barrier", "w0:walk-loop", "w0:scan-publish",
                  "loader:dma-issue", "copy:barrier", "loader:dma-wait", "copy:copy", "w0:barrier",
-                 "w0:trailers", "w0:interval-setup", "-", "loader:barrier"]
+                 "w0:trailers", "w0:interval-setup", "w1:barrier", "loader:barrier",
+                 "copy:barrier-min-over-waves", "copy:prepare-max-over-waves"]
         ntl = max(d[15], 1)
         res["phase_cycles_per_tile"] = {n: round(d[k] / ntl, 1) for k, n in enumerate(names)}
         res["stamps_note"] = "diagnostic build (s_memtime, thread 0 of each workgroup), last step only; shares, not time"

@@ -30,23 +30,17 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& w, uint32_t t) {
   return (d >> (8 * (t & 3))) & 0xffu;
 }
 
-// 16 bytes starting at byte offset `a` of an LDS byte array whose base is 16B aligned.
-// Five aligned dword reads + v_alignbyte (no unaligned LDS access).
+// 16 bytes starting at byte offset `a` of an LDS byte array: one unaligned ds_read_b128
+// (gfx950 runs LDS in unaligned access mode) instead of five aligned dword reads + alignbit.
+typedef uint32_t lds_v4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t __attribute__((aligned(1))) lds_u32u;
 __device__ __forceinline__ uint4 lds_win16(const uint8_t* lds, uint32_t a) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (a & ~3u));
-  uint32_t s = (a & 3u) * 8u;
-  uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-  uint4 r;
-  r.x = __builtin_amdgcn_alignbit(w1, w0, s);
-  r.y = __builtin_amdgcn_alignbit(w2, w1, s);
-  r.z = __builtin_amdgcn_alignbit(w3, w2, s);
-  r.w = __builtin_amdgcn_alignbit(w4, w3, s);
-  return r;
+  const lds_v4u v = *reinterpret_cast<const lds_v4u*>(lds + a);
+  return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t a) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (a & ~3u));
-  return __builtin_amdgcn_alignbit(w[1], w[0], (a & 3u) * 8u);
+  return *reinterpret_cast<const lds_u32u*>(lds + a);
 }
 
 // byte mask selecting bytes [lo, hi) of a dword whose first byte is byte `base`
@@ -965,7 +959,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 // diagnostic per-phase cycle stamps (MTBLX_STAMPS builds only; lane 0 of a wave)
 struct Stamps {
 #ifdef MTBLX_STAMPS
-  uint64_t acc[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t prev = 0;
   __device__ __forceinline__ void init() { prev = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void hit(int k) {
@@ -1564,13 +1558,22 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
       const uint32_t nch = nrow * cpr;
       uint8_t* vd0 = a.vals + pv + (r.fv ? B.ivb[r.f] : 0u);
       const int rowbase = lane & ~15;
-      for (uint32_t c = r.k; __ballot(c < nch) != 0ull; c += 16) {   // wave-uniform trip count
-        const bool act = c < nch;
-        const uint32_t e = act ? (pow2 ? c >> cprs : c / cpr) : 0u;
-        const uint32_t src = (uint32_t)__shfl((int)vsrc, rowbase + (int)e, kWave);
-        if (act) {
-          const uint4 w4 = lds_win16(B.stage, src + 16u * (c - e * cpr));
-          *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4.x, w4.y, w4.z, w4.w};
+      // 4 chunks per lane per pass: the 4 permutes and LDS reads are in flight together
+      // before the stores (one latency chain per pass instead of per chunk)
+      for (uint32_t c0 = r.k; __ballot(c0 < nch) != 0ull; c0 += 64) {   // wave-uniform trip count
+        uint4 w4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t c = c0 + 16u * (uint32_t)u;
+          const bool act = c < nch;
+          const uint32_t e = act ? (pow2 ? c >> cprs : c / cpr) : 0u;
+          const uint32_t src = (uint32_t)__shfl((int)vsrc, rowbase + (int)e, kWave);
+          w4[u] = act ? lds_win16(B.stage, src + 16u * (c - e * cpr)) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t c = c0 + 16u * (uint32_t)u;
+          if (c < nch) *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4[u].x, w4[u].y, w4[u].z, w4[u].w};
         }
       }
     } else if (live) {
@@ -1626,6 +1629,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
   uint32_t fb = (uint32_t)cw * (kWave / 16);
   if (fb < nint) {
     const CopyRow r = copy_prepare(B, fb, lane);
+    ST.hit(14);
     wait_flag(ready, want);
     ST.hit(0);
     if (a.write) copy_emit(B, a, r, lane);
@@ -1902,6 +1906,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           pipe_lookback_issue(a, tc + G, G, lbv, lane);
           pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kPipeCopyWaves);
         }
+        ST.hit(1);
       } else {
         pipe_copy(C, a, wv - kPipeCopyWave0, lane, &S.ready, (uint32_t)it + 1, ST);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1910,9 +1915,9 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     }
     raw_barrier();
     if (wv == 0) { ST.hit(8); ++ntl; }
-    else if (wv == kPipeCopyWave0) ST.hit(5);
+    else if (wv >= kPipeCopyWave0) ST.hit(5);
     else if (loader) ST.hit(12);
-    else ST.hit(1);
+    else ST.hit(11);
   }
   // retire this wave's outstanding global stores before the workgroup ends
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1921,9 +1926,23 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   // wave 0: [2] trailers + walk loop, [3] scans + publish, [8] barrier.  wave 1: [1]
   // look-back (+ barrier).  first loader: [4] DMA issue, [6] DMA wait + barrier.  first copy
   // wave: [0] wait ready, [7] copy, [5] barrier.  Summed over workgroups (lane 0); [15] tiles.
+  // copy waves: [13] the smallest barrier wait among them (the last to arrive), [14] the
+  // longest prepare of the first round (before the wait for the look-back), per workgroup
+  __shared__ unsigned long long cmin, cmax;
+  if (tid == 0) { cmin = ~0ull; cmax = 0; }
+  __syncthreads();
+  if (lane == 0 && wv >= kPipeCopyWave0) {
+    atomicMin(&cmin, (unsigned long long)ST.acc[5]);
+    atomicMax(&cmax, (unsigned long long)ST.acc[14]);
+  }
+  __syncthreads();
+  if (tid == 0 && a.dbg) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 13), cmin);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 14), cmax);
+  }
   if (lane == 0 && a.dbg && (wv <= kPipeLoadWave || wv == kPipeCopyWave0)) {
     for (int k = 0; k < 13; ++k) {
-      const bool mine = (wv == 0) ? (k == 2 || k == 3 || k == 8 || k == 9 || k == 10) : (wv == 1) ? (k == 1) : loader ? (k == 4 || k == 6 || k == 11 || k == 12) : (k == 0 || k == 5 || k == 7);
+      const bool mine = (wv == 0) ? (k == 2 || k == 3 || k == 8 || k == 9 || k == 10) : (wv == 1) ? (k == 1 || k == 11) : loader ? (k == 4 || k == 6 || k == 12) : (k == 0 || k == 5 || k == 7);
       if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)ST.acc[k]);
     }
     if (wv == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 15), (unsigned long long)ntl);

@@ -1219,15 +1219,23 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
   if (contig) {
     // range byte x at stage offset 16 + x; wave-instruction m writes chunks [64m, 64m + 64)
     const uint32_t nch = (uint32_t)((e - r0 + 15) >> 4);
-    for (uint32_t m = part; m * kWave < nch; m += kPipeLoadWaves) {
+    // chunks [0, nfull) are 16-byte aligned and inside the buffer: whole pieces of them take a
+    // lean loop (address add + DMA); the tail piece goes lane by lane
+    const bool al = ((base + r0) & 15ull) == 0;
+    const uint64_t room = a.data_len > r0 ? (a.data_len - r0) / 16u : 0u;
+    const uint32_t nfull = al ? (uint32_t)min<uint64_t>(nch, room) : 0u;
+    const uint32_t mfull = nfull / kWave;   // pieces made only of such chunks
+    uint32_t m = part;
+    const uint8_t* gp = a.data + r0 + 16ull * ((uint64_t)m * kWave + (uint32_t)lane);
+    for (; m < mfull; m += kPipeLoadWaves, gp += 16 * kWave * kPipeLoadWaves)
+      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
+    for (; m * kWave < nch; m += kPipeLoadWaves) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
-      if (c < nch) {
-        if (go + 16 <= a.data_len && ((base + go) & 15ull) == 0)
-          __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
-        else
-          *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
-      }
+      if (c < nfull)
+        __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
+      else if (c < nch)
+        *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
     }
     if (part == 0 && lane < (int)nb) {
       B.boff[lane] = (uint32_t)(16 + off_l - r0);

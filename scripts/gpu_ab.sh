@@ -13,14 +13,17 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   tail -1 gpurun_out/gpu_tests.log
   [ $rc -eq 0 ] || { echo "TESTS FAILED rc=$rc: stop"; exit 1; }
 fi
-for r in 1 2; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 50 --lib oxidized-mtbl_amd/build/libmtblx_base.so > gpurun_out/ab_base$r.log 2>&1 || exit 3
+BA="--no-cpu-baseline --no-e2e --no-crc --no-ceiling --steps 200 --warmup 20 ${BENCH_ARGS:-}"
+for r in 1 2 3; do
+  timeout -k 10 300 python bench.py $BA --lib oxidized-mtbl_amd/build/libmtblx_base.so > gpurun_out/ab_base$r.log 2>&1 || exit 3
   val gpurun_out/ab_base$r.log base
-  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 50 > gpurun_out/ab_new$r.log 2>&1 || exit 3
+  timeout -k 10 300 python bench.py $BA > gpurun_out/ab_new$r.log 2>&1 || exit 3
   val gpurun_out/ab_new$r.log new
 done
-timeout -k 10 300 python bench.py --no-cpu-baseline --stamps > gpurun_out/stamps.log 2>&1 || exit 3
-val gpurun_out/stamps.log stamps
+if [ "${STAMPS:-0}" = 1 ]; then
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e --no-crc --stamps > gpurun_out/stamps.log 2>&1 || exit 3
+  val gpurun_out/stamps.log stamps
+fi
 if [ "${LARGE:-0}" = 1 ]; then
   for bs in 16384 65536; do
     timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --block-size $bs --blocks $((100000 * 4096 / bs)) > gpurun_out/large_$bs.log 2>&1 || exit 3

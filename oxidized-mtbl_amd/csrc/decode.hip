@@ -1581,7 +1581,11 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const uint32_t c = c0 + 16u * (uint32_t)u;
+#ifdef MTBLX_ABL_NOVSTORE   // diagnostic: the value reads without the value stores
+          if (c < nch) asm volatile("" ::"v"(w4[u].x), "v"(w4[u].y), "v"(w4[u].z), "v"(w4[u].w));
+#else
           if (c < nch) *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4[u].x, w4[u].y, w4[u].z, w4[u].w};
+#endif
         }
       }
     } else if (live) {

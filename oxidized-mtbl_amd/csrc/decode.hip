@@ -975,24 +975,27 @@ struct Stamps {
 
 constexpr int kPipeThreads = 1024;
 constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loaders (issue no stores)
-constexpr int kPipeLoadWaves = 2;                                        // waves 2..3
-constexpr int kPipeCopyWave0 = kPipeLoadWave + kPipeLoadWaves;           // waves 4..15 copy
-constexpr int kPipeCopyWaves = kPipeThreads / kWave - kPipeCopyWave0;
-constexpr int kPipeRows = kPipeCopyWaves * (kWave / 16);                 // intervals per copy round
 constexpr int kP2Spi = 16;                                               // slots per interval (= DPP row)
 
 // Pipeline configurations.  TB = staging bytes of a tile buffer, NBUF = tile buffers in
 // LDS (3: DMA / walk / copy of three tiles overlap; 2: DMA of the next tile overlaps the
 // walk + copy of this one), MAXBLK blocks and MAXINT (<= 64: one walk lane each) restart
 // intervals per tile.
-template <int TB_, int NBUF_, int MAXBLK_, int MAXINT_, bool VERIFY_ = false>
+// LOADW LDS-DMA loader waves (waves 2 .. 2 + LOADW - 1); the rest from 2 + LOADW copy.
+template <int TB_, int NBUF_, int MAXBLK_, int MAXINT_, bool VERIFY_ = false, int LOADW_ = 2>
 struct PipeCfg {
   static constexpr int TB = TB_, NBUF = NBUF_, MAXBLK = MAXBLK_, MAXINT = MAXINT_;
   static constexpr int SLOTS = MAXINT * kP2Spi;
   static constexpr bool VERIFY = VERIFY_;   // fused CRC-32C of every staged block (f1)
+  static constexpr int LOADW = LOADW_;
+  static constexpr int COPY0 = kPipeLoadWave + LOADW;             // first copy wave
+  static constexpr int NCOPY = kPipeThreads / kWave - COPY0;      // copy waves
+  static constexpr int ROWS = NCOPY * (kWave / 16);               // intervals per copy round
 };
-using PipeSmall = PipeCfg<49152, 3, 16, 56>;   // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
-using PipeLarge = PipeCfg<65664, 2, 2, 64>;    // blocks up to ~64 KiB (cfg3, cfg4 64 KiB)
+// 64 KiB tiles: the DMA of the next tile is the other half of the iteration, so four loader
+// waves issue it (the copy of a <= 64-interval tile takes two rounds with 10 or 12 copy waves)
+using PipeSmall = PipeCfg<49152, 3, 16, 56>;          // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
+using PipeLarge = PipeCfg<65664, 2, 2, 64, false, 4>; // blocks up to ~64 KiB (cfg3, cfg4 64 KiB)
 using PipeSmallV = PipeCfg<49152, 3, 16, 56, true>;
 using PipeLargeV = PipeCfg<65664, 2, 2, 64, true>;
 
@@ -1227,9 +1230,9 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
     const uint32_t mfull = nfull / kWave;   // pieces made only of such chunks
     uint32_t m = part;
     const uint8_t* gp = a.data + r0 + 16ull * ((uint64_t)m * kWave + (uint32_t)lane);
-    for (; m < mfull; m += kPipeLoadWaves, gp += 16 * kWave * kPipeLoadWaves)
+    for (; m < mfull; m += P::LOADW, gp += 16 * kWave * P::LOADW)
       __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
-    for (; m * kWave < nch; m += kPipeLoadWaves) {
+    for (; m * kWave < nch; m += P::LOADW) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
       if (c < nfull)
@@ -1254,7 +1257,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
         if (base + off < 16 || ((base + off) & ~15ull) < base) a0 = off;  // unaligned data base: not reached
         const uint32_t delta = (uint32_t)(off - a0);
         const uint32_t nch = (delta + L + 15u) >> 4;
-        for (uint32_t m = part; m * kWave < nch; m += kPipeLoadWaves) {
+        for (uint32_t m = part; m * kWave < nch; m += P::LOADW) {
           const uint32_t c = m * kWave + lane;
           const uint64_t go = a0 + 16ull * c;
           if (c < nch) {
@@ -1645,7 +1648,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
     wait_flag(ready, want);
     ST.hit(0);
     if (a.write) copy_emit(B, a, r, lane);
-    for (fb += kPipeRows; fb < nint; fb += kPipeRows) {   // wave-uniform
+    for (fb += P::ROWS; fb < nint; fb += P::ROWS) {   // wave-uniform
       const CopyRow r2 = copy_prepare(B, fb, lane);
       if (a.write) copy_emit(B, a, r2, lane);
     }
@@ -1673,7 +1676,8 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
 // slicing-by-4 over 16 words, 4 chunks in flight per lane; contributions are XORed into a
 // per-block LDS accumulator; the last of the three waves to finish a tile finalises it.
 // ---------------------------------------------------------------------------------
-constexpr int kCrcWaves = 3;   // the look-back wave + the two loader waves
+template <class P>
+constexpr int kCrcWaves = 1 + P::LOADW;   // the look-back wave + the loader waves
 
 template <class P>
 __device__ __forceinline__ uint32_t crc_word4(const PipeLds<P>& S, uint32_t c, uint32_t w) {
@@ -1701,12 +1705,12 @@ __device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, 
   }
   const uint32_t incl = wave_incl_scan(mych), excl = incl - mych;
   constexpr int kCh = 2;   // chunks in flight per lane (register budget: 128 VGPRs at 16 waves/CU)
-  for (uint32_t base = 0; base < total; base += kCh * kCrcWaves * kWave) {
+  for (uint32_t base = 0; base < total; base += kCh * kCrcWaves<P> * kWave) {
     uint32_t c[kCh], d0[kCh], jk[kCh], sft[kCh];   // jk = block << 16 | chunk
     int32_t q[kCh], p0[kCh];   // first dword index; block position of the window's first byte
 #pragma unroll
     for (int i = 0; i < kCh; ++i) {
-      const uint32_t ch = base + (uint32_t)i * kCrcWaves * kWave + gl;
+      const uint32_t ch = base + (uint32_t)i * kCrcWaves<P> * kWave + gl;
       uint32_t j0 = 0;
       for (uint32_t j = 1; j < nb; ++j) j0 += ((uint32_t)__shfl((int)excl, (int)j, kWave) <= ch) ? 1u : 0u;
       const uint32_t e0 = (uint32_t)__shfl((int)excl, (int)j0, kWave);
@@ -1750,7 +1754,7 @@ __device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, 
   uint32_t old = 0;
   if (lane == 0) old = __hip_atomic_fetch_add(&S.crcdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
   old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-  if (old % kCrcWaves != kCrcWaves - 1) return;
+  if (old % kCrcWaves<P> != kCrcWaves<P> - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   uint32_t crc = 0, L = 0, o = kNotStaged;
   if (lane < (int)nb) {
@@ -1823,7 +1827,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     ilen = a.blk_len[b0 + j];
   };
   // loaders split every tile's DMA pieces (even / odd 1 KiB pieces)
-  const bool loader = wv >= kPipeLoadWave && wv < kPipeLoadWave + kPipeLoadWaves;
+  const bool loader = wv >= kPipeLoadWave && wv < kPipeLoadWave + P::LOADW;
   const uint32_t part = (uint32_t)(wv - kPipeLoadWave);
   if (loader) {
     load_info(0);
@@ -1867,12 +1871,12 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
         wait_flag(&S.pub, it + 1);
-        pipe_copy(C, a, wv - kPipeCopyWave0, lane, &S.ready, it + 1, ST);
+        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, it + 1, ST);
         ST.hit(7);
       }
       raw_barrier();
       if (wv == 0) { ST.hit(8); ++ntl; }
-      else if (wv == kPipeCopyWave0) ST.hit(5);
+      else if (wv == P::COPY0) ST.hit(5);
       else if (loader) ST.hit(12);
       else ST.hit(1);
     }
@@ -1916,18 +1920,18 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
             if (++spins > (1u << 24)) break;
           }
           pipe_lookback_issue(a, tc + G, G, lbv, lane);
-          pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kPipeCopyWaves);
+          pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
         }
         ST.hit(1);
       } else {
-        pipe_copy(C, a, wv - kPipeCopyWave0, lane, &S.ready, (uint32_t)it + 1, ST);
+        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(7);
       }
     }
     raw_barrier();
     if (wv == 0) { ST.hit(8); ++ntl; }
-    else if (wv >= kPipeCopyWave0) ST.hit(5);
+    else if (wv >= P::COPY0) ST.hit(5);
     else if (loader) ST.hit(12);
     else ST.hit(11);
   }
@@ -1943,7 +1947,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   __shared__ unsigned long long cmin, cmax;
   if (tid == 0) { cmin = ~0ull; cmax = 0; }
   __syncthreads();
-  if (lane == 0 && wv >= kPipeCopyWave0) {
+  if (lane == 0 && wv >= P::COPY0) {
     atomicMin(&cmin, (unsigned long long)ST.acc[5]);
     atomicMax(&cmax, (unsigned long long)ST.acc[14]);
   }
@@ -1952,7 +1956,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 13), cmin);
     atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + 14), cmax);
   }
-  if (lane == 0 && a.dbg && (wv <= kPipeLoadWave || wv == kPipeCopyWave0)) {
+  if (lane == 0 && a.dbg && (wv <= kPipeLoadWave || wv == P::COPY0)) {
     for (int k = 0; k < 13; ++k) {
       const bool mine = (wv == 0) ? (k == 2 || k == 3 || k == 8 || k == 9 || k == 10) : (wv == 1) ? (k == 1 || k == 11) : loader ? (k == 4 || k == 6 || k == 12) : (k == 0 || k == 5 || k == 7);
       if (mine) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg + k), (unsigned long long)ST.acc[k]);

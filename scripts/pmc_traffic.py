@@ -29,7 +29,7 @@ def rows(pattern):
 
 
 # the product decode of the cfg2 batch: k_decode_pipe<PipeSmall> (not the fused-verify variant)
-KERNEL_MATCH = "PipeCfg<49152, 3, 16, 56, false>"
+KERNEL_MATCH = "PipeCfg<49152, 3, 16, 56, false"
 
 
 def counter(d, name, kernel):

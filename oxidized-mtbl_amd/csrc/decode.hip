@@ -976,6 +976,7 @@ struct Stamps {
 constexpr int kPipeThreads = 1024;
 constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loaders (issue no stores)
 constexpr int kP2Spi = 16;                                               // slots per interval (= DPP row)
+constexpr uint32_t kLargeDmaSplit = 24;   // PipeLarge, short copies: pieces staged before the walk ends (of ~64)
 
 // Pipeline configurations.  TB = staging bytes of a tile buffer, NBUF = tile buffers in
 // LDS (3: DMA / walk / copy of three tiles overlap; 2: DMA of the next tile overlaps the
@@ -1205,8 +1206,10 @@ __device__ __forceinline__ bool walk_careful_pos(const uint8_t* stage, uint16_t*
 // wave 0: LDS-DMA of tile t into B (contiguous range, or one 16 B aligned slot per block).
 // (off_l, len_l) = directory entry of block `lane` of the tile (lanes < nb).
 template <class P>
+// Pieces (1 KiB wave-instructions) m in [mlo, mhi) with m = part (mod LOADW) of the
+// contiguous layout are issued; the per-block slot layout is issued whole when mlo == 0.
 __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint32_t t, uint64_t off_l, uint32_t len_l,
-                                         int lane, uint32_t part) {
+                                         int lane, uint32_t part, uint32_t mlo = 0, uint32_t mhi = 0xFFFFFFFFu) {
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void g_void;
   const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
@@ -1227,12 +1230,13 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
     const bool al = ((base + r0) & 15ull) == 0;
     const uint64_t room = a.data_len > r0 ? (a.data_len - r0) / 16u : 0u;
     const uint32_t nfull = al ? (uint32_t)min<uint64_t>(nch, room) : 0u;
-    const uint32_t mfull = nfull / kWave;   // pieces made only of such chunks
-    uint32_t m = part;
+    const uint32_t mfull = min(nfull / kWave, mhi);   // pieces made only of such chunks
+    uint32_t m = part + ((mlo + P::LOADW - 1 - part) / P::LOADW) * P::LOADW;   // first piece >= mlo
+    if (mlo <= part) m = part;
     const uint8_t* gp = a.data + r0 + 16ull * ((uint64_t)m * kWave + (uint32_t)lane);
     for (; m < mfull; m += P::LOADW, gp += 16 * kWave * P::LOADW)
       __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
-    for (; m * kWave < nch; m += P::LOADW) {
+    for (; m * kWave < nch && m < mhi; m += P::LOADW) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
       if (c < nfull)
@@ -1244,7 +1248,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
       B.boff[lane] = (uint32_t)(16 + off_l - r0);
       B.blen[lane] = len_l;
     }
-  } else {
+  } else if (mlo == 0) {
     // per-block slots of a.slot bytes (blocks not adjacent in the buffer)
     for (uint32_t j = 0; j < nb; ++j) {
       const uint64_t off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off_l >> 32), (int)j) << 32) |
@@ -1356,6 +1360,25 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
     B.nint = nint;
   }
   // block totals (regular: differences of the interval scan) and tile-relative block bases.
+  if (nb == 1) {
+    // one block per tile (64 KiB blocks): every cross-lane value is lane 0's or the last
+    // interval's -- readlanes instead of permutes, no scans
+    const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 0);
+    const uint32_t tc = n0 ? (uint32_t)__builtin_amdgcn_readlane((int)ic, (int)n0 - 1) : 0u;
+    const uint32_t tkk = n0 ? (uint32_t)__builtin_amdgcn_readlane((int)ik, (int)n0 - 1) : 0u;
+    const uint32_t tvv = n0 ? (uint32_t)__builtin_amdgcn_readlane((int)iv, (int)n0 - 1) : 0u;
+    if (lane == 0) {
+      B.bok[0] = ok; B.bwr[0] = 1; B.bst[0] = ok ? MTBLX_ST_OK : gst;
+      B.bcnt[0] = ok ? tc : gc; B.bkb[0] = ok ? tkk : gk; B.bvb[0] = ok ? tvv : gv;
+      B.brb[0] = 0; B.bkbb[0] = 0; B.bvbb[0] = 0;
+    }
+    if (fl) {
+      B.icnt[lane] = ic - c;
+      B.ikb[lane] = ik - k;
+      B.ivb[lane] = iv - v;
+    }
+    return;
+  }
   // Every lane executes the permutes (a disabled source lane reads as 0).
   const int ea_l = bint0 ? (int)bint0 - 1 : 0, eb_l = incl ? (int)incl - 1 : 0;
   const uint32_t ea0 = (uint32_t)__shfl((int)ic, ea_l, kWave), eb0 = (uint32_t)__shfl((int)ic, eb_l, kWave);
@@ -1854,7 +1877,19 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         ST.hit(3);
       } else if (loader) {
         if (it + 1 < nloc) {
-          pipe_dma(S.buf[(it + 1) & 1u], a, tc + G, ioff, ilen, lane, part);
+          // DMA landing in LDS slows the walker's tail (LDS writes and fences queue behind it)
+          // by ~3.5k cycles per 64 KiB tile, but beside the copy it slows a key-heavy copy
+          // (cfg3's long keys read many 16-byte key planes).  So: when the previous tile's key
+          // bytes were under a third of its value bytes (the copy is short), stage only the
+          // first kLargeDmaSplit pieces beside the walk's chain and the rest after the walk.
+          // (the other buffer still holds that tile's totals: the DMA writes only its stage)
+          PipeBuf<P>& N = S.buf[(it + 1) & 1u];
+          const bool late = it >= 1 && 3ull * N.ttot[1] <= (uint64_t)N.ttot[2];
+          pipe_dma(N, a, tc + G, ioff, ilen, lane, part, 0, late ? kLargeDmaSplit : 0xFFFFFFFFu);
+          if (late) {
+            wait_flag(&S.pub, it + 1);
+            pipe_dma(N, a, tc + G, ioff, ilen, lane, part, kLargeDmaSplit);
+          }
           load_info(it + 2);
         }
         ST.hit(4);

@@ -252,16 +252,37 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
   return before + inc - x;
 }
 
-// copy n bytes from global src to dst (LDS or global, generic pointer)
-__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n) {
-  uint64_t o = 0;
-  for (; o + 16 <= n; o += 16) {
-    const v4u w = *reinterpret_cast<const v4u*>(src + o);
-    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+// copy n bytes from global src to dst (LDS or global, generic pointer).  Four 16-byte loads
+// are in flight before their stores (the loads are the latency: a serial load -> store chain
+// per 16 bytes was most of the encode time); stores are unaligned 16-byte stores (gfx950 runs
+// in unaligned access mode).  A tail of 1..15 bytes is read as the 16-byte window ending at n
+// when the record is at least 16 bytes long (never before `base`, the blob's start), else
+// byte by byte.
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n, const uint8_t* base) {
+  // chunks of 16 bytes: [0, nfull); tail bytes [16 nfull, n)
+  const uint64_t nfull = n / 16;
+  for (uint64_t c = 0; c < nfull; c += 4) {
+    v4u w[4];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[o + k] = (uint8_t)(ws[k >> 2] >> (8 * (k & 3)));
+    for (int u = 0; u < 4; ++u)
+      if (c + u < nfull) w[u] = *reinterpret_cast<const v4u*>(src + 16 * (c + u));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c + u < nfull) *reinterpret_cast<v4u*>(dst + 16 * (c + u)) = w[u];
   }
-  for (; o < n; ++o) dst[o] = src[o];
+  const uint32_t t = (uint32_t)(n % 16);
+  if (t == 0) return;
+  const uint64_t to = 16 * nfull;
+  if (src + n >= base + 16) {   // the 16-byte window ending at n holds the tail in its last t bytes
+    const v4u w = *reinterpret_cast<const v4u*>(src + n - 16);
+    for (uint32_t k = 0; k < t; ++k) {
+      const uint32_t q = 16 - t + k;
+      const uint32_t d = q < 4 ? w.x : q < 8 ? w.y : q < 12 ? w.z : w.w;
+      dst[to + k] = (uint8_t)(d >> (8 * (q & 3)));
+    }
+  } else {
+    for (uint64_t k = to; k < n; ++k) dst[k] = src[k];
+  }
 }
 
 __device__ __forceinline__ void put32(uint8_t* p, uint32_t v) {
@@ -348,8 +369,8 @@ __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent
   n += venc(h + n, e.kl - e.sh);
   n += venc(h + n, e.vl);
   for (uint32_t k = 0; k < n; ++k) dst[k] = h[k];
-  copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh);
-  copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl);
+  copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys);
+  copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl, R.vals);
 }
 
 __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
@@ -376,7 +397,7 @@ __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeo
   return excl;
 }
 
-__global__ void __launch_bounds__(kThreads) k_encode(EncArgs a) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) k_encode(EncArgs a) {   // 2 per CU
   __shared__ EncLds S;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int i = tid; i < 256; i += kThreads) {   // slicing-by-4 tables from the byte table

@@ -17,9 +17,10 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
 }
 step gpu_tests 900 python -m pytest tests -m gpu -x -q
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 50 --warmup 10
 rm -rf gpurun_out/prof_$TAG
-step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/stats -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
+step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/stats -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e
 step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_$TAG/fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-crc
 step prof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_$TAG/write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-crc
 find gpurun_out/prof_$TAG -name "*.csv" | sort

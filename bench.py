@@ -698,6 +698,24 @@ def main():
         ntl = max(d[15], 1)
         res["phase_cycles_per_tile"] = {n: round(d[k] / ntl, 1) for k, n in enumerate(names)}
         res["stamps_note"] = "diagnostic build (s_memtime, thread 0 of each workgroup), last step only; shares, not time"
+        import ctypes as C
+        from mtblx import _lib as mlib
+        L = mlib.lib()
+        if hasattr(L, "mtblx_dbg_timeline"):
+            G = 1024
+            tl = np.zeros((G, 8), np.uint64)
+            if L.mtblx_dbg_timeline(tl.ctypes.data_as(C.POINTER(C.c_uint64)), G) == 0:
+                tl = tl[tl[:, 0] > 0].astype(np.int64)
+                t0 = tl[:, 0].min()
+                us = (tl[:, :6] - t0) / 100.0   # s_memrealtime ticks at 100 MHz
+                res["timeline_us"] = {
+                    n: {"min": round(float(us[:, k].min()), 2), "mean": round(float(us[:, k].mean()), 2),
+                        "max": round(float(us[:, k].max()), 2)}
+                    for k, n in enumerate(["entry", "preload", "first_walk", "iter0", "loop_end", "exit"])}
+                res["timeline_us"]["tiles_per_wg"] = [int(tl[:, 6].min()), int(tl[:, 6].max())]
+                res["timeline_us"]["wgs"] = int(tl.shape[0])
+                res["timeline_raw"] = [[round(float(x), 1) for x in us[i, [1, 3, 4, 5]]] + [int(tl[i, 6])]
+                                       for i in range(us.shape[0])]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(data, off, ln, args.cpu_seconds)
     if rank == 0:

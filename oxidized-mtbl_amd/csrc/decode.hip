@@ -67,13 +67,31 @@ typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef uint16_t __attribute__((aligned(1))) u16u;
 
+// Output stores.  The decoded keys / values / ends are written once and never read back by
+// this launch: non-temporal stores (MTBLX_NT_STORES) stream them out instead of leaving the
+// XCD L2s full of dirty lines that the end-of-launch release must write back.
+#ifndef MTBLX_NT_STORES
+#define MTBLX_NT_STORES 1
+#endif
+#ifndef MTBLX_NT_LOADS   // LDS-DMA of the block bytes with the non-temporal policy (aux = 2)
+#define MTBLX_NT_LOADS 0
+#endif
+#ifndef MTBLX_WSEND_LIGHT
+#define MTBLX_WSEND_LIGHT 1
+#endif
+#if MTBLX_NT_STORES
+#define ost(p, ...) __builtin_nontemporal_store((__VA_ARGS__), (p))
+#else
+#define ost(p, ...) (void)(*(p) = (__VA_ARGS__))
+#endif
+
 // store the first m (0..16) bytes of w at p
 __device__ __forceinline__ void store_bytes(uint8_t* p, uint4 w, uint32_t m) {
-  if (m == 16) { *reinterpret_cast<v4u*>(p) = v4u{w.x, w.y, w.z, w.w}; return; }
-  if (m & 8) { *reinterpret_cast<v2u*>(p) = v2u{w.x, w.y}; w = make_uint4(w.z, w.w, 0, 0); p += 8; }
-  if (m & 4) { *reinterpret_cast<u32u*>(p) = w.x; w.x = w.y; p += 4; }
-  if (m & 2) { *reinterpret_cast<u16u*>(p) = (uint16_t)w.x; w.x >>= 16; p += 2; }
-  if (m & 1) { *p = (uint8_t)w.x; }
+  if (m == 16) { ost(reinterpret_cast<v4u*>(p), v4u{w.x, w.y, w.z, w.w}); return; }
+  if (m & 8) { ost(reinterpret_cast<v2u*>(p), v2u{w.x, w.y}); w = make_uint4(w.z, w.w, 0, 0); p += 8; }
+  if (m & 4) { ost(reinterpret_cast<u32u*>(p), w.x); w.x = w.y; p += 4; }
+  if (m & 2) { ost(reinterpret_cast<u16u*>(p), (uint16_t)w.x); w.x >>= 16; p += 2; }
+  if (m & 1) { ost(p, (uint8_t)w.x); }
 }
 
 // Inclusive scan over the 64 lanes with DPP (row_shr 1/2/4/8 inside each 16-lane row,
@@ -357,8 +375,16 @@ __device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bi
 __device__ __forceinline__ void ws_end(const TileArgs& a) {
   __syncthreads();
   if (threadIdx.x == 0) {
+#if MTBLX_WSEND_LIGHT
+    // What the last workgroup reads from the others is only `flags`, which they update with
+    // agent-scope atomics; the __syncthreads above waited (vmcnt) until this workgroup's were
+    // performed.  No agent-scope release: on gfx950 it writes back the XCD's whole L2
+    // (buffer_wbl2), i.e. every dirty output line, once per workgroup.
+    const uint32_t old = __hip_atomic_fetch_add(&a.hdr->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t old = __hip_atomic_fetch_add(&a.hdr->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     if (old == gridDim.x - 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const unsigned long long f = __hip_atomic_load(&a.hdr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -973,6 +999,16 @@ struct Stamps {
 #endif
 };
 
+#ifdef MTBLX_STAMPS
+// diagnostic timeline (s_memrealtime, 100 MHz) per workgroup of the last k_decode_pipe launch:
+// [0] entry [1] preload done [2] first walk done (it = -1) [3] it = 0 done [4] loop end
+// [5] after ws_end [6] tiles of this workgroup
+__device__ uint64_t g_tl[1024][8];
+#define TL(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TL(k) do { } while (0)
+#endif
+
 constexpr int kPipeThreads = 1024;
 constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loaders (issue no stores)
 constexpr int kP2Spi = 16;                                               // slots per interval (= DPP row)
@@ -1235,12 +1271,12 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
     if (mlo <= part) m = part;
     const uint8_t* gp = a.data + r0 + 16ull * ((uint64_t)m * kWave + (uint32_t)lane);
     for (; m < mfull; m += P::LOADW, gp += 16 * kWave * P::LOADW)
-      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? 2 : 0);
     for (; m * kWave < nch && m < mhi; m += P::LOADW) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
       if (c < nfull)
-        __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? 2 : 0);
       else if (c < nch)
         *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
     }
@@ -1571,8 +1607,8 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
   const bool live = r.live && B.bwr[r.j];   // bwr may have been cleared by the look-back (overflow)
   if (live) {
     const uint64_t gr = pr + B.icnt[r.f] + r.k;
-    a.key_end[gr] = r.ks + r.klen - B.bkbb[r.j];
-    a.val_end[gr] = r.vs + r.vl - B.bvbb[r.j];
+    ost(a.key_end + gr, r.ks + r.klen - B.bkbb[r.j]);
+    ost(a.val_end + gr, r.vs + r.vl - B.bvbb[r.j]);
   }
 #ifndef MTBLX_ABL_NOVAL
   // values.  Fast path (wave-uniform): every live entry of this round has the same value
@@ -1610,7 +1646,7 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
 #ifdef MTBLX_ABL_NOVSTORE   // diagnostic: the value reads without the value stores
           if (c < nch) asm volatile("" ::"v"(w4[u].x), "v"(w4[u].y), "v"(w4[u].z), "v"(w4[u].w));
 #else
-          if (c < nch) *reinterpret_cast<v4u*>(vd0 + 16u * c) = v4u{w4[u].x, w4[u].y, w4[u].z, w4[u].w};
+          if (c < nch) ost(reinterpret_cast<v4u*>(vd0 + 16u * c), v4u{w4[u].x, w4[u].y, w4[u].z, w4[u].w});
 #endif
         }
       }
@@ -1823,6 +1859,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
   Stamps ST;
   ST.init();
+  TL(0);
   ws_begin(a);
   if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; }
   if constexpr (P::VERIFY) {
@@ -1861,6 +1898,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     if (P::NBUF == 3 && nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
   }
   __syncthreads();
+  TL(1);
   if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
   uint64_t ntl = 0;
 
@@ -1965,14 +2003,21 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       }
     }
     raw_barrier();
+    if (it == -1) TL(2);
+    else if (it == 0) TL(3);
     if (wv == 0) { ST.hit(8); ++ntl; }
     else if (wv >= P::COPY0) ST.hit(5);
     else if (loader) ST.hit(12);
     else ST.hit(11);
   }
+  TL(4);
   // retire this wave's outstanding global stores before the workgroup ends
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ws_end(a);
+  TL(5);
+#ifdef MTBLX_STAMPS
+  if (tid == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][6] = nloc;
+#endif
 #ifdef MTBLX_STAMPS
   // wave 0: [2] trailers + walk loop, [3] scans + publish, [8] barrier.  wave 1: [1]
   // look-back (+ barrier).  first loader: [4] DMA issue, [6] DMA wait + barrier.  first copy
@@ -2079,6 +2124,13 @@ int resident_grid(uint32_t ntiles) {
 
 // workspace: [0, 128) diagnostic stamps | [128, 256) WsHdr | 3 u64 per tile (tiles <= nblk).
 // Zero-filled once by the caller; every launch leaves it ready for the next (ws_end).
+#ifdef MTBLX_STAMPS
+extern "C" int mtblx_dbg_timeline(uint64_t* out, uint32_t nwg) {   // diagnostic build only
+  if (nwg > 1024) nwg = 1024;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mtblx::g_tl), (size_t)nwg * 8 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
 
 extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed,

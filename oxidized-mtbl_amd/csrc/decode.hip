@@ -1491,7 +1491,8 @@ __device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t
 // per-block outputs.  tinc = inclusive prefix of this workgroup's previous tile.
 template <class P>
 __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3],
-                                              uint64_t lbv[kMaxLookbackLoads], int lane) {
+                                              uint64_t lbv[kMaxLookbackLoads], int lane, uint32_t* ready,
+                                              uint32_t rv) {
   const uint32_t nb = B.nb, b0 = B.b0;
   const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
   uint64_t sr = 0, sk = 0, sv = 0;
@@ -1529,6 +1530,13 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
     B.tpre[0] = pr; B.tpre[1] = pk; B.tpre[2] = pv;
     if (t == a.ntiles - 1) { a.totals[0] = tinc[0]; a.totals[1] = tinc[1]; a.totals[2] = tinc[2]; }
   }
+  // the copy waves need only tpre, and bwr where a block overflows the caller's buffers: when
+  // the whole tile fits, release them before the per-block outputs are written
+  const bool fits = !a.write || (tinc[0] <= a.rec_cap && tinc[1] <= a.keys_cap && tinc[2] <= a.vals_cap);
+  if (fits) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(ready, rv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   if (lane < (int)nb) {
     const uint32_t j = lane, b = b0 + j;
     const uint64_t rb = pr + B.brb[j], kb = pk + B.bkbb[j], vb = pv + B.bvbb[j];
@@ -1543,6 +1551,10 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
       ws_flag(a, 1ull);
     }
     a.status[b] = st;
+  }
+  if (!fits) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(ready, rv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -1937,9 +1949,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       } else if (wv == 1) {
         wait_flag(&S.pub, it + 1);
         pipe_lookback_issue(a, tc, G, lbv, lane);
-        pipe_lookback(C, a, tc, G, tinc, lbv, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&S.ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, it + 1);
         ST.hit(1);
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
@@ -1978,9 +1988,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       PipeBuf<P>& C = S.buf[(uint32_t)it % P::NBUF];
       const uint32_t tc = g + (uint32_t)it * G;
       if (wv == 1) {
-        pipe_lookback(C, a, tc, G, tinc, lbv, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&S.ready, (uint32_t)it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, (uint32_t)it + 1);
         ST.hit(1);
         // CRC of tile it while lbv is dead (its words were consumed above): lower register pressure
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, (uint32_t)it & 1u);

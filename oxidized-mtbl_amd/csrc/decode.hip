@@ -71,7 +71,7 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 // this launch: non-temporal stores (MTBLX_NT_STORES) stream them out instead of leaving the
 // XCD L2s full of dirty lines that the end-of-launch release must write back.
 #ifndef MTBLX_NT_STORES
-#define MTBLX_NT_STORES 1
+#define MTBLX_NT_STORES 2
 #endif
 #ifndef MTBLX_NT_LOADS   // LDS-DMA of the block bytes with the non-temporal policy (aux = 2)
 #define MTBLX_NT_LOADS 0
@@ -84,14 +84,21 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 #else
 #define ost(p, ...) (void)(*(p) = (__VA_ARGS__))
 #endif
+// byte-granular stores (keys of any length, value tails): MTBLX_NT_STORES == 1 streams them
+// too; == 2 keeps them in L2, where partial lines merge before they are written back
+#if MTBLX_NT_STORES == 1
+#define ostb(p, ...) __builtin_nontemporal_store((__VA_ARGS__), (p))
+#else
+#define ostb(p, ...) (void)(*(p) = (__VA_ARGS__))
+#endif
 
 // store the first m (0..16) bytes of w at p
 __device__ __forceinline__ void store_bytes(uint8_t* p, uint4 w, uint32_t m) {
-  if (m == 16) { ost(reinterpret_cast<v4u*>(p), v4u{w.x, w.y, w.z, w.w}); return; }
-  if (m & 8) { ost(reinterpret_cast<v2u*>(p), v2u{w.x, w.y}); w = make_uint4(w.z, w.w, 0, 0); p += 8; }
-  if (m & 4) { ost(reinterpret_cast<u32u*>(p), w.x); w.x = w.y; p += 4; }
-  if (m & 2) { ost(reinterpret_cast<u16u*>(p), (uint16_t)w.x); w.x >>= 16; p += 2; }
-  if (m & 1) { ost(p, (uint8_t)w.x); }
+  if (m == 16) { ostb(reinterpret_cast<v4u*>(p), v4u{w.x, w.y, w.z, w.w}); return; }
+  if (m & 8) { ostb(reinterpret_cast<v2u*>(p), v2u{w.x, w.y}); w = make_uint4(w.z, w.w, 0, 0); p += 8; }
+  if (m & 4) { ostb(reinterpret_cast<u32u*>(p), w.x); w.x = w.y; p += 4; }
+  if (m & 2) { ostb(reinterpret_cast<u16u*>(p), (uint16_t)w.x); w.x >>= 16; p += 2; }
+  if (m & 1) { ostb(p, (uint8_t)w.x); }
 }
 
 // Inclusive scan over the 64 lanes with DPP (row_shr 1/2/4/8 inside each 16-lane row,

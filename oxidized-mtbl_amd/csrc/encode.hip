@@ -258,6 +258,10 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
 // in unaligned access mode).  A tail of 1..15 bytes is read as the 16-byte window ending at n
 // when the record is at least 16 bytes long (never before `base`, the blob's start), else
 // byte by byte.
+#ifndef MTBLX_ENC_NT_STORES
+#define MTBLX_ENC_NT_STORES 1
+#endif
+
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n, const uint8_t* base) {
   // chunks of 16 bytes: [0, nfull); tail bytes [16 nfull, n)
   const uint64_t nfull = n / 16;
@@ -501,7 +505,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       const uint64_t nch = L / 16;
       for (uint64_t c = tid; c < nch; c += kThreads) {
         const v4a x = *reinterpret_cast<const v4a*>(S.ob + 16 * c);
+#if MTBLX_ENC_NT_STORES   // the framed file bytes are written once: stream them out
+        __builtin_nontemporal_store(v4u{x.x, x.y, x.z, x.w}, reinterpret_cast<v4u*>(dst + 16 * c));
+#else
         *reinterpret_cast<v4u*>(dst + 16 * c) = v4u{x.x, x.y, x.z, x.w};
+#endif
       }
       for (uint64_t o = 16 * nch + tid; o < L; o += kThreads) dst[o] = S.ob[o];
     }

@@ -88,6 +88,10 @@ inline void hip_check(hipError_t e, const char* what) {
 inline void abi_check(int rc, const char* what) {
   if (rc != MTBLX_OK) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
 }
+// totals[3] bit 1: the launch's look-back timed out and nothing it wrote may be used (mtblx.h)
+inline void launch_check(uint64_t flags, const char* what) {
+  if (flags & 2ull) throw std::runtime_error(std::string(what) + ": look-back timeout, outputs discarded");
+}
 // device buffer (hipMalloc), freed with the owner
 struct DevBuf {
   void* p = nullptr;
@@ -147,6 +151,7 @@ inline Decoded decode_batch(const uint8_t* d_data, uint64_t data_len, const uint
   abi_check(mtblx_count_blocks(&in, &out, ws.p, wsb, nullptr), "mtblx_count_blocks");
   hip_check(hipDeviceSynchronize(), "sync");
   const auto tot = download<uint64_t>(out.totals, 4);
+  launch_check(tot[3], "mtblx_count_blocks");
   DevBuf ke(4 * tot[0] + 4), ve(4 * tot[0] + 4), kk(tot[1] + 1), vv(tot[2] + 1);
   out.key_end = ke.as<uint32_t>();
   out.val_end = ve.as<uint32_t>();
@@ -157,6 +162,7 @@ inline Decoded decode_batch(const uint8_t* d_data, uint64_t data_len, const uint
   out.vals_cap = tot[2];
   abi_check(mtblx_decode_blocks(&in, &out, ws.p, wsb, nullptr), "mtblx_decode_blocks");
   hip_check(hipDeviceSynchronize(), "sync");
+  launch_check(download<uint64_t>(out.totals, 4)[3], "mtblx_decode_blocks");
   h.nrec = download<uint32_t>(out.nrec, nblk);
   h.status = download<int32_t>(out.status, nblk);
   h.rec_base = download<uint64_t>(out.rec_base, nblk);

@@ -41,6 +41,8 @@ extern "C" {
 #define MTBLX_E_HIP (-2)      /* a HIP runtime call failed                              */
 #define MTBLX_E_NODEV (-3)    /* no gfx950 device visible                               */
 #define MTBLX_E_FORMAT (-4)   /* host-side file/format error (reader API)               */
+#define MTBLX_E_TIMEOUT (-5)  /* a decode launch reported a look-back timeout (totals[3] bit 1) twice:
+                                 its outputs were discarded (synchronous entry points only)  */
 
 /* ---- per-block status (status[b]) ----
  * Exact correspondence with the reference's behaviour on the same bytes:         */
@@ -84,8 +86,17 @@ typedef struct mtblx_decoded {
   uint64_t keys_cap;
   uint8_t* vals;        /* device [vals_cap] */
   uint64_t vals_cap;
-  uint64_t* totals;     /* device [4]: records, key bytes, value bytes, flags (bit0 = overflow,
-                           bit1 = look-back timeout: outputs not trustworthy) */
+  uint64_t* totals;     /* device [4]: records, key bytes, value bytes, flags:
+                             bit0 = some block's outputs overflowed the caller's capacity (its
+                                    status is MTBLX_ST_OVERFLOW; totals[0..2] are still exact)
+                             bit1 = LOOK-BACK TIMEOUT: NOTHING this launch wrote may be used.
+                           The decode is one persistent launch whose workgroups (one per CU) hand
+                           their tiles' output sizes to each other; it relies on all of them being
+                           resident at once.  If another kernel holds CUs for long enough, a bounded
+                           wait gives up and sets bit1.  Every reader surface of this library
+                           (mtblx/codec.py, reader.py, include/mtbl.hpp, mtblx_pipe_decode) checks
+                           it and raises / re-runs; a direct caller must check it too and re-run.
+                           Env MTBLX_DEBUG_FLAGS (test knob): bits ORed into every launch's totals[3]. */
 } mtblx_decoded;
 
 /* Library identity / device check. */
@@ -157,6 +168,9 @@ int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, co
  * block_at_index -> BlockIter::seek(key) -> the first record if its key equals `key`
  * (the next index entry's first record when the seek runs past the block), with the
  * reference's exact BlockIter::seek (src/block.rs:154-194) on the raw index and data blocks.
+ * Quirk kept: when the seek runs past the block and the NEXT block fails Block::init
+ * (InvalidBlock), Reader::get returns the value of the last entry the seek parsed in the old
+ * block (FOUND with that value), or None if it parsed none -- not an error.
  * file: the whole mtbl file on the device; index_off/index_len: the index block content
  * (host-side framing, mtblx_frame_block); verify: check each data block's crc32c as
  * Reader::block does.  keys[key_end[q-1] .. key_end[q]) = query q (device).
@@ -281,6 +295,15 @@ int mtblx_host_alloc(void** p, uint64_t bytes);
 int mtblx_host_free(void* p);
 int mtblx_host_register(void* p, uint64_t bytes);   /* pin an existing range, e.g. an mmap'd file */
 int mtblx_host_unregister(void* p);
+
+/* ---- diagnostic: device copy at the HBM ceiling ----
+ * dst[0 .. bytes) = src[0 .. bytes) (16-byte aligned, bytes % 16 == 0) by a plain gfx950
+ * streaming kernel: 16 B per lane per access, 2^(variant & 3) accesses in flight per lane,
+ * 8 workgroups per CU.  bench.py takes the best of a sweep as this box's copy ceiling, the
+ * reference its roofline fraction is read against besides the 8 TB/s spec.  Asynchronous. */
+#define MTBLX_COPY_NT_STORES 4
+#define MTBLX_COPY_NT_LOADS 8
+int mtblx_stream_copy(void* dst, const void* src, uint64_t bytes, int variant, void* stream);
 
 #ifdef __cplusplus
 }

@@ -911,7 +911,16 @@ int32_t oracle_file_scan(const uint8_t* data, uint64_t len, int32_t verify, int3
       oiter nb;
       int b = oblock_at_index(&r, &idx, &nb);
       if (b == PANIC) { res->end = ORC_END_PANIC; goto out; }
-      if (b <= -10) { res->end = ORC_END_ERR_NEXT; res->err = -10 - b; goto out; }
+      if (b <= -10) {
+        if (mode == 1) {
+          /* Reader::get (src/reader.rs:111-122) matches Some(_) -- this Some(Err) too -- and
+           * returns Ok(ReaderIntoGet::new(iter.bi)): bi is still the OLD iterator (not
+           * reassigned on Err, :376-379), so its last parsed value, or Ok(None) (:195-203) */
+          if (bi.has_val && bi.voff + bi.vlen <= bi.L) oscan_push(&o, bi.key, bi.klen, bi.d + bi.voff, bi.vlen);
+          break;
+        }
+        res->end = ORC_END_ERR_NEXT; res->err = -10 - b; goto out;
+      }
       if (b == 0) break;
       oiter_free(&bi);
       bi = nb;

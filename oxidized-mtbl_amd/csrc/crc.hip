@@ -18,7 +18,7 @@
 
 namespace mtblx_crc {
 
-__global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data, const uint64_t* blk_off,
+__global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data, uint64_t data_len, const uint64_t* blk_off,
                                                             const uint32_t* blk_len, uint32_t nblk, uint32_t* crc_out,
                                                             uint8_t* bad, int framed) {
   __shared__ uint32_t T[256];
@@ -30,10 +30,14 @@ __global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data,
     const uint64_t off = blk_off[b];
     const uint64_t L = blk_len[b];
     const uint8_t* d = data + off;
-    const uint32_t acc = wave_crc32c(d, L, T, lane);
+    // a window past the buffer: the reference's slice panics before the checksum (bad = 1)
+    const bool oob = off + L > data_len;
+    const uint32_t acc = oob ? 0u : wave_crc32c(d, L, T, lane);
     if (lane == 0) {
       if (crc_out) crc_out[b] = acc;
-      if (bad) {
+      if (bad && oob) {
+        bad[b] = 1;
+      } else if (bad) {
         uint32_t stored = 0;
         if (framed && off >= 4)
           stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
@@ -59,7 +63,7 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   }
   const uint32_t need = (in->nblk + 3u) / 4u;
   hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, dim3(need < (uint32_t)grid ? need : (uint32_t)grid),
-                     dim3(mtblx_crc::kThreads), 0, reinterpret_cast<hipStream_t>(stream), in->data, in->blk_off,
+                     dim3(mtblx_crc::kThreads), 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len, in->blk_off,
                      in->blk_len, in->nblk, crc, bad, framed);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

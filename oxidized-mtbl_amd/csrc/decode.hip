@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "crc_dev.h"
@@ -21,6 +23,12 @@ namespace mtblx {
 
 constexpr int kWave = 64;
 constexpr uint64_t kU32Max = 0xFFFFFFFFull;
+// block stage offsets: not staged in LDS (read from HBM)
+constexpr uint32_t kNotStaged = 0xFFFFFFFFu;
+// stage offset of a block whose window [blk_off, blk_off + blk_len) runs past data_len: the
+// reference's slice of it panics (BytesView::slice, src/lib.rs:93-99) -> MTBLX_ST_CORRUPT, and
+// nothing reads it
+constexpr uint32_t kOutOfBounds = 0xFFFFFFFEu;
 
 // ----------------------------------------------------------------------------------
 // small helpers
@@ -236,7 +244,16 @@ __device__ GenOut generic_block(const uint8_t* d, uint64_t L, uint8_t* keys, uin
     next = p + ns + vl;
     if (next == cur) { o.st = MTBLX_ST_LOOP; break; }            // never terminates in the reference
   }
+  // key / value END offsets are u32 relative to the block (include/mtblx.h): a block whose
+  // rebuilt keys or values reach 4 GiB (shared prefixes re-expanded, e.g. a crafted 256 KiB
+  // block) is not representable -> UNSUPPORTED, nothing written (the caller decodes it on the host)
+  if (!WRITE && (o.kb > kU32Max || o.vb > kU32Max)) o = GenOut{0, 0, 0, MTBLX_ST_UNSUPPORTED};
   return o;
+}
+
+// blocks of a tile the exact path must not write: outside the data buffer, or UNSUPPORTED
+__device__ __forceinline__ bool gen_writable(uint32_t bo, int32_t st) {
+  return bo != kOutOfBounds && st != MTBLX_ST_UNSUPPORTED;
 }
 
 // ----------------------------------------------------------------------------------
@@ -259,7 +276,6 @@ __device__ GenOut generic_block(const uint8_t* d, uint64_t L, uint8_t* keys, uin
 // agent-scope atomic per tile (the value IS the flag; no fences), <= 4 loads per thread,
 // issued before walk 2 and consumed after it.
 
-constexpr uint32_t kNotStaged = 0xFFFFFFFFu;
 constexpr int kThreads = 256;
 constexpr int kMaxLookbackLoads = 4;               // G - 1 <= 4 * 256
 constexpr uint64_t kReady = 1ull << 63;
@@ -335,7 +351,7 @@ struct TileArgs {
   uint8_t* vals;
   uint64_t vals_cap;
   uint64_t* totals;
-  uint64_t* lbw;    // workspace tile entries: 3 u64 per tile {agg parity 0, agg parity 1, exact key bytes}
+  uint64_t* lbw;    // workspace tile entries: kTileWords u64 per tile (lb_slot / lbx_slot)
   struct WsHdr* hdr;
   uint64_t* dbg;    // [16] phase stamps (diagnostic build only)
   int write;
@@ -346,6 +362,7 @@ struct TileArgs {
   uint32_t wscap;   // tile entries the workspace holds (from workspace_bytes)
   uint32_t par;     // launch parity: aggregates live in slot `par` of each tile entry
   uint32_t hw_other;
+  unsigned long long inject;   // debug: bits ORed into totals[3] (MTBLX_DEBUG_FLAGS, mtblx_impl_run)
 };
 
 // Workspace header (byte 128 of the workspace).  The workspace carries state from call to
@@ -361,8 +378,13 @@ struct WsHdr {
   unsigned long long flags;   // bit0 overflow, bit1 look-back timeout (-> totals[3])
 };
 
-__device__ __forceinline__ uint64_t* lb_slot(const TileArgs& a, uint64_t t) { return a.lbw + 3 * t + a.par; }
-__device__ __forceinline__ uint64_t* lbx_slot(const TileArgs& a, uint64_t t) { return a.lbw + 3 * t + 2; }
+// workspace tile entry t: {packed aggregate of launch parity 0, of parity 1, exact key bytes,
+// exact records | exact value bytes << 32}.  The exact words are written only when a field of
+// the packed word saturates (pack_agg).
+constexpr int kTileWords = 4;
+__device__ __forceinline__ uint64_t* lb_slot(const TileArgs& a, uint64_t t) { return a.lbw + kTileWords * t + a.par; }
+__device__ __forceinline__ uint64_t* lbx_slot(const TileArgs& a, uint64_t t) { return a.lbw + kTileWords * t + 2; }
+__device__ __forceinline__ uint64_t* lbx2_slot(const TileArgs& a, uint64_t t) { return a.lbw + kTileWords * t + 3; }
 
 // kernel prologue: pick the parity, clear the other parity's slots of every tile a previous
 // launch of that parity used (the next launch uses them)
@@ -373,7 +395,7 @@ __device__ __forceinline__ void ws_begin(TileArgs& a) {
   if (a.hw_other > a.wscap) a.hw_other = a.wscap;   // never write past the caller's workspace
   const uint32_t n = blockDim.x, tid = threadIdx.x;
   for (uint64_t t = (uint64_t)blockIdx.x * n + tid; t < a.hw_other; t += (uint64_t)gridDim.x * n)
-    a.lbw[3 * t + (a.par ^ 1u)] = 0;
+    a.lbw[kTileWords * t + (a.par ^ 1u)] = 0;
 }
 
 __device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bit) { atomicOr(&a.hdr->flags, bit); }
@@ -395,7 +417,7 @@ __device__ __forceinline__ void ws_end(const TileArgs& a) {
     if (old == gridDim.x - 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const unsigned long long f = __hip_atomic_load(&a.hdr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.totals[3] = f;
+      a.totals[3] = f | a.inject;
       __hip_atomic_store(&a.hdr->flags, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t h = __hip_atomic_load(&a.hdr->hw[a.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.ntiles > h) __hip_atomic_store(&a.hdr->hw[a.par], a.ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -558,8 +580,44 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
-__device__ __forceinline__ uint64_t pack_agg(uint32_t r, uint32_t k, uint32_t v) {
-  return kReady | ((uint64_t)r << 42) | ((uint64_t)v << 21) | (uint64_t)(k < kField ? k : kField);
+// Publish the aggregate (records r, key bytes k, value bytes v) of tile t: one packed 8-byte
+// agent-scope word, ready | r << 42 | v << 21 | k (21 bits each).  If any of the three does not
+// fit its field, the exact values go to the tile's side words first (release-ordered) and the
+// packed word carries the marker k == kField; lb_take then reads all three from the side words.
+// (A tile can hold one block of up to 4 GiB: k_decode_tiles, or an unstaged block.)
+__device__ __forceinline__ void lb_publish(const TileArgs& a, uint64_t t, uint32_t r, uint64_t k, uint32_t v) {
+  uint64_t w;
+  if (r >= kField || v >= kField || k >= kField) {
+    __hip_atomic_store(lbx_slot(a, t), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(lbx2_slot(a, t), (uint64_t)r | ((uint64_t)v << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the side words are performed before the flag word
+    w = kReady | ((uint64_t)kField << 42) | ((uint64_t)kField << 21) | (uint64_t)kField;
+  } else {
+    w = kReady | ((uint64_t)r << 42) | ((uint64_t)v << 21) | k;
+  }
+  __hip_atomic_store(lb_slot(a, t), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Add the aggregate of tile i (its ready packed word w) to the running sums.
+__device__ __forceinline__ void lb_take(const TileArgs& a, uint64_t i, uint64_t w, uint64_t& sr, uint64_t& sk,
+                                        uint64_t& sv) {
+  uint64_t r = (w >> 42) & kField, v = (w >> 21) & kField, k = w & kField;
+  if (k == kField) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    k = __hip_atomic_load(lbx_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t x = __hip_atomic_load(lbx2_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r = (uint32_t)x;
+    v = x >> 32;
+  }
+  sr += r;
+  sk += k;
+  sv += v;
+}
+
+// wave-wide sum of per-lane look-back sums (32-bit adds unless some lane saw an exact word)
+__device__ __forceinline__ uint64_t lb_wave_sum(uint64_t x) {
+  return __ballot(x >= (1ull << 24)) == 0ull ? (uint64_t)wave_sum32((uint32_t)x) : wave_sum64(x);
 }
 
 template <class C>
@@ -628,7 +686,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
       if (tid < (int)nb) {
         const uint64_t off = a.blk_off[b0 + tid];
         const uint32_t L = a.blk_len[b0 + tid];
-        S.boff[tid] = (off >= r0 && off + L <= r1) ? (uint32_t)(16 + off - r0) : kNotStaged;
+        S.boff[tid] = off + L > a.data_len ? kOutOfBounds
+                      : (off >= r0 && off + L <= r1) ? (uint32_t)(16 + off - r0) : kNotStaged;
         S.blen[tid] = L;
       }
     } else {
@@ -638,7 +697,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         const uint64_t off = a.blk_off[b0 + j];
         const uint32_t so = 16u + j * a.slot;
         uint32_t bo = kNotStaged;
-        if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)C::TB) bo = so + stage_slot(a, S.stage + so, off, L, lane);
+        if (off + L > a.data_len) bo = kOutOfBounds;
+        else if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)C::TB) bo = so + stage_slot(a, S.stage + so, off, L, lane);
         if (lane == 0) { S.boff[j] = bo; S.blen[j] = L; }
       }
     }
@@ -665,7 +725,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
       uint32_t n = 0, R = 0, ok = 0;
       if (lane < (int)nb) {
         const uint32_t j = lane, L = S.blen[j], bo = S.boff[j];
-        if (bo != kNotStaged && L >= 8) {
+        if (bo < kOutOfBounds && L >= 8) {
           n = lds_rd32(S.stage, bo + L - 4);
           if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
         }
@@ -680,7 +740,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         S.bn[lane] = n;
         S.bR[lane] = R;
         S.bok[lane] = ok;
-        S.bwr[lane] = 1;
+        S.bwr[lane] = S.boff[lane] != kOutOfBounds;
         S.bst[lane] = MTBLX_ST_OK;
         S.bint0[lane] = incl - n;
       }
@@ -714,11 +774,13 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
     if (tid < (int)nb && !S.bok[tid]) {
       const uint32_t j = tid, bo = S.boff[j], L = S.blen[j];
       const uint8_t* d = (bo != kNotStaged) ? (S.stage + bo) : (a.data + a.blk_off[b0 + j]);
-      GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
+      const GenOut o = bo == kOutOfBounds ? GenOut{0, 0, 0, MTBLX_ST_CORRUPT}
+                                          : generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
       S.bcnt[j] = o.nrec;
       S.bkb[j] = (uint32_t)o.kb;
       S.bvb[j] = (uint32_t)o.vb;
       S.bst[j] = o.st;
+      if (!gen_writable(bo, o.st)) S.bwr[j] = 0;
     }
     // interval scan (regular blocks only) -> exclusive bases
     {
@@ -761,13 +823,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
 
     // ---- 5. publish the tile aggregate, issue the look-back loads ----
     const uint32_t agg_r = S.ttot[0], agg_k = S.ttot[1], agg_v = S.ttot[2];
-    if (tid == 0) {
-      if (agg_k >= kField) {
-        __hip_atomic_store(lbx_slot(a, t), (uint64_t)agg_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      }
-      __hip_atomic_store(lb_slot(a, t), pack_agg(agg_r, agg_k, agg_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid == 0) lb_publish(a, t, agg_r, agg_k, agg_v);
     const uint32_t lo = (t >= G) ? t - G + 1 : 0;   // window of predecessors [lo, t)
     uint64_t lw[kMaxLookbackLoads];
 #pragma unroll
@@ -834,23 +890,13 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
           w = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (++spins > (1u << 22)) { timeout = true; w = kReady; }
         }
-        if (i >= (int64_t)lo) {
-          sr += (w >> 42) & kField;
-          sv += (w >> 21) & kField;
-          uint64_t kk = w & kField;
-          if (kk == kField) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            kk = __hip_atomic_load(lbx_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          sk += kk;
-        }
+        if (i >= (int64_t)lo) lb_take(a, (uint64_t)i, w, sr, sk, sv);
       }
       if (timeout) ws_flag(a, 2ull);
-      // per-thread sums are < 2^23 (4 tiles x 21-bit fields) unless a key field saturated
-      sr = wave_sum32((uint32_t)sr);
-      sv = wave_sum32((uint32_t)sv);
-      if (__ballot(sk >= (1ull << 24)) == 0ull) sk = wave_sum32((uint32_t)sk);
-      else sk = wave_sum64(sk);
+      // per-thread sums are < 2^23 (4 tiles x 21-bit fields) unless a tile published exact words
+      sr = lb_wave_sum(sr);
+      sv = lb_wave_sum(sv);
+      sk = lb_wave_sum(sk);
       if (lane == 0) { S.lbsum[wv][0] = sr; S.lbsum[wv][1] = sk; S.lbsum[wv][2] = sv; }
       __syncthreads();
       if (tid == 0) {
@@ -1288,7 +1334,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
         *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
     }
     if (part == 0 && lane < (int)nb) {
-      B.boff[lane] = (uint32_t)(16 + off_l - r0);
+      B.boff[lane] = off_l + len_l > a.data_len ? kOutOfBounds : (uint32_t)(16 + off_l - r0);
       B.blen[lane] = len_l;
     }
   } else if (mlo == 0) {
@@ -1299,7 +1345,9 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
       const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)len_l, (int)j);
       const uint32_t so = 16u + j * a.slot;
       uint32_t bo = kNotStaged;
-      if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)P::TB) {
+      if (off + L > a.data_len) {
+        bo = kOutOfBounds;
+      } else if (L + 15u <= a.slot && so + a.slot + 32u <= (uint32_t)P::TB) {
         uint64_t a0 = ((base + off) & ~15ull) - base;
         if (base + off < 16 || ((base + off) & ~15ull) < base) a0 = off;  // unaligned data base: not reached
         const uint32_t delta = (uint32_t)(off - a0);
@@ -1334,7 +1382,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   if (lane < (int)nb) {
     L = B.blen[lane];
     bo = B.boff[lane];
-    if (bo != kNotStaged && L >= 8) {
+    if (bo < kOutOfBounds && L >= 8) {
       n = lds_rd32(B.stage, bo + L - 4);
       if (n != 0 && (uint64_t)(n + 1ull) * 4ull <= L) { R = L - 4u * (n + 1u); ok = 1; }
     }
@@ -1382,9 +1430,11 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   int32_t gst = MTBLX_ST_OK;
   if (lane < (int)nb && !ok) {
     const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + lane]);
-    const GenOut o = generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
+    const GenOut o = bo == kOutOfBounds ? GenOut{0, 0, 0, MTBLX_ST_CORRUPT}
+                                        : generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
     gc = o.nrec; gk = (uint32_t)o.kb; gv = (uint32_t)o.vb; gst = o.st;
   }
+  const uint32_t gwr = ok || gen_writable(bo, gst);
   // interval scan over regular blocks (one interval per lane)
   const bool reg = fl && jok;
   const uint32_t c = reg ? cnt : 0u, k = reg ? kb : 0u, v = reg ? vb : 0u;
@@ -1394,11 +1444,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)ik, 63) + wave_sum32(gk);
   const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)iv, 63) + wave_sum32(gv);
   if (lane == 0) {
-    if (tk >= kField) {
-      __hip_atomic_store(lbx_slot(a, t), (uint64_t)tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
-    __hip_atomic_store(lb_slot(a, t), pack_agg(tr, tk, tv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lb_publish(a, t, tr, tk, tv);
     B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
     B.nint = nint;
   }
@@ -1411,7 +1457,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
     const uint32_t tkk = n0 ? (uint32_t)__builtin_amdgcn_readlane((int)ik, (int)n0 - 1) : 0u;
     const uint32_t tvv = n0 ? (uint32_t)__builtin_amdgcn_readlane((int)iv, (int)n0 - 1) : 0u;
     if (lane == 0) {
-      B.bok[0] = ok; B.bwr[0] = 1; B.bst[0] = ok ? MTBLX_ST_OK : gst;
+      B.bok[0] = ok; B.bwr[0] = gwr; B.bst[0] = ok ? MTBLX_ST_OK : gst;
       B.bcnt[0] = ok ? tc : gc; B.bkb[0] = ok ? tkk : gk; B.bvb[0] = ok ? tvv : gv;
       B.brb[0] = 0; B.bkbb[0] = 0; B.bvbb[0] = 0;
     }
@@ -1440,7 +1486,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   const uint32_t jc = wave_incl_scan(bc), jk = wave_incl_scan(bk), jv = wave_incl_scan(bv);
   const uint32_t brb = jc - bc, bkbb = jk - bk, bvbb = jv - bv;
   if (lane < (int)nb) {
-    B.bok[lane] = ok; B.bwr[lane] = 1; B.bst[lane] = ok ? MTBLX_ST_OK : gst;
+    B.bok[lane] = ok; B.bwr[lane] = gwr; B.bst[lane] = ok ? MTBLX_ST_OK : gst;
     B.bcnt[lane] = bc; B.bkb[lane] = bk; B.bvb[lane] = bv;
     B.brb[lane] = brb; B.bkbb[lane] = bkbb; B.bvbb[lane] = bvbb;
   }
@@ -1515,20 +1561,12 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
       if (++spins > (1u << 22)) { timeout = true; w = kReady; }
     }
     if (i < lo) continue;
-    sr += (w >> 42) & kField;
-    sv += (w >> 21) & kField;
-    uint64_t kk = w & kField;
-    if (kk == kField) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      kk = __hip_atomic_load(lbx_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    sk += kk;
+    lb_take(a, (uint64_t)i, w, sr, sk, sv);
   }
   if (timeout) ws_flag(a, 2ull);
-  sr = wave_sum32((uint32_t)sr);
-  sv = wave_sum32((uint32_t)sv);
-  if (__ballot(sk >= (1ull << 24)) == 0ull) sk = wave_sum32((uint32_t)sk);
-  else sk = wave_sum64(sk);
+  sr = lb_wave_sum(sr);
+  sv = lb_wave_sum(sv);
+  sk = lb_wave_sum(sk);
   const uint64_t pr = tinc[0] + sr, pk = tinc[1] + sk, pv = tinc[2] + sv;
   tinc[0] = pr + B.ttot[0];
   tinc[1] = pk + B.ttot[1];
@@ -1706,11 +1744,13 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
 #endif
 }
 
-__device__ __forceinline__ void wait_flag(const uint32_t* flag, uint32_t want) {
+// Wait for a workgroup-local LDS counter.  Bounded: giving up means this launch's outputs are
+// not trustworthy (look-back / hand-off timeout, totals[3] bit 1), never a hang.
+__device__ __forceinline__ void wait_flag(const TileArgs& a, const uint32_t* flag, uint32_t want) {
   uint32_t spins = 0;
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 24)) break;
+    if (++spins > (1u << 24)) { ws_flag(a, 2ull); break; }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
@@ -1723,7 +1763,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
   if (fb < nint) {
     const CopyRow r = copy_prepare(B, fb, lane);
     ST.hit(14);
-    wait_flag(ready, want);
+    wait_flag(a, ready, want);
     ST.hit(0);
     if (a.write) copy_emit(B, a, r, lane);
     for (fb += P::ROWS; fb < nint; fb += P::ROWS) {   // wave-uniform
@@ -1731,7 +1771,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
       if (a.write) copy_emit(B, a, r2, lane);
     }
   } else {
-    wait_flag(ready, want);
+    wait_flag(a, ready, want);
     ST.hit(0);
   }
   // irregular blocks: exact serial write (thread per block)
@@ -1772,14 +1812,14 @@ __device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, 
   uint32_t total = 0;
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t L = B.blen[j];
-    total += (B.boff[j] != kNotStaged && L >= 4u) ? (L + 63u) / 64u : 0u;
+    total += (B.boff[j] < kOutOfBounds && L >= 4u) ? (L + 63u) / 64u : 0u;
   }
   // per-lane chunk prefix of the tile's blocks (lane j < nb holds the first chunk of block j)
   uint32_t mych = 0, myL = 0, mybo = 0;
   if (lane < (int)nb) {
     myL = B.blen[lane];
     mybo = B.boff[lane];
-    mych = (mybo != kNotStaged && myL >= 4u) ? (myL + 63u) / 64u : 0u;
+    mych = (mybo < kOutOfBounds && myL >= 4u) ? (myL + 63u) / 64u : 0u;
   }
   const uint32_t incl = wave_incl_scan(mych), excl = incl - mych;
   constexpr int kCh = 2;   // chunks in flight per lane (register budget: 128 VGPRs at 16 waves/CU)
@@ -1838,9 +1878,9 @@ __device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, 
   if (lane < (int)nb) {
     L = B.blen[lane];
     o = B.boff[lane];
-    if (o != kNotStaged && L >= 4u) {
+    if (o < kOutOfBounds && L >= 4u) {
       crc = S.cacc[par][lane] ^ 0xFFFFFFFFu;
-    } else if (o != kNotStaged) {   // < 4 bytes: byte-wise with the init
+    } else if (o < kOutOfBounds) {   // < 4 bytes: byte-wise with the init
       uint32_t x = 0xFFFFFFFFu;
       for (uint32_t t = 0; t < L; ++t) x = S.crcT[0][(x ^ B.stage[o + t]) & 0xffu] ^ (x >> 8);
       crc = x ^ 0xFFFFFFFFu;
@@ -1860,7 +1900,9 @@ __device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, 
     if (a.crc_bad) {
       uint8_t bad = 0;
       const uint64_t off = a.blk_off[b];
-      if (a.crc_framed && off >= 4) {
+      if (o == kOutOfBounds) {
+        bad = 1;   // the reference's slice of the block panics before its checksum
+      } else if (a.crc_framed && off >= 4) {
         const uint8_t* d = a.data + off;
         const uint32_t stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
         bad = stored != crc;
@@ -1944,7 +1986,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           const bool late = it >= 1 && 3ull * N.ttot[1] <= (uint64_t)N.ttot[2];
           pipe_dma(N, a, tc + G, ioff, ilen, lane, part, 0, late ? kLargeDmaSplit : 0xFFFFFFFFu);
           if (late) {
-            wait_flag(&S.pub, it + 1);
+            wait_flag(a, &S.pub, it + 1);
             pipe_dma(N, a, tc + G, ioff, ilen, lane, part, kLargeDmaSplit);
           }
           load_info(it + 2);
@@ -1954,13 +1996,13 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+1 (read next phase)
         ST.hit(6);
       } else if (wv == 1) {
-        wait_flag(&S.pub, it + 1);
+        wait_flag(a, &S.pub, it + 1);
         pipe_lookback_issue(a, tc, G, lbv, lane);
         pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, it + 1);
         ST.hit(1);
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
-        wait_flag(&S.pub, it + 1);
+        wait_flag(a, &S.pub, it + 1);
         pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, it + 1, ST);
         ST.hit(7);
       }
@@ -2005,7 +2047,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           uint32_t spins = 0;
           while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) break;
+            if (++spins > (1u << 24)) { ws_flag(a, 2ull); break; }
           }
           pipe_lookback_issue(a, tc + G, G, lbv, lane);
           pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
@@ -2146,15 +2188,22 @@ extern "C" int mtblx_dbg_timeline(uint64_t* out, uint32_t nwg) {   // diagnostic
 }
 #endif
 
-extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 24u + 64u; }
+extern "C" size_t mtblx_impl_ws_bytes(uint32_t nblk) { return 256u + (size_t)nblk * 8u * kTileWords + 64u; }
 
 extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed,
                                    void* stream);
 
+// MTBLX_DEBUG_FLAGS (test knob): bits ORed into totals[3] at the end of every decode launch,
+// e.g. 2 = report a look-back timeout, to check that every reader surface rejects such a launch.
+static unsigned long long debug_flags() {
+  const char* e = getenv("MTBLX_DEBUG_FLAGS");
+  return e ? strtoull(e, nullptr, 0) : 0ull;
+}
+
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t ws_bytes,
                               int write, hipStream_t s, int verify, uint32_t* crc, uint8_t* crc_bad, int framed) {
   const uint32_t nblk = in->nblk;
-  const uint64_t cap64 = ws_bytes > 320u ? (ws_bytes - 320u) / 24u : 0u;
+  const uint64_t cap64 = ws_bytes > 320u ? (ws_bytes - 320u) / (8u * kTileWords) : 0u;
   const uint32_t wscap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;
   const Plan p = make_plan(nblk, in->max_blk_len);
   uint64_t* dbg = reinterpret_cast<uint64_t*>(ws);
@@ -2164,7 +2213,7 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
              p.ntiles,     out->nrec,     out->rec_base, out->key_base, out->val_base, out->status, out->key_end,
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
              lbw,          hdr,           dbg,          write ? 1 : 0, crc,         crc_bad,       framed ? 1 : 0,
-             wscap,        0,             0};
+             wscap,        0,             0,            debug_flags()};
   if (p.kind == 0) {
     if (verify)
       hipLaunchKernelGGL(k_decode_pipe<PipeSmallV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);

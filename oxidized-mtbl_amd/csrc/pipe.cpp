@@ -466,14 +466,20 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
       for (uint32_t j = 0; j < c.nb; ++j)
         if (s.hz[j] != MTBLX_SNAPPY_OK) zerr[c.b0 + j] = 1;
     uint64_t nr = s.htot[0], kb = s.htot[1], vb = s.htot[2];
-    if (s.htot[3] & 1ull) {
-      // the slot's output capacity was too small (keys far longer than the block bytes):
-      // totals hold the exact sizes, so grow the slot and decode the chunk again
+    if (s.htot[3] & 3ull) {
+      // bit 0: the slot's output capacity was too small (keys far longer than the block bytes):
+      // totals hold the exact sizes, so grow the slot and decode the chunk again.
+      // bit 1: the launch's look-back timed out (mtblx.h): its outputs are discarded and the
+      // chunk is decoded again as a fresh launch; a second timeout fails the call.
       Caps c2 = s.cap;
-      c2.rec = std::max(c2.rec, nr + 1);
-      c2.keys = std::max(c2.keys, kb + 64);
-      c2.vals = std::max(c2.vals, vb + 64);
-      if (hipStreamSynchronize(p->s_d2h) != hipSuccess || alloc_outputs(s, c2) != MTBLX_OK) return MTBLX_E_HIP;
+      if (s.htot[3] & 1ull) {
+        c2.rec = std::max(c2.rec, nr + 1);
+        c2.keys = std::max(c2.keys, kb + 64);
+        c2.vals = std::max(c2.vals, vb + 64);
+      }
+      const bool grow = (s.htot[3] & 1ull) != 0;
+      if (hipStreamSynchronize(p->s_d2h) != hipSuccess || (grow && alloc_outputs(s, c2) != MTBLX_OK))
+        return MTBLX_E_HIP;
       mtblx_block_batch in{s.d + s.data_at(), std::max<uint64_t>(compression == 0 ? c.hi - c.lo : c.ubytes, 1),
                            reinterpret_cast<const uint64_t*>(s.d),
                            reinterpret_cast<const uint32_t*>(s.d + 8 * s.cap.blocks), c.nb, c.maxlen};
@@ -488,6 +494,7 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
       nr = s.htot[0];
       kb = s.htot[1];
       vb = s.htot[2];
+      if (s.htot[3] & 2ull) return MTBLX_E_TIMEOUT;
     }
     flags |= s.htot[3] & ~1ull;
     hipStream_t so = p->s_d2h;

@@ -114,6 +114,7 @@ struct It {
   uint64_t current, next, klen, kcap, c, voff, vlen;
   int cmp;            // sign of key[c] - target[c] when c < min(klen, tlen), else 0
   bool has_next;
+  bool has_val;       // `val` is Some: an entry has been parsed (src/block.rs:70-71, :136)
 };
 
 enum { R_OK = 1, R_END = 0, R_PANIC = -1, R_LOOP = -2 };
@@ -215,6 +216,7 @@ __device__ int parse_next_key(const Blk& b, It& it, const uint8_t* t, uint64_t t
   it.next = p + ns + vl;
   it.voff = p + ns;
   it.vlen = vl;
+  it.has_val = true;
   if (it.next == it.current && it.current == prev) return R_LOOP;
   return R_OK;
 }
@@ -250,7 +252,7 @@ __device__ __forceinline__ bool valid(const Blk& b, const It& it) { return it.cu
 // BlockIter::init (src/block.rs:75-93)
 __device__ __forceinline__ int iter_init(const Blk& b, It& it) {
   if (b.n == 0) return R_PANIC;
-  it.current = b.R; it.has_next = false; it.next = 0;
+  it.current = b.R; it.has_next = false; it.next = 0; it.has_val = false;
   it.klen = 0; it.kcap = 0; it.c = 0; it.cmp = 0; it.voff = 0; it.vlen = 0;
   return R_OK;
 }
@@ -336,7 +338,15 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
       if (!valid(ib, ii)) break;
       b = block_at_index(f, ib, ii, db);
       if (b == R_PANIC) { res = MTBLX_GET_PANIC; break; }
-      if (b == 2) { res = MTBLX_GET_ERR; break; }                  // Some(Err) from next()
+      if (b == 2) {
+        // next() returned Some(Err(InvalidBlock)).  Reader::get matches Some(_) and returns
+        // Ok(ReaderIntoGet::new(iter.bi)) with iter.bi still the OLD block iterator (it is not
+        // reassigned on Err, src/reader.rs:111-122, :376-379): its `val` is the last entry the
+        // seek parsed -> Ok(Some(that value)), or Ok(None) if the seek parsed none (:195-203).
+        // block_at_index left db untouched (Block::init failed before assigning it).
+        if (di.has_val) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - file) + di.voff; rl = di.vlen; }
+        break;
+      }
       if (b == 0) break;
       if (iter_init(db, di) != R_OK) { res = MTBLX_GET_PANIC; break; }
       restart_at(db, di, 0);                                       // seek_to_first

@@ -18,19 +18,25 @@ int main(int argc, char** argv) {
     return 2;
   }
   const mtbl::Bytes data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  const mtbl::Reader reader = mtbl::Reader::open(data);   // Reader::new(mmap).unwrap()
-  mtbl::ReaderIntoIter iter = reader.into_iter();
   std::string out;
-  while (auto r = iter.next()) {   // examples/dump.rs:14-20
-    out += '"';
-    out.append(reinterpret_cast<const char*>(r->key), r->key_len);
-    out += "\" \"";
-    out.append(reinterpret_cast<const char*>(r->val), r->val_len);
-    out += "\"\n";
-    if (out.size() > (1u << 20)) {
-      std::fwrite(out.data(), 1, out.size(), stdout);
-      out.clear();
+  try {
+    const mtbl::Reader reader = mtbl::Reader::open(data);   // Reader::new(mmap).unwrap()
+    mtbl::ReaderIntoIter iter = reader.into_iter();
+    while (auto r = iter.next()) {   // examples/dump.rs:14-20
+      out += '"';
+      out.append(reinterpret_cast<const char*>(r->key), r->key_len);
+      out += "\" \"";
+      out.append(reinterpret_cast<const char*>(r->val), r->val_len);
+      out += "\"\n";
+      if (out.size() > (1u << 20)) {
+        std::fwrite(out.data(), 1, out.size(), stdout);
+        out.clear();
+      }
     }
+  } catch (const std::exception& e) {   // the reference's unwrap() / panic: message, non-zero exit
+    std::fwrite(out.data(), 1, out.size(), stdout);
+    std::fprintf(stderr, "dump: %s\n", e.what());
+    return 1;
   }
   std::fwrite(out.data(), 1, out.size(), stdout);
   return 0;

@@ -17,7 +17,7 @@ u32p = C.POINTER(C.c_uint32)
 u64p = C.POINTER(C.c_uint64)
 i32p = C.POINTER(C.c_int32)
 
-MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT = 0, -1, -2, -3, -4
+MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT, MTBLX_E_TIMEOUT = 0, -1, -2, -3, -4, -5
 ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW, ST_DECOMPRESS = range(7)
 SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL = range(3)
 DIR_OK, DIR_PANIC, DIR_UNSUPPORTED = range(3)
@@ -33,7 +33,7 @@ EXPORTS = [
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
     "mtblx_pipe_decode", "mtblx_pipe_set", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
-    "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev",
+    "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
@@ -152,6 +152,8 @@ def lib() -> C.CDLL:
                                                   C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                                   C.c_void_p]
         L.mtblx_snappy_decompress_dev.restype = C.c_int
+        L.mtblx_stream_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
+        L.mtblx_stream_copy.restype = C.c_int
         L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]
         L.mtblx_host_alloc.restype = C.c_int
         L.mtblx_host_free.argtypes = [C.c_void_p]

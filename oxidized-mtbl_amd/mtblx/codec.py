@@ -18,6 +18,15 @@ from ._lib import BlockBatch, Decoded
 
 _checked_devices = set()
 
+FLAG_OVERFLOW = 1      # totals[3] bit 0: some block's outputs did not fit (status MTBLX_ST_OVERFLOW)
+FLAG_TIMEOUT = 2       # totals[3] bit 1: the launch's look-back timed out -- nothing it wrote is valid
+
+
+class LaunchTimeout(RuntimeError):
+    """A decode / encode launch reported a look-back timeout (include/mtblx.h, totals[3] bit 1):
+    its persistent workgroups lost co-residency (another kernel held CUs) and its outputs are
+    not trustworthy.  Re-run the call."""
+
 
 def _require_device():
     """The library handle, after checking (once per device) that the current device is a
@@ -95,8 +104,12 @@ class DecodedBlocks:
         return c
 
     # ---------------- host views ----------------
-    def totals_host(self):
+    def totals_host(self, check: bool = True):
+        """(records, key bytes, value bytes, flags); raises LaunchTimeout if the launch that
+        wrote them timed out (check=False returns the raw flags)."""
         t = self.totals.cpu().numpy().view(np.uint64)
+        if check and int(t[3]) & FLAG_TIMEOUT:
+            raise LaunchTimeout("mtblx decode launch: look-back timeout, outputs discarded (re-run)")
         return int(t[0]), int(t[1]), int(t[2]), int(t[3])
 
     def to_host(self) -> "HostDecoded":

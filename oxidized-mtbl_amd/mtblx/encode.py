@@ -88,6 +88,12 @@ class Encoded:
     status: torch.Tensor    # int32 MTBLX_ST_*
     totals: torch.Tensor    # int64 [2]: bytes, flags
 
+    def check(self) -> "Encoded":
+        """raise codec.LaunchTimeout if the encode launch's look-back timed out (totals[1] bit 1)"""
+        if int(self.totals[1].item()) & codec.FLAG_TIMEOUT:
+            raise codec.LaunchTimeout("mtblx_encode_blocks: look-back timeout, outputs discarded (re-run)")
+        return self
+
     def batch(self) -> codec.DeviceBatch:
         """the encoded blocks as a decode batch (mtblx_decode_blocks input)"""
         ml = int(self.blk_len.max().item()) if self.blk_len.numel() else 0

@@ -92,6 +92,8 @@ class HostPipe:
         ln = np.ascontiguousarray(blk_len, np.uint32)
         rc = _lib.lib().mtblx_pipe_decode(self._p, f.ctypes.data, f.size, int(compression), off.ctypes.data,
                                           ln.ctypes.data, off.size, C.byref(out.c), C.byref(self.stats))
+        if rc == _lib.MTBLX_E_TIMEOUT:
+            raise codec.LaunchTimeout("mtblx_pipe_decode: a chunk's decode timed out twice (look-back)")
         if rc != 0:
             raise RuntimeError(f"mtblx_pipe_decode failed: {rc}")
         return self.stats

@@ -18,12 +18,13 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests 900 python -m pytest tests -m gpu -x -q
+  step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py
+  step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e
   find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \; | head -20
 fi

@@ -137,3 +137,27 @@ def test_get_batch_corrupted(oracle):
         qs = [recs[int(i)][0] for i in rng.integers(0, len(recs), 40)] + [b"", b"\xff" * 20]
         for verify in (True, False):
             _check_get(oracle, bytes(d), qs, verify=verify)
+
+
+def test_get_stale_value_when_next_block_invalid(oracle):
+    """ADVICE r1: Reader::get whose seek runs past a block while the NEXT block fails Block::init
+    returns Ok(Some(value of the last entry the seek parsed in the old block)) -- the crate's
+    match on Some(_) (src/reader.rs:111-122) -- not an error."""
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(30)
+    raw = bytearray(bytes(data))
+    b = 11
+    e = int(off[b]) + int(ln[b])
+    for n in (0xFFFFFFFF, 0x80000000, 0x40000001, 0x3FFFFFFF, int(ln[b]) // 4 + 1):
+        blk = bytes(raw[int(off[b]):e - 4]) + n.to_bytes(4, "little")
+        if oracle.decode_block(blk)[0] == 1:       # Block::init -> None (InvalidBlock)
+            raw[e - 4:e] = n.to_bytes(4, "little")
+            break
+    else:
+        pytest.skip("no restart count gives InvalidBlock for this block")
+    recs = oracle.file_scan(bytes(data), "iter")["records"]
+    prev_last = [k for k, _ in recs][:int(synth.cfg2_file.last_block_nrec[:b].sum())][-1]
+    qs = [prev_last + b"\x00", prev_last + b"\x00\x01", prev_last, recs[0][0]]
+    stale = oracle.file_scan(bytes(raw), "get", key=qs[0], verify=False)
+    assert stale["end"] == 0 and len(stale["records"]) == 1    # Ok(Some(stale value))
+    _check_get(oracle, bytes(raw), qs, verify=False)

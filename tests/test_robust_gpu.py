@@ -1,0 +1,145 @@
+"""Robustness of the device decode: launches that must never hand back wrong records.
+
+- A tile whose aggregate does not fit the packed look-back word (>= 2^21 value bytes or records in
+  one tile: one block > 64 KiB is one tile of k_decode_tiles) publishes exact side words; every
+  later tile's bases must still equal the oracle's.
+- A look-back timeout (include/mtblx.h, totals[3] bit 1) is rejected by every reader surface:
+  codec (Python), Reader (Python), HostPipe (C ABI, synchronous: re-runs the chunk once, then
+  MTBLX_E_TIMEOUT) and the C++ surface (include/mtbl.hpp, through the `dump` example).  The
+  timeout is injected with the library's MTBLX_DEBUG_FLAGS test knob.
+- A block window past the end of the data buffer: the reference's slice panics (CORRUPT), the
+  device reads nothing outside the buffer, and the framed checksum check reports it bad.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import corpus
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _codec():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mtblx import codec
+    return codec
+
+
+def _decode(data, off, ln):
+    codec = _codec()
+    import torch
+    out = codec.decode_blocks(codec.DeviceBatch.from_host(data, off, ln))
+    torch.cuda.synchronize()
+    return out.to_host()
+
+
+def _assert_same(dev, orc):
+    for k in ("status", "nrec", "rec_base", "key_base", "val_base", "key_end", "val_end", "keys", "vals"):
+        a, b = getattr(dev, k), getattr(orc, k)
+        assert np.array_equal(a, b), (k, np.nonzero(a != b)[0][:8] if a.shape == b.shape else (a.shape, b.shape))
+    assert dev.totals[3] == 0
+
+
+def test_tile_aggregate_exact_words(oracle):
+    """an early block holding a >= 2 MiB value, and one holding >= 2^21
+    records, ahead of ordinary blocks in the same batch."""
+    rng = np.random.default_rng(41)
+    big_val = oracle.build_block([(b"k0", rng.integers(0, 256, (5 << 19) + 77, dtype=np.uint8).tobytes()),
+                                  (b"k1", b"v")])
+    n = (1 << 21) + 4321
+    many = oracle.build_block([(i.to_bytes(3, "big"), b"") for i in range(n)])
+    rest = corpus.builder_blocks(oracle, seed=42, count=30, max_bytes=9000)
+    blocks = [big_val, rest[0], many] + rest[1:]
+    data, off, ln = corpus.pack(blocks, rng=rng)
+    orc = oracle.decode_blocks(data, off, ln)
+    assert int(orc.nrec[2]) == n and int(orc.val_base[1] - orc.val_base[0]) >= (1 << 21)
+    _assert_same(_decode(data, off, ln), orc)
+
+
+def test_window_past_buffer_is_corrupt(oracle):
+    """blk_off + blk_len > data_len -> MTBLX_ST_CORRUPT with no records (the
+    reference's BytesView::slice panics), for the pipelined (4 KiB) and the exact (> 64 KiB)
+    kernels; in-bounds blocks are unaffected; the framed checksum check flags the block."""
+    codec = _codec()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(200)
+    rng = np.random.default_rng(43)
+    big = [oracle.build_block(corpus.random_records(rng, 1500, 8, 60, 40, 60)) for _ in range(3)]
+    bd, bo, bl = corpus.pack(big, rng=rng)
+    for d_, o_, l_ in ((data, off, ln), (bd, bo, bl)):
+        cut = int(o_[-1]) + int(l_[-1]) // 2     # the last block overhangs the buffer
+        o2 = np.concatenate([o_, [cut + 100]]).astype(np.uint64)   # and one starts past it
+        l2 = np.concatenate([l_, [64]]).astype(np.uint32)
+        dd = d_[:cut].copy()
+        dev = _decode(dd, o2, l2)
+        nb = o_.size
+        assert dev.status[nb - 1] == 2 and dev.status[nb] == 2 and dev.nrec[nb - 1] == 0 and dev.nrec[nb] == 0
+        orc = oracle.decode_blocks(dd, o_[: nb - 1], l_[: nb - 1])
+        assert np.array_equal(dev.status[: nb - 1], orc.status) and np.array_equal(dev.nrec[: nb - 1], orc.nrec)
+        assert np.array_equal(dev.keys, orc.keys) and np.array_equal(dev.vals, orc.vals)
+        assert np.array_equal(dev.key_end, orc.key_end) and np.array_equal(dev.val_end, orc.val_end)
+        batch = codec.DeviceBatch.from_host(dd, o2, l2)
+        _, bad = codec.crc32c_blocks(batch, framed=True)
+        out, _, vbad = codec.decode_verify(batch, framed=True, fused=True)
+        torch.cuda.synchronize()
+        assert bad.cpu().numpy()[nb - 1:].tolist() == [1, 1]
+        assert vbad.cpu().numpy()[nb - 1:].tolist() == [1, 1]
+
+
+def test_lookback_timeout_rejected_everywhere(oracle, monkeypatch, tmp_path):
+    """no API hands back records from a launch whose look-back timed out."""
+    codec = _codec()
+    import torch
+    from mtblx import pipe, reader, synth
+    from mtblx.writer import Writer
+    data, off, ln = synth.cfg2_file(300)
+    w = Writer(4096, 16)
+    for k, v in synth.cfg1_records(2000):
+        w.insert(k, v)
+    fbytes = w.into_inner()
+    path = tmp_path / "f.mtbl"
+    path.write_bytes(fbytes)
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    # sanity: without the knob everything decodes
+    out = codec.decode_blocks(batch)
+    torch.cuda.synchronize()
+    nr, kb, vb, fl = out.totals_host()
+    assert fl == 0
+    monkeypatch.setenv("MTBLX_DEBUG_FLAGS", "2")
+    # codec: the count pass and the decode both report it
+    with pytest.raises(codec.LaunchTimeout):
+        codec.decode_blocks(batch)
+    ws = codec.Workspace(batch.nblk)
+    codec.decode_into(batch, out, ws)
+    torch.cuda.synchronize()
+    with pytest.raises(codec.LaunchTimeout):
+        out.to_host()
+    assert out.totals_host(check=False)[3] & 2
+    # Reader (index decode at open)
+    with pytest.raises(codec.LaunchTimeout):
+        reader.Reader(fbytes).iter()
+    # end-to-end pipe: the chunk is re-run once, then MTBLX_E_TIMEOUT
+    ho = pipe.HostOutputs(off.size, nr, kb, vb)
+    with pytest.raises(codec.LaunchTimeout):
+        pipe.HostPipe().decode(data, off, ln, ho)
+    # C++ surface
+    dump = os.path.join(ROOT, "oxidized-mtbl_amd", "build", "dump")
+    if os.path.exists(dump):
+        r = subprocess.run([dump, str(path)], capture_output=True, timeout=120, env=dict(os.environ))
+        assert r.returncode == 1 and b"look-back timeout" in r.stderr, r
+        assert r.stdout == b""
+    monkeypatch.delenv("MTBLX_DEBUG_FLAGS")
+    # and the same workspace works again afterwards
+    codec.decode_into(batch, out, ws)
+    torch.cuda.synchronize()
+    assert out.totals_host() == (nr, kb, vb, 0)
+    if os.path.exists(dump):
+        r = subprocess.run([dump, str(path)], capture_output=True, timeout=120)
+        assert r.returncode == 0 and r.stdout.count(b"\n") == 2000

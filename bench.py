@@ -577,9 +577,7 @@ def main():
     # key/value bytes written + 2 x u32 end offsets per record + 24 B of per-block outputs
     alg_bytes = block_bytes + kbytes + vbytes + 8 * nrec + 24 * batch.nblk
 
-    # Measured BEFORE the decode steps (they also bring the clock up; the decode steps then
-    # follow on a warm GPU, as in a long-running service):
-    # (1) stream-copy ceiling on this box: the in-repo gfx950 copy kernel
+    # stream-copy ceiling on this box, measured before the decode steps: the in-repo gfx950 copy kernel
     #     (mtblx_stream_copy: 16 B per lane, 1-8 accesses in flight, optional non-temporal
     #     stores / loads) moving the same number of bytes (half read, half written) as one
     #     decode launch; best variant of the sweep
@@ -598,16 +596,76 @@ def main():
             def cp(v=var):
                 if CL.mtblx_stream_copy(dst.data_ptr(), src.data_ptr(), half, v, hs) != 0:
                     raise RuntimeError("mtblx_stream_copy failed")
-            for _ in range(3):
+            for _ in range(2):
                 cp()
-            c_ms = _timed(cp, stream, 10)
+            c_ms = _timed(cp, stream, 5)
             gbs = 2 * half / (c_ms * 1e-3) / 1e9
             if ceiling is None or gbs > ceiling:
                 ceiling, ceiling_variant = gbs, var
         del src, dst
         torch.cuda.empty_cache()
 
-    # (2) f1: device CRC-32C verify of the same blocks (separate kernel; the stored checksums sit
+    def step():
+        # one mtblx_decode_blocks call = one decode kernel launch (no fills: the workspace resets itself)
+        codec.decode_into(batch, out, ws, stream)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+    torch.cuda.synchronize()
+    h = out.totals_host()
+    st = out.status[: batch.nblk]
+    # validity: every block OK and the decoded totals equal what the Writer wrote (16 B keys, 64 B values)
+    if h[3] != 0 or not bool((st == 0).all().item()) or h[0] != exp_nrec or h[1] != 16 * exp_nrec \
+            or h[2] != 64 * exp_nrec:
+        if args.lib:
+            log(f"(ablation build) totals={h}")
+        else:
+            raise RuntimeError(f"decode failed: totals={h}, bad blocks={int((st != 0).sum().item())}")
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # HIP events on the decode stream bracket the timed region (one pair: an event between two
+    # launches costs ~10 us of idle GPU per step on this stack); the launches run back to back,
+    # so region / K is the kernel's average launch duration (rocprofv3 agrees: profiles/)
+    e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        e_start.record(stream)
+        for i in range(args.steps):
+            step()
+        e_end.record(stream)
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (must stay below the GPU time)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    k_decode_ms = e_start.elapsed_time(e_end) / args.steps
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_bytes = block_bytes * world
+    total_recs = nrec * world
+    value = total_bytes / (elapsed / args.steps) / 2**30
+
+    # roofline of the (only) decode kernel: algorithmic bytes per launch / its launch duration
+    achieved = alg_bytes / (k_decode_ms * 1e-3) / 1e9
+    mx = int(ln.max())
+    kernel = ("k_decode_pipe<PipeSmall>" if mx <= PIPE_MAX_BLOCK else
+              "k_decode_pipe<PipeLarge>" if mx <= PIPE_LARGE_MAX_BLOCK else "k_decode_tiles")
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("kernel") == kernel and int(tj.get("blocks", -1)) == int(batch.nblk):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    # f1: device CRC-32C verify of the same blocks (separate kernel; the stored checksums sit
     # right before each content in the file the batch addresses)
     crc_info = None
     if not args.no_crc:
@@ -638,66 +696,6 @@ def main():
                                             "vs_decode_then_crc_GiB_per_s": None}}
 
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-
-    def step(i=None):
-        # one mtblx_decode_blocks call = one decode kernel launch (no fills: the workspace resets itself)
-        if i is not None:
-            ev[i][0].record(stream)
-        codec.decode_into(batch, out, ws, stream)
-        if i is not None:
-            ev[i][1].record(stream)
-
-    with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step()
-    torch.cuda.synchronize()
-    h = out.totals_host()
-    st = out.status[: batch.nblk]
-    # validity: every block OK and the decoded totals equal what the Writer wrote (16 B keys, 64 B values)
-    if h[3] != 0 or not bool((st == 0).all().item()) or h[0] != exp_nrec or h[1] != 16 * exp_nrec \
-            or h[2] != 64 * exp_nrec:
-        if args.lib:
-            log(f"(ablation build) totals={h}")
-        else:
-            raise RuntimeError(f"decode failed: totals={h}, bad blocks={int((st != 0).sum().item())}")
-
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        for i in range(args.steps):
-            step(i)
-    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (must stay below the GPU time)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-
-    k_decode_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_bytes = block_bytes * world
-    total_recs = nrec * world
-    value = total_bytes / (elapsed / args.steps) / 2**30
-
-    # roofline of the (only) decode kernel: algorithmic bytes per launch / its launch duration
-    achieved = alg_bytes / (k_decode_ms * 1e-3) / 1e9
-    mx = int(ln.max())
-    kernel = ("k_decode_pipe<PipeSmall>" if mx <= PIPE_MAX_BLOCK else
-              "k_decode_pipe<PipeLarge>" if mx <= PIPE_LARGE_MAX_BLOCK else "k_decode_tiles")
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("kernel") == kernel and int(tj.get("blocks", -1)) == int(batch.nblk):
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
     if crc_info is not None:
         crc_info["fused_decode_verify"]["vs_decode_then_crc_GiB_per_s"] = \
             round(block_bytes / ((k_decode_ms + crc_info["ms"]) * 1e-3) / 2**30, 1)
@@ -721,7 +719,7 @@ def main():
                    "blocks_per_gpu": int(batch.nblk), "block_bytes_per_gpu": block_bytes,
                    "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
                    "parallelism": f"block-sharded x{world}, no collective"},
-        "kernels_ms": {f"{kernel} (HIP events around each call)": round(k_decode_ms, 4)},
+        "kernels_ms": {f"{kernel} (HIP events around the timed region / steps)": round(k_decode_ms, 4)},
         "host_enqueue_ms_per_step": round(t_enq * 1e3 / args.steps, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -383,11 +383,18 @@ __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeo
   while (j >= 0) {
     const int64_t idx = j - lane;
     uint64_t w = idx >= 0 ? __hip_atomic_load(a.lbw + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kIncl;
+    // bounded by wall time (s_memrealtime, 100 MHz; 20 s): tickets are claimed by running
+    // workgroups, so this only gives up if the chip stalls -- never on a slow predecessor
+    uint64_t t0 = 0;
     uint32_t spins = 0;
     while (__ballot(!(w & (kIncl | kAgg))) != 0ull) {
       __builtin_amdgcn_s_sleep(1);
       if (!(w & (kIncl | kAgg))) w = __hip_atomic_load(a.lbw + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > (1u << 22)) { timeout = true; w |= kIncl; }
+      if ((++spins & 63u) == 0u) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) t0 = t;
+        if (t - t0 > 2000000000ull) { timeout = true; w |= kIncl; }
+      }
     }
     const uint64_t im = __ballot((w & kIncl) != 0ull);
     const int first = im ? __builtin_ctzll(im) : kWave;

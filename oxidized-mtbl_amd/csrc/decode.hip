@@ -1103,6 +1103,9 @@ struct PipeCfg {
   static constexpr int COPY0 = kPipeLoadWave + LOADW;             // first copy wave
   static constexpr int NCOPY = kPipeThreads / kWave - COPY0;      // copy waves
   static constexpr int ROWS = NCOPY * (kWave / 16);               // intervals per copy round
+  // look-back words per lane loaded one iteration early (the VERIFY kernels carry the CRC
+  // state in the same 128-VGPR budget: 4, else they spill)
+  static constexpr int LBL = VERIFY_ ? 4 : 6;
 };
 // (PipeLarge with four loaders and ten copy waves: +0.8 % on 16 B keys, -16 % on cfg3's long
 // Zipf keys, whose copy is the longer half of the iteration)
@@ -1529,15 +1532,14 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
 // Look-back of tile t over the window [lo, t): the tiles claimed by other workgroups since this
 // workgroup's previous tile lo - 1 (whose inclusive prefix `tinc` it holds): prefix(t) =
 // tinc + sum of A(lo .. t-1).  With static round-robin tiles the window was G - 1 words; with
-// claimed tiles (k_decode_pipe) it varies around that.  The kPipeLbLoads * 64 most recent words
-// are loaded one iteration early by the look-back wave; older ones (a longer window) are
-// loaded when consumed.
-constexpr int kPipeLbLoads = 6;
-
-__device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t t, int64_t lo,
-                                                    uint64_t lbv[kPipeLbLoads], int lane) {
+// claimed tiles (k_decode_pipe) it varies around that.  The 64 * P::LBL most recent words
+// (P::LBL per lane) are loaded one iteration early by the look-back wave; older ones (a longer
+// window) are loaded when consumed.
+template <int NL>
+__device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t t, int64_t lo, uint64_t (&lbv)[NL],
+                                                    int lane) {
 #pragma unroll
-  for (int m = 0; m < kPipeLbLoads; ++m) {
+  for (int m = 0; m < NL; ++m) {
     const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
     lbv[m] = (i >= lo) ? __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kReady;
   }
@@ -1546,13 +1548,13 @@ __device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t 
 // wave 1: re-poll the words of tile t that were not ready when loaded, until all are or
 // the copy waves have finished this iteration (the barrier must not wait for laggards;
 // what is still missing is polled again when the tile is consumed).
-__device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t, int64_t lo,
-                                                   uint64_t lbv[kPipeLbLoads], int lane, const uint32_t* cdone,
-                                                   uint32_t want) {
+template <int NL>
+__device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t, int64_t lo, uint64_t (&lbv)[NL],
+                                                   int lane, const uint32_t* cdone, uint32_t want) {
   for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
     bool pend = false;
 #pragma unroll
-    for (int m = 0; m < kPipeLbLoads; ++m) {
+    for (int m = 0; m < NL; ++m) {
       const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
       pend |= (i >= lo) && !(lbv[m] & kReady);
     }
@@ -1560,7 +1562,7 @@ __device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t
     if (__hip_atomic_load(cdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return;
     __builtin_amdgcn_s_sleep(2);
 #pragma unroll
-    for (int m = 0; m < kPipeLbLoads; ++m) {
+    for (int m = 0; m < NL; ++m) {
       const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
       if (i >= lo && !(lbv[m] & kReady)) lbv[m] = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1572,7 +1574,7 @@ __device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t
 // workgroup's previous tile (lo - 1).
 template <class P>
 __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, uint32_t t, int64_t lo, uint64_t tinc[3],
-                                              uint64_t lbv[kPipeLbLoads], int lane, uint32_t* ready,
+                                              uint64_t (&lbv)[P::LBL], int lane, uint32_t* ready,
                                               uint32_t rv) {
   const uint32_t nb = B.nb, b0 = B.b0;
   uint64_t sr = 0, sk = 0, sv = 0;
@@ -1587,11 +1589,11 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
     lb_take(a, (uint64_t)i, w, sr, sk, sv);
   };
 #pragma unroll
-  for (int m = 0; m < kPipeLbLoads; ++m) {
+  for (int m = 0; m < P::LBL; ++m) {
     const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
     if (i >= lo) take(i, lbv[m]);
   }
-  for (int64_t base = (int64_t)t - 1 - (int64_t)kPipeLbLoads * kWave; base >= lo; base -= kWave) {   // rare
+  for (int64_t base = (int64_t)t - 1 - (int64_t)P::LBL * kWave; base >= lo; base -= kWave) {   // rare
     const int64_t i = base - lane;
     if (i >= lo) take(i, __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
@@ -1980,7 +1982,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   }
 
   uint64_t tinc[3] = {0, 0, 0};           // wave 1
-  uint64_t lbv[kPipeLbLoads];             // wave 1: look-back words of the next tile to copy
+  uint64_t lbv[P::LBL];                   // wave 1: look-back words of the next tile to copy
   uint64_t ioff = 0;                      // loaders: directory entry (lane < nb) of the next tile to stage
   uint32_t ilen = 0;
   auto load_info = [&](uint32_t t) {

@@ -376,7 +376,6 @@ struct WsHdr {
   uint32_t done;
   uint32_t hw[2];
   unsigned long long flags;   // bit0 overflow, bit1 look-back timeout (-> totals[3])
-  uint32_t ticket;            // k_decode_pipe: tiles claimed beyond the static first two per workgroup
 };
 
 // workspace tile entry t: {packed aggregate of launch parity 0, of parity 1, exact key bytes,
@@ -405,7 +404,9 @@ __device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bi
 // kWaitTicks of wall time (s_memrealtime, 100 MHz) and the launch reports a timeout (totals[3]
 // bit 1) instead of hanging.  Generous on purpose: a predecessor tile can legitimately take
 // long (a multi-MiB block on the exact serial path), and giving up is only for lost
-// co-residency.  Call once per spin; the clock is read every 64 spins.
+// co-residency (tiles are assigned round-robin: t = g + k G; claiming them from a ticket
+// instead removes that assumption but measured 25 % slower on cfg2 -- one hot atomic word and
+// longer look-back waits -- DESIGN.md §4).  Call once per spin; the clock is read every 64.
 constexpr uint64_t kWaitTicks = 20ull * 100000000ull;   // 20 s
 struct WaitBound {
   uint64_t t0 = 0;
@@ -437,8 +438,6 @@ __device__ __forceinline__ void ws_end(const TileArgs& a) {
       const unsigned long long f = __hip_atomic_load(&a.hdr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       a.totals[3] = f | a.inject;
       __hip_atomic_store(&a.hdr->flags, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // every claim of this launch returned before its workgroup counted itself done
-      __hip_atomic_store(&a.hdr->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t h = __hip_atomic_load(&a.hdr->hw[a.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.ntiles > h) __hip_atomic_store(&a.hdr->hw[a.par], a.ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1083,8 +1082,6 @@ __device__ uint64_t g_tl[1024][8];
 #endif
 
 constexpr int kPipeThreads = 1024;
-constexpr uint32_t kTileRing = 8;          // tile ids in flight (claim 4 ahead .. previous tile)
-constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 constexpr int kPipeLoadWave = 2;                                         // LDS-DMA loaders (issue no stores)
 constexpr int kP2Spi = 16;                                               // slots per interval (= DPP row)
 constexpr uint32_t kLargeDmaSplit = 24;   // PipeLarge, short copies: pieces staged before the walk ends (of ~64)
@@ -1103,9 +1100,6 @@ struct PipeCfg {
   static constexpr int COPY0 = kPipeLoadWave + LOADW;             // first copy wave
   static constexpr int NCOPY = kPipeThreads / kWave - COPY0;      // copy waves
   static constexpr int ROWS = NCOPY * (kWave / 16);               // intervals per copy round
-  // look-back words per lane loaded one iteration early (the VERIFY kernels carry the CRC
-  // state in the same 128-VGPR budget: 4, else they spill)
-  static constexpr int LBL = VERIFY_ ? 4 : 6;
 };
 // (PipeLarge with four loaders and ten copy waves: +0.8 % on 16 B keys, -16 % on cfg3's long
 // Zipf keys, whose copy is the longer half of the iteration)
@@ -1135,7 +1129,6 @@ struct alignas(16) PipeBuf {
 template <class P>
 struct alignas(16) PipeLds {
   PipeBuf<P> buf[P::NBUF];
-  uint32_t tile[kTileRing];   // tile id of local tile k at [k % kTileRing] (kNoTile: none)
   uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
   uint32_t pub;      // wave 0 sets after publishing the aggregate of the tile it walked
   uint32_t cdone;    // copy waves that finished their copy (monotonic)
@@ -1529,17 +1522,13 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   }
 }
 
-// Look-back of tile t over the window [lo, t): the tiles claimed by other workgroups since this
-// workgroup's previous tile lo - 1 (whose inclusive prefix `tinc` it holds): prefix(t) =
-// tinc + sum of A(lo .. t-1).  With static round-robin tiles the window was G - 1 words; with
-// claimed tiles (k_decode_pipe) it varies around that.  The 64 * P::LBL most recent words
-// (P::LBL per lane) are loaded one iteration early by the look-back wave; older ones (a longer
-// window) are loaded when consumed.
-template <int NL>
-__device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t t, int64_t lo, uint64_t (&lbv)[NL],
-                                                    int lane) {
+// wave 1: issue the look-back loads of tile t (aggregates of tiles t-G+1 .. t-1) one
+// iteration before they are consumed; they complete behind the copy phase.
+__device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t t, uint32_t G,
+                                                    uint64_t lbv[kMaxLookbackLoads], int lane) {
+  const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
 #pragma unroll
-  for (int m = 0; m < NL; ++m) {
+  for (int m = 0; m < kMaxLookbackLoads; ++m) {
     const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
     lbv[m] = (i >= lo) ? __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kReady;
   }
@@ -1548,13 +1537,14 @@ __device__ __forceinline__ void pipe_lookback_issue(const TileArgs& a, uint32_t 
 // wave 1: re-poll the words of tile t that were not ready when loaded, until all are or
 // the copy waves have finished this iteration (the barrier must not wait for laggards;
 // what is still missing is polled again when the tile is consumed).
-template <int NL>
-__device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t, int64_t lo, uint64_t (&lbv)[NL],
-                                                   int lane, const uint32_t* cdone, uint32_t want) {
+__device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t, uint32_t G,
+                                                   uint64_t lbv[kMaxLookbackLoads], int lane, const uint32_t* cdone,
+                                                   uint32_t want) {
+  const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
   for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
     bool pend = false;
 #pragma unroll
-    for (int m = 0; m < NL; ++m) {
+    for (int m = 0; m < kMaxLookbackLoads; ++m) {
       const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
       pend |= (i >= lo) && !(lbv[m] & kReady);
     }
@@ -1562,40 +1552,35 @@ __device__ __forceinline__ void pipe_lookback_poll(const TileArgs& a, uint32_t t
     if (__hip_atomic_load(cdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return;
     __builtin_amdgcn_s_sleep(2);
 #pragma unroll
-    for (int m = 0; m < NL; ++m) {
+    for (int m = 0; m < kMaxLookbackLoads; ++m) {
       const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
       if (i >= lo && !(lbv[m] & kReady)) lbv[m] = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-// wave 1: finish the look-back of tile t (re-polling words that were not ready yet, then any
-// words older than the prefetched ones), per-block outputs.  tinc = inclusive prefix of this
-// workgroup's previous tile (lo - 1).
+// wave 1: finish the look-back of tile t (re-polling words that were not ready yet),
+// per-block outputs.  tinc = inclusive prefix of this workgroup's previous tile.
 template <class P>
-__device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, uint32_t t, int64_t lo, uint64_t tinc[3],
-                                              uint64_t (&lbv)[P::LBL], int lane, uint32_t* ready,
+__device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, uint32_t t, uint32_t G, uint64_t tinc[3],
+                                              uint64_t lbv[kMaxLookbackLoads], int lane, uint32_t* ready,
                                               uint32_t rv) {
   const uint32_t nb = B.nb, b0 = B.b0;
+  const int64_t lo = (t >= G) ? (int64_t)t - G + 1 : 0;
   uint64_t sr = 0, sk = 0, sv = 0;
   bool timeout = false;
-  auto take = [&](int64_t i, uint64_t w) {
+#pragma unroll
+  for (int m = 0; m < kMaxLookbackLoads; ++m) {
+    const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
+    uint64_t w = lbv[m];
     WaitBound wb;
     while (!(w & kReady)) {
       __builtin_amdgcn_s_sleep(2);
       w = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (wb.expired()) { timeout = true; w = kReady; }
     }
+    if (i < lo) continue;
     lb_take(a, (uint64_t)i, w, sr, sk, sv);
-  };
-#pragma unroll
-  for (int m = 0; m < P::LBL; ++m) {
-    const int64_t i = (int64_t)t - 1 - lane - (int64_t)m * kWave;
-    if (i >= lo) take(i, lbv[m]);
-  }
-  for (int64_t base = (int64_t)t - 1 - (int64_t)P::LBL * kWave; base >= lo; base -= kWave) {   // rare
-    const int64_t i = base - lane;
-    if (i >= lo) take(i, __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
   if (timeout) ws_flag(a, 2ull);
   sr = lb_wave_sum(sr);
@@ -1951,23 +1936,12 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   __shared__ PipeLds<P> S;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t g = blockIdx.x, G = gridDim.x;
-  // Tiles.  A workgroup's local tiles k = 0, 1 are g and g + G (static: no claim latency at
-  // start); every later one is CLAIMED with one returning atomic on the workspace ticket:
-  // tile 2G + ticket, in claim order.  Claimed tiles belong to running workgroups, so every
-  // predecessor of a tile a workgroup waits on is being worked on (progress does not rest on
-  // all workgroups being resident), and faster workgroups -- or XCDs -- take more tiles (no
-  // tail of the slowest).  Tile k's id sits in S.tile[k % kTileRing] from the barrier after
-  // its claim: claimed 4 iterations ahead (3 for two buffers), directory loaded one later, DMA
-  // one later, walked, copied.  kNoTile ends the sequence (claims past ntiles).
+  const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
   Stamps ST;
   ST.init();
   TL(0);
   ws_begin(a);
-  if (tid == 0) {
-    S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0;
-    S.tile[0] = g < a.ntiles ? g : kNoTile;
-    S.tile[1] = g + G < a.ntiles ? g + G : kNoTile;
-  }
+  if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; }
   if constexpr (P::VERIFY) {
     for (int i = tid; i < 256; i += kPipeThreads) {   // slicing-by-4 tables from the byte table
       uint32_t t = mtblx_crc::kTab.byte[i];
@@ -1982,37 +1956,26 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   }
 
   uint64_t tinc[3] = {0, 0, 0};           // wave 1
-  uint64_t lbv[P::LBL];                   // wave 1: look-back words of the next tile to copy
-  uint64_t ioff = 0;                      // loaders: directory entry (lane < nb) of the next tile to stage
+  uint64_t lbv[kMaxLookbackLoads];        // wave 1: look-back words of the next tile to copy
+  uint64_t ioff = 0;                      // wave 0: directory entry (lane < nb) of the next tile to stage
   uint32_t ilen = 0;
-  auto load_info = [&](uint32_t t) {
-    if (t == kNoTile) return;
-    const uint32_t b0 = t * a.bpt, nb = min(a.bpt, a.nblk - b0);
+  auto load_info = [&](uint32_t kk) {
+    if (kk >= nloc) return;
+    const uint32_t b0 = (g + kk * G) * a.bpt, nb = min(a.bpt, a.nblk - b0);
     const uint32_t j = (uint32_t)lane < nb ? (uint32_t)lane : nb - 1;
     ioff = a.blk_off[b0 + j];
     ilen = a.blk_len[b0 + j];
   };
-  // loaders split every tile's DMA pieces (even / odd 1 KiB pieces); loader 0 also claims
+  // loaders split every tile's DMA pieces (even / odd 1 KiB pieces)
   const bool loader = wv >= kPipeLoadWave && wv < kPipeLoadWave + P::LOADW;
   const uint32_t part = (uint32_t)(wv - kPipeLoadWave);
-  auto claim = [&](uint32_t k, uint32_t prev_id) {   // loader 0: tile id of local tile k
-    if (part != 0) return;
-    uint32_t t = kNoTile;
-    if (prev_id != kNoTile && lane == 0) {
-      const uint32_t c = __hip_atomic_fetch_add(&a.hdr->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t = 2u * G + c < a.ntiles ? 2u * G + c : kNoTile;
-    }
-    if (lane == 0) S.tile[k % kTileRing] = t;
-  };
-  const uint32_t t0 = g < a.ntiles ? g : kNoTile, t1 = g + G < a.ntiles ? g + G : kNoTile;
   if (loader) {
-    load_info(t0);
-    if (t0 != kNoTile) pipe_dma(S.buf[0], a, t0, ioff, ilen, lane, part);
-    load_info(t1);
-    claim(2, t1);
+    load_info(0);
+    if (nloc > 0) pipe_dma(S.buf[0], a, g, ioff, ilen, lane, part);
+    load_info(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (wv == 1) {
-    if (P::NBUF == 3 && t0 != kNoTile) pipe_lookback_issue(a, t0, 0, lbv, lane);
+    if (P::NBUF == 3 && nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
   }
   __syncthreads();
   TL(1);
@@ -2022,18 +1985,16 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   if constexpr (P::NBUF == 2) {
     // two buffers: tile it is walked, looked back and copied in iteration it while the
     // loaders stage tile it+1 into the other buffer
-    for (uint32_t it = 0;; ++it) {
-      const uint32_t tc = S.tile[it % kTileRing];
-      if (tc == kNoTile) break;   // uniform: every wave reads it after the same barrier
-      const uint32_t tn = S.tile[(it + 1) % kTileRing];
+    for (uint32_t it = 0; it < nloc; ++it) {
       PipeBuf<P>& C = S.buf[it & 1u];
+      const uint32_t tc = g + it * G;
       if (wv == 0) {
         pipe_walk(C, a, tc, lane, ST);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&S.pub, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(3);
       } else if (loader) {
-        if (tn != kNoTile) {
+        if (it + 1 < nloc) {
           // DMA landing in LDS slows the walker's tail (LDS writes and fences queue behind it)
           // by ~3.5k cycles per 64 KiB tile, but beside the copy it slows a key-heavy copy
           // (cfg3's long keys read many 16-byte key planes).  So: when the previous tile's key
@@ -2042,24 +2003,21 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           // (the other buffer still holds that tile's totals: the DMA writes only its stage)
           PipeBuf<P>& N = S.buf[(it + 1) & 1u];
           const bool late = it >= 1 && 3ull * N.ttot[1] <= (uint64_t)N.ttot[2];
-          pipe_dma(N, a, tn, ioff, ilen, lane, part, 0, late ? kLargeDmaSplit : 0xFFFFFFFFu);
+          pipe_dma(N, a, tc + G, ioff, ilen, lane, part, 0, late ? kLargeDmaSplit : 0xFFFFFFFFu);
           if (late) {
             wait_flag(a, &S.pub, it + 1);
-            pipe_dma(N, a, tn, ioff, ilen, lane, part, kLargeDmaSplit);
+            pipe_dma(N, a, tc + G, ioff, ilen, lane, part, kLargeDmaSplit);
           }
+          load_info(it + 2);
         }
-        const uint32_t t2 = S.tile[(it + 2) % kTileRing];
-        load_info(t2);
-        claim(it + 3, t2);
         ST.hit(4);
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 1 + (int)part, lane, it & 1u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+1 (read next phase)
         ST.hit(6);
       } else if (wv == 1) {
-        const int64_t lo = it ? (int64_t)S.tile[(it - 1) % kTileRing] + 1 : 0;
         wait_flag(a, &S.pub, it + 1);
-        pipe_lookback_issue(a, tc, lo, lbv, lane);
-        pipe_lookback(C, a, tc, lo, tinc, lbv, lane, &S.ready, it + 1);
+        pipe_lookback_issue(a, tc, G, lbv, lane);
+        pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, it + 1);
         ST.hit(1);
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
@@ -2074,24 +2032,20 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       else ST.hit(1);
     }
   } else
-  for (int it = -1;; ++it) {
+  for (int it = -1; it < (int)nloc; ++it) {
     const uint32_t k1 = (uint32_t)(it + 1), k2 = (uint32_t)(it + 2);
-    const uint32_t tc = it >= 0 ? S.tile[(uint32_t)it % kTileRing] : kNoTile;
-    if (it >= 0 && tc == kNoTile) break;   // uniform: every wave reads it after the same barrier
-    const uint32_t t1n = S.tile[k1 % kTileRing];
     if (wv == 0) {
       // walk first: the aggregate A(tile it+1) is published as early as possible
-      if (t1n != kNoTile) {
-        pipe_walk(S.buf[k1 % P::NBUF], a, t1n, lane, ST);
+      if (k1 < nloc) {
+        pipe_walk(S.buf[k1 % P::NBUF], a, g + k1 * G, lane, ST);
         if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       ST.hit(3);
     } else if (loader) {
-      const uint32_t t2n = S.tile[k2 % kTileRing];
-      if (t2n != kNoTile) pipe_dma(S.buf[k2 % P::NBUF], a, t2n, ioff, ilen, lane, part);
-      const uint32_t t3n = S.tile[(k2 + 1) % kTileRing];
-      load_info(t3n);
-      claim(k2 + 2, t3n);
+      if (k2 < nloc) {
+        pipe_dma(S.buf[k2 % P::NBUF], a, g + k2 * G, ioff, ilen, lane, part);
+        load_info(k2 + 1);
+      }
       ST.hit(4);
       if constexpr (P::VERIFY) {
         if (it >= 0) pipe_crc(S.buf[(uint32_t)it % P::NBUF], a, S, 1 + (int)part, lane, (uint32_t)it & 1u);
@@ -2100,13 +2054,13 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       ST.hit(6);
     } else if (it >= 0) {
       PipeBuf<P>& C = S.buf[(uint32_t)it % P::NBUF];
+      const uint32_t tc = g + (uint32_t)it * G;
       if (wv == 1) {
-        const int64_t lo = it ? (int64_t)S.tile[(uint32_t)(it - 1) % kTileRing] + 1 : 0;
-        pipe_lookback(C, a, tc, lo, tinc, lbv, lane, &S.ready, (uint32_t)it + 1);
+        pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, (uint32_t)it + 1);
         ST.hit(1);
         // CRC of tile it while lbv is dead (its words were consumed above): lower register pressure
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, (uint32_t)it & 1u);
-        if (t1n != kNoTile) {
+        if (k1 < nloc) {
           // the other workgroups publish A(tile it+1's predecessors) about when this
           // workgroup's wave 0 publishes A(tile it+1): issue the look-back loads after that
           WaitBound wb;
@@ -2114,8 +2068,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
             __builtin_amdgcn_s_sleep(1);
             if (wb.expired()) { ws_flag(a, 2ull); break; }
           }
-          pipe_lookback_issue(a, t1n, (int64_t)tc + 1, lbv, lane);
-          pipe_lookback_poll(a, t1n, (int64_t)tc + 1, lbv, lane, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
+          pipe_lookback_issue(a, tc + G, G, lbv, lane);
+          pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
         }
         ST.hit(1);
       } else {
@@ -2127,7 +2081,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     raw_barrier();
     if (it == -1) TL(2);
     else if (it == 0) TL(3);
-    if (wv == 0) { ST.hit(8); if (it >= 0) ++ntl; }
+    if (wv == 0) { ST.hit(8); ++ntl; }
     else if (wv >= P::COPY0) ST.hit(5);
     else if (loader) ST.hit(12);
     else ST.hit(11);
@@ -2138,7 +2092,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   ws_end(a);
   TL(5);
 #ifdef MTBLX_STAMPS
-  if (tid == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][6] = ntl;
+  if (tid == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][6] = nloc;
 #endif
 #ifdef MTBLX_STAMPS
   // wave 0: [2] trailers + walk loop, [3] scans + publish, [8] barrier.  wave 1: [1]
@@ -2221,7 +2175,7 @@ int pipe_grid(uint32_t ntiles) {
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    cached = std::max(1, ncu);  // 1 workgroup per CU (the look-back window has no size limit)
+    cached = std::max(1, std::min(ncu, kMaxLookbackLoads * kWave + 1));  // 1 workgroup per CU
   }
   return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
 }

@@ -748,7 +748,7 @@ def main():
         L = mlib.lib()
         if hasattr(L, "mtblx_dbg_timeline"):
             G = 1024
-            tl = np.zeros((G, 8), np.uint64)
+            tl = np.zeros((G, 16), np.uint64)
             if L.mtblx_dbg_timeline(tl.ctypes.data_as(C.POINTER(C.c_uint64)), G) == 0:
                 tl = tl[tl[:, 0] > 0].astype(np.int64)
                 t0 = tl[:, 0].min()
@@ -759,8 +759,11 @@ def main():
                     for k, n in enumerate(["entry", "preload", "first_walk", "iter0", "loop_end", "exit"])}
                 res["timeline_us"]["tiles_per_wg"] = [int(tl[:, 6].min()), int(tl[:, 6].max())]
                 res["timeline_us"]["wgs"] = int(tl.shape[0])
-                res["timeline_raw"] = [[round(float(x), 1) for x in us[i, [1, 3, 4, 5]]] + [int(tl[i, 6])]
+                ux = (tl[:, 7:12] - t0) / 100.0     # penult, last look-back, copy0 done, copyN done, penult look-back
+                res["timeline_raw"] = [[round(float(x), 1) for x in us[i, [1, 3, 4, 5]]] + [int(tl[i, 6])] +
+                                       [round(float(x), 1) for x in ux[i]]
                                        for i in range(us.shape[0])]
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(data, off, ln, args.cpu_seconds)
     if rank == 0:

@@ -224,6 +224,24 @@ int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk_rec, uint3
                         int framed, uint8_t* out, uint64_t out_cap, uint64_t* blk_off, uint32_t* blk_len,
                         int32_t* status, uint64_t* totals, void* workspace, size_t ws_bytes, void* stream);
 
+/* Writer::into_inner's tail on the device (src/writer.rs:132-138, :155-181, :239-265;
+ * src/metadata.rs:61-79) for ONE file whose data blocks mtblx_encode_blocks wrote framed:
+ * data[region_off .. region_off + data_bytes) holds them back to back; blk_off/blk_len (device
+ * [nblk], offsets relative to `data`) and blk_rec (device [nblk + 1], absolute record indices
+ * into rec) are that call's directory and plan for this file.  Writes the whole file to
+ * `file` (device; the data region is copied unless file == data + region_off): the data
+ * blocks, then the index block -- one entry per data block, key = bytes_shortest_separator(
+ * its last key, the next block's first key) with the crate's write_u16 APPEND quirk (the
+ * last block's entry keeps the file's last key), value = varint64(the block's file offset)
+ * -- built by BlockBuilder with `restart_interval` and framed with CompressionType::None,
+ * then the 512-byte footer (block_size clamped to >= 1024 as WriterBuilder::block_size).
+ * nblk == 0 writes the empty file.  Synchronous (allocates its temporaries: once per file);
+ * *file_len = bytes written.  Byte-identical to the crate's Writer for the same records. */
+int mtblx_encode_index(const mtblx_records* rec, const uint64_t* blk_rec, uint32_t nblk, uint64_t block_size,
+                       uint32_t restart_interval, const uint8_t* data, uint64_t region_off, uint64_t data_bytes,
+                       const uint64_t* blk_off, const uint32_t* blk_len, uint8_t* file, uint64_t file_cap,
+                       uint64_t* file_len, void* stream);
+
 /* ---- snappy raw decompression on the device (f4) ----
  * Reader::block's decompression step for CompressionType::Snappy (src/reader.rs:166-170 ->
  * src/compression.rs:57-68, :116-119, snap::raw::Decoder::decompress_vec), for a batch of

@@ -1075,10 +1075,13 @@ struct Stamps {
 // diagnostic timeline (s_memrealtime, 100 MHz) per workgroup of the last k_decode_pipe launch:
 // [0] entry [1] preload done [2] first walk done (it = -1) [3] it = 0 done [4] loop end
 // [5] after ws_end [6] tiles of this workgroup
-__device__ uint64_t g_tl[1024][8];
+__device__ uint64_t g_tl[1024][16];
 #define TL(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// stamp by lane 0 of the calling wave (any wave)
+#define TLW(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define TL(k) do { } while (0)
+#define TLW(k) do { } while (0)
 #endif
 
 constexpr int kPipeThreads = 1024;
@@ -2057,6 +2060,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       const uint32_t tc = g + (uint32_t)it * G;
       if (wv == 1) {
         pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, (uint32_t)it + 1);
+        if (it + 1 == (int)nloc) TLW(8);         // look-back of the last tile done
+        else if (it + 2 == (int)nloc) TLW(11);   // ... of the second-to-last
         ST.hit(1);
         // CRC of tile it while lbv is dead (its words were consumed above): lower register pressure
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, (uint32_t)it & 1u);
@@ -2074,6 +2079,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         ST.hit(1);
       } else {
         pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST);
+        if (wv == P::COPY0 && it + 1 == (int)nloc) TLW(9);   // first copy wave: last tile's stores issued
+        if (wv == P::COPY0 + P::NCOPY - 1 && it + 1 == (int)nloc) TLW(10);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(7);
       }
@@ -2081,6 +2088,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     raw_barrier();
     if (it == -1) TL(2);
     else if (it == 0) TL(3);
+    else if (it + 2 == (int)nloc) TL(7);   // end of the second-to-last iteration
     if (wv == 0) { ST.hit(8); ++ntl; }
     else if (wv >= P::COPY0) ST.hit(5);
     else if (loader) ST.hit(12);
@@ -2203,7 +2211,7 @@ int resident_grid(uint32_t ntiles) {
 #ifdef MTBLX_STAMPS
 extern "C" int mtblx_dbg_timeline(uint64_t* out, uint32_t nwg) {   // diagnostic build only
   if (nwg > 1024) nwg = 1024;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mtblx::g_tl), (size_t)nwg * 8 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mtblx::g_tl), (size_t)nwg * 16 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -33,7 +33,7 @@ EXPORTS = [
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
     "mtblx_pipe_decode", "mtblx_pipe_set", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
-    "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy",
+    "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
@@ -152,6 +152,10 @@ def lib() -> C.CDLL:
                                                   C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                                   C.c_void_p]
         L.mtblx_snappy_decompress_dev.restype = C.c_int
+        L.mtblx_encode_index.argtypes = [C.POINTER(Records), C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_void_p,
+                                         C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, u64p,
+                                         C.c_void_p]
+        L.mtblx_encode_index.restype = C.c_int
         L.mtblx_stream_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
         L.mtblx_stream_copy.restype = C.c_int
         L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]

@@ -137,3 +137,41 @@ def encode_blocks(recs: DeviceRecords, blk_rec: torch.Tensor, restart_interval: 
                   stream=None) -> Encoded:
     bufs = EncodeBuffers(recs, int(blk_rec.numel()) - 1, device=recs.key_end.device)
     return encode_into(recs, blk_rec, bufs, restart_interval, framed, stream)
+
+
+def write_file(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16, stream=None) -> torch.Tensor:
+    """The crate's Writer on the device for ONE file (src/writer.rs): insert every record
+    (block cut: plan; BlockBuilder + write_block: encode_blocks, framed), then into_inner
+    (index block + footer: mtblx_encode_index).  -> the file bytes (device uint8), byte-identical
+    to Writer::into_inner for the same records (CompressionType::None)."""
+    L = codec._require_device()
+    dev = recs.key_end.device
+    blk = plan(recs, block_size, restart_interval, stream=stream)
+    nblk = int(blk.numel()) - 1
+    kbytes = int(recs.key_end[-1].item()) if recs.n else 0
+    if nblk:
+        e = encode_blocks(recs, blk, restart_interval, framed=True, stream=stream)
+        torch.cuda.synchronize()
+        e.check()
+        if int(e.totals[1].item()) & 1:
+            raise WriterPanic(int((e.status != 0).nonzero()[0].item()) if bool((e.status != 0).any()) else 0)
+        data_bytes = int(e.totals[0].item())
+        data, off, ln = e.out, e.blk_off, e.blk_len
+    else:
+        data_bytes = 0
+        data = off = ln = None
+    # index block: separators (<= last key + 2 B) + varint64 offsets + headers + restarts + framing
+    cap = data_bytes + kbytes + 36 * nblk + 64 + 512
+    file = torch.empty(cap, dtype=torch.uint8, device=dev)
+    n = C.c_uint64(0)
+    rc_ = recs.cstruct()
+    u = codec._u
+    rc = L.mtblx_encode_index(C.byref(rc_), C.c_void_p(u(blk)), nblk, int(block_size), int(restart_interval),
+                              C.c_void_p(u(data) if data is not None else u(file)), 0, data_bytes,
+                              C.c_void_p(u(off) if off is not None else 0), C.c_void_p(u(ln) if ln is not None else 0),
+                              C.c_void_p(file.data_ptr()), cap, C.byref(n), C.c_void_p(codec._stream_handle(stream)))
+    if rc == _lib.MTBLX_E_TIMEOUT:
+        raise codec.LaunchTimeout("mtblx_encode_index: look-back timeout")
+    if rc != 0:
+        raise RuntimeError(f"mtblx_encode_index failed: {rc}")
+    return file[: n.value]

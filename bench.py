@@ -759,7 +759,7 @@ def main():
                     for k, n in enumerate(["entry", "preload", "first_walk", "iter0", "loop_end", "exit"])}
                 res["timeline_us"]["tiles_per_wg"] = [int(tl[:, 6].min()), int(tl[:, 6].max())]
                 res["timeline_us"]["wgs"] = int(tl.shape[0])
-                ux = (tl[:, 7:12] - t0) / 100.0     # penult, last look-back, copy0 done, copyN done, penult look-back
+                ux = (tl[:, 7:16] - t0) / 100.0     # penult, last look-back, copy0 done, copyN done, penult look-back, drains
                 res["timeline_raw"] = [[round(float(x), 1) for x in us[i, [1, 3, 4, 5]]] + [int(tl[i, 6])] +
                                        [round(float(x), 1) for x in ux[i]]
                                        for i in range(us.shape[0])]

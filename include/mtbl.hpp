@@ -179,9 +179,10 @@ inline Decoded decode_batch(const uint8_t* d_data, uint64_t data_len, const uint
 // ------------------------------------------------------------------ Writer (src/writer.rs)
 class Writer {
  public:
-  Writer(uint64_t block_size, uint64_t restart_interval, CompressionType c)
+  Writer(uint64_t block_size, uint64_t restart_interval, CompressionType c, uint32_t level = 0)
       : w_(mtblx_writer_new(block_size, restart_interval, static_cast<uint32_t>(c))) {
-    if (!w_) throw std::invalid_argument("CompressionType::None and ::Snappy only (DESIGN.md §9)");
+    if (!w_) throw std::invalid_argument("CompressionType: None, Snappy, Zlib, Zstd only (Lz4: the crate's Err)");
+    mtblx_writer_set_level(w_, level);
   }
   Writer(const Writer&) = delete;
   Writer& operator=(const Writer&) = delete;
@@ -214,14 +215,15 @@ class Writer {
 class WriterBuilder {   // src/writer.rs:15-80
  public:
   WriterBuilder& compression_type(CompressionType c) { c_ = c; return *this; }
-  WriterBuilder& compression_level(uint32_t) { return *this; }   // snappy has no level
+  WriterBuilder& compression_level(uint32_t l) { level_ = l; return *this; }
   WriterBuilder& block_size(uint64_t n) { bs_ = std::max(n, MIN_BLOCK_SIZE); return *this; }
   WriterBuilder& block_restart_interval(uint64_t n) { iv_ = n; return *this; }
-  Writer memory() const { return Writer(bs_, iv_, c_); }
+  Writer memory() const { return Writer(bs_, iv_, c_, level_); }
 
  private:
   CompressionType c_ = CompressionType::None;
   uint64_t bs_ = DEFAULT_BLOCK_SIZE, iv_ = DEFAULT_BLOCK_RESTART_INTERVAL;
+  uint32_t level_ = 0;   // DEFAULT_COMPRESSION_LEVEL (src/lib.rs:8)
 };
 inline Writer Writer::memory() { return WriterBuilder().memory(); }
 
@@ -316,7 +318,6 @@ inline Reader::Reader(const uint8_t* data, size_t len, bool verify) : file_(data
   if (mtblx_read_footer(file_.data(), file_.size(), &f) != MTBLX_OK) throw Error(static_cast<MtblError>(f.err));
   std::memcpy(&meta_, f.meta, sizeof(meta_));
   version_ = f.version;
-  if (meta_.compression_algorithm > 1) throw std::invalid_argument("zlib / zstd files are out of scope");
   uint64_t coff = 0, clen = 0;
   int panic = 0;
   const int rc = mtblx_frame_block(file_.data(), file_.size(), version_, meta_.index_block_offset, verify ? 1 : 0,
@@ -360,47 +361,33 @@ inline Reader::Reader(const uint8_t* data, size_t len, bool verify) : file_(data
       bad = download<uint8_t>(d_bad.p, nent);
     }
   }
-  // Reader::block's decompression (src/reader.rs:166-170): snappy on the host (compression
-  // stays on the host per the north star); then one device decode of every block
+  // Reader::block's decompression (src/reader.rs:166-170), any CompressionType, on the host
+  // (compression stays on the host per the north star: mtblx_decompress_blocks); then one
+  // device decode of every block
   std::vector<uint8_t> zerr(nent, 0);
-  if (nent && meta_.compression_algorithm == 1) {
-    std::vector<uint64_t> uoff(nent, 0), ulen(nent, 0);
-    uint64_t tot = 0;
-    for (uint32_t i = 0; i < nent; ++i) {
-      uint64_t u = 0;
-      if (dst[i] != MTBLX_DIR_OK ||
-          mtblx_snappy_uncompressed_len(file_.data() + boff[i], blen[i], &u) != MTBLX_SNAPPY_OK || u > 0xFFFFFFFFull) {
-        zerr[i] = dst[i] == MTBLX_DIR_OK;
-        u = 0;
-      }
-      uoff[i] = tot;
-      ulen[i] = u;
-      tot += u;
-    }
-    Bytes ubuf(tot + 1);
+  if (nent && meta_.compression_algorithm != 0) {
+    std::vector<uint64_t> so(nent, 0), uoff(nent, 0), ulen(nent, 0);
+    std::vector<uint32_t> sn(nent, 0);
     std::vector<int32_t> zst(nent, 0);
-    std::vector<uint64_t> so(nent), su(nent), sl(nent);
-    std::vector<uint32_t> sn(nent);
-    uint32_t m = 0;
-    std::vector<uint32_t> idxs;
     for (uint32_t i = 0; i < nent; ++i)
-      if (dst[i] == MTBLX_DIR_OK && !zerr[i]) {
-        so[m] = boff[i]; sn[m] = blen[i]; su[m] = uoff[i]; sl[m] = ulen[i];
-        idxs.push_back(i);
-        ++m;
-      }
-    mtblx_snappy_decompress_blocks(file_.data(), so.data(), sn.data(), ubuf.data(), su.data(), sl.data(), zst.data(),
-                                   m, 16);
-    for (uint32_t q = 0; q < m; ++q)
-      if (zst[q] != MTBLX_SNAPPY_OK) zerr[idxs[q]] = 1;
+      if (dst[i] == MTBLX_DIR_OK) { so[i] = boff[i]; sn[i] = blen[i]; }
+    uint8_t* ubuf = nullptr;
+    mtblx_decompress_blocks(static_cast<uint32_t>(meta_.compression_algorithm), file_.data(), so.data(), sn.data(),
+                            nent, 16, &ubuf, uoff.data(), ulen.data(), zst.data());
+    if (!ubuf) throw std::bad_alloc();
     std::vector<uint32_t> ul(nent);
     uint32_t mx = 0;
+    uint64_t tot = 0;
     for (uint32_t i = 0; i < nent; ++i) {
+      zerr[i] = dst[i] == MTBLX_DIR_OK && zst[i] != MTBLX_CODEC_OK;
+      if (ulen[i] > 0xFFFFFFFFull) { mtblx_free(ubuf); throw std::runtime_error("decompressed block >= 4 GiB"); }
       ul[i] = zerr[i] ? 0u : (uint32_t)ulen[i];
       mx = std::max(mx, ul[i]);
+      tot = std::max(tot, uoff[i] + ulen[i]);
     }
-    DevBuf d_u = upload(ubuf.data(), ubuf.size()), d_uo = upload(uoff.data(), nent), d_ul = upload(ul.data(), nent);
-    dec_ = decode_batch(d_u.as<uint8_t>(), ubuf.size(), d_uo.as<uint64_t>(), d_ul.as<uint32_t>(), nent, mx);
+    DevBuf d_u = upload(ubuf, tot + 1), d_uo = upload(uoff.data(), nent), d_ul = upload(ul.data(), nent);
+    mtblx_free(ubuf);
+    dec_ = decode_batch(d_u.as<uint8_t>(), tot + 1, d_uo.as<uint64_t>(), d_ul.as<uint32_t>(), nent, mx);
   } else if (nent) {
     std::vector<uint32_t> l2(blen);
     for (uint32_t i = 0; i < nent; ++i)

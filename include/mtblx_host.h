@@ -75,11 +75,37 @@ uint64_t mtblx_snappy_decompress_blocks(const uint8_t* file, const uint64_t* blk
                                         uint8_t* dst, const uint64_t* dst_off, const uint64_t* dst_len, int32_t* st,
                                         uint64_t nblk, uint32_t threads);
 
-/* Writer (src/writer.rs).  compression: 0 = None, 1 = Snappy (data blocks compressed with
- * mtblx_snappy_compress; the index block is always None, src/writer.rs:165-173); other values
- * return NULL (zlib / zstd are out of scope). */
+/* ---- host block (de)compression, every CompressionType (src/compression.rs:57-81) ----
+ * compression: 0 None, 1 Snappy (the in-repo raw codec above), 2 Zlib (system zlib: the
+ * zlib-wrapped stream flate2's ZlibDecoder / ZlibEncoder read and write), 5 Zstd (libzstd.so.1
+ * loaded at run time: the C library the crate zstd 0.5 wraps; all frames until the input
+ * ends, stream::copy_decode); 3 Lz4 / 4 Lz4hc: the crate's Err "unsupported".  A decoder
+ * error is the crate's io::Error -> Error::Io (Reader::block, src/reader.rs:166).
+ * Compressed BYTES are not pinned to the crate's encoders. */
+#define MTBLX_CODEC_OK 0
+#define MTBLX_CODEC_CORRUPT 1       /* decoder / encoder error -> Error::Io */
+#define MTBLX_CODEC_UNSUPPORTED 2   /* Lz4 / Lz4hc / unknown, or libzstd.so.1 not loadable */
+int mtblx_codec_available(uint32_t compression);   /* 1 if this host can (de)compress it */
+/* *out malloc'd (free with mtblx_free); returns MTBLX_CODEC_* */
+int mtblx_decompress(uint32_t compression, const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len);
+int mtblx_compress(uint32_t compression, uint32_t level, const uint8_t* src, uint64_t n, uint8_t** out,
+                   uint64_t* out_len);
+/* batch for Reader::block's decompression step: block b's stored bytes file[blk_off[b] ..
+ * + blk_len[b]) decompressed by `threads` host threads (0 = 16) into ONE malloc'd buffer *dst
+ * (mtblx_free): block b at (*dst)[dst_off[b] .. + dst_len[b]) (16-byte aligned starts, length 0
+ * on failure); st[b] (may be NULL) = MTBLX_CODEC_*; returns the number of failed blocks.  The
+ * {*dst, dst_off, dst_len} triple is directly a decode batch directory (mtblx_block_batch). */
+uint64_t mtblx_decompress_blocks(uint32_t compression, const uint8_t* file, const uint64_t* blk_off,
+                                 const uint32_t* blk_len, uint64_t nblk, uint32_t threads, uint8_t** dst,
+                                 uint64_t* dst_off, uint64_t* dst_len, int32_t* st);
+
+/* Writer (src/writer.rs).  compression: 0 None, 1 Snappy, 2 Zlib, 5 Zstd: data blocks are
+ * compressed with mtblx_compress (the index block never, src/writer.rs:165-173); returns NULL
+ * for other values or a codec this host lacks.  mtblx_writer_set_level =
+ * WriterBuilder::compression_level (default 0, src/lib.rs:8). */
 typedef struct mtblx_writer mtblx_writer;
 mtblx_writer* mtblx_writer_new(uint64_t block_size, uint64_t restart_interval, uint32_t compression);
+int mtblx_writer_set_level(mtblx_writer* w, uint32_t level);
 /* MTBLX_OK, or MTBLX_E_FORMAT where the reference panics ("out-of-order key", ...) */
 int mtblx_writer_insert(mtblx_writer* w, const uint8_t* key, uint64_t klen, const uint8_t* val, uint64_t vlen);
 int mtblx_writer_insert_batch(mtblx_writer* w, const uint8_t* keys, const uint64_t* key_end, const uint8_t* vals,

@@ -665,6 +665,69 @@ int32_t oracle_writer_finish(oracle_writer* w, uint8_t** out, uint64_t* out_len)
   return 0;
 }
 
+/* ==================== zlib / zstd decompression ====================
+ * src/compression.rs:85-92 (flate2 ZlibDecoder::read_to_end: a zlib-wrapped deflate stream,
+ * bytes after its end unread, input ending first -> Err) and :140-145 (zstd::stream::copy_decode:
+ * every frame until the input ends).  Both are format-defined; the oracle calls the system
+ * zlib and libzstd.so.1 (the C library the zstd crate wraps) -- test infrastructure, the
+ * crates themselves are not in /root/reference. */
+#include <dlfcn.h>
+#include <zlib.h>
+
+int32_t oracle_zlib_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len) {
+  z_stream z;
+  memset(&z, 0, sizeof z);
+  if (inflateInit(&z) != Z_OK) return 1;
+  uint64_t cap = 4096, len = 0;
+  uint8_t* o = (uint8_t*)malloc(cap);
+  z.next_in = (Bytef*)s;
+  z.avail_in = (uInt)n;
+  for (;;) {
+    if (len == cap) { cap *= 2; o = (uint8_t*)realloc(o, cap); }
+    z.next_out = o + len;
+    z.avail_out = (uInt)(cap - len);
+    int r = inflate(&z, Z_NO_FLUSH);
+    len = cap - z.avail_out;
+    if (r == Z_STREAM_END) break;
+    if (r != Z_OK && !(r == Z_BUF_ERROR && z.avail_out == 0)) { inflateEnd(&z); free(o); return 1; }
+  }
+  inflateEnd(&z);
+  *out = o; *out_len = len;
+  return 0;
+}
+
+typedef struct { const void* src; size_t size; size_t pos; } ozin;
+typedef struct { void* dst; size_t size; size_t pos; } ozout;
+int32_t oracle_zstd_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len) {
+  static void* h = NULL;
+  if (!h) h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return 1;
+  void* (*create)(void) = (void* (*)(void))dlsym(h, "ZSTD_createDStream");
+  size_t (*freeds)(void*) = (size_t (*)(void*))dlsym(h, "ZSTD_freeDStream");
+  size_t (*init)(void*) = (size_t (*)(void*))dlsym(h, "ZSTD_initDStream");
+  size_t (*dec)(void*, ozout*, ozin*) = (size_t (*)(void*, ozout*, ozin*))dlsym(h, "ZSTD_decompressStream");
+  unsigned (*iserr)(size_t) = (unsigned (*)(size_t))dlsym(h, "ZSTD_isError");
+  if (!create || !freeds || !init || !dec || !iserr) return 1;
+  void* d = create();
+  if (!d || iserr(init(d))) { if (d) freeds(d); return 1; }
+  uint64_t cap = 4096, len = 0;
+  uint8_t* o = (uint8_t*)malloc(cap);
+  ozin in = {s, (size_t)n, 0};
+  size_t last = 0;
+  for (;;) {
+    if (len == cap) { cap *= 2; o = (uint8_t*)realloc(o, cap); }
+    ozout ob = {o + len, (size_t)(cap - len), 0};
+    last = dec(d, &ob, &in);
+    if (iserr(last)) { freeds(d); free(o); return 1; }
+    len += ob.pos;
+    if (in.pos == in.size && ob.pos < ob.size) break;   /* input consumed, output drained */
+  }
+  freeds(d);
+  if (last != 0) { free(o); return 1; }                   /* the input ended inside a frame */
+  *out = o; *out_len = len;
+  return 0;
+}
+
 /* ==================== snappy raw decompression ====================
  * src/compression.rs:116-119 calls snap::raw::Decoder::decompress_vec (crate snap 1.x, not in
  * /root/reference).  Restated from the published snappy format (format_description.txt):
@@ -800,8 +863,13 @@ static int oreader_block(const oreader* r, uint64_t off, const uint8_t** blk, ui
     uint8_t* u; uint64_t ul;
     if (oracle_snappy_decompress(b, sz, &u, &ul)) return ORC_ERR_IO;
     *owned = u; b = u; sz = ul;
+  } else if (r->meta[M_COMP] == 2 || r->meta[M_COMP] == 5) {
+    uint8_t* u; uint64_t ul;
+    const int e = r->meta[M_COMP] == 2 ? oracle_zlib_decompress(b, sz, &u, &ul) : oracle_zstd_decompress(b, sz, &u, &ul);
+    if (e) return ORC_ERR_IO;
+    *owned = u; b = u; sz = ul;
   } else if (r->meta[M_COMP] != 0) {
-    return ORC_ERR_IO;   /* zlib / zstd: out of scope for this oracle */
+    return ORC_ERR_IO;   /* Lz4 / Lz4hc: the crate's Err "unsupported" (src/compression.rs:63-67) */
   }
   int st = oblock_init(b, sz, ro);
   if (st == ORC_ST_INVALID_BLOCK) { free(*owned); *owned = NULL; return ORC_ERR_INVALID_BLOCK; }

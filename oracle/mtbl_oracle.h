@@ -137,6 +137,10 @@ int32_t oracle_file_scan(const uint8_t* data, uint64_t len, int32_t verify_check
                          uint64_t max_records, oracle_scan_result* res);
 void oracle_scan_free(oracle_scan_result* res);
 
+/* zlib / zstd block decompression (src/compression.rs:85-92, :140-145): 0 ok, *out malloc'd */
+int32_t oracle_zlib_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len);
+int32_t oracle_zstd_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,8 @@
 #include "mtblx.h"
 #include "mtblx_host.h"
 
+int mtblx_compress_vec(uint32_t c, uint32_t level, const uint8_t* src, uint64_t n, std::vector<uint8_t>& out);
+
 namespace {
 
 inline void wr32(uint8_t* p, uint32_t v) { memcpy(p, &v, 4); }
@@ -158,6 +160,8 @@ extern "C" uint32_t mtblx_crc32c(const uint8_t* d, uint64_t n) {
 struct mtblx_writer {
   uint64_t meta[9] = {0};  // footer order, src/metadata.rs:61-79
   uint32_t compression = 0;
+  uint32_t level = 0;        // WriterBuilder::compression_level (DEFAULT_COMPRESSION_LEVEL = 0)
+  bool failed = false;       // a compressor error: Err(Error::Io) from insert / into_inner
   BlockBuilder data, index;
   std::vector<uint8_t> last_key;
   uint64_t last_offset = 0, pending_offset = 0;
@@ -180,11 +184,11 @@ struct mtblx_writer {
   uint64_t write_block(BlockBuilder& b, bool is_data) {
     b.finish(scratch);
     const std::vector<uint8_t>* stored = &scratch;
-    if (is_data && compression == 1) {
-      zbuf.resize(mtblx_snappy_max_compressed_len(scratch.size()));
-      uint64_t zl = 0;
-      mtblx_snappy_compress(scratch.data(), scratch.size(), zbuf.data(), zbuf.size(), &zl);
-      zbuf.resize(zl);
+    if (is_data && compression != 0) {   // compress (src/compression.rs:70-81), codecs_host.cpp
+      if (mtblx_compress_vec(compression, level, scratch.data(), scratch.size(), zbuf) != MTBLX_CODEC_OK) {
+        failed = true;   // the crate returns the io::Error from insert / into_inner
+        zbuf.clear();
+      }
       stored = &zbuf;
     }
     uint8_t hdr[14];
@@ -215,8 +219,15 @@ struct mtblx_writer {
 };
 
 extern "C" mtblx_writer* mtblx_writer_new(uint64_t block_size, uint64_t restart_interval, uint32_t compression) {
-  if (compression > 1) return nullptr;  // None and Snappy only (mtblx_host.h)
+  // None, Snappy, Zlib, Zstd (Lz4 / Lz4hc: the crate's compress returns Err "unsupported")
+  if (!(compression <= 2 || compression == 5) || !mtblx_codec_available(compression)) return nullptr;
   return new mtblx_writer(block_size, restart_interval, compression);
+}
+
+extern "C" int mtblx_writer_set_level(mtblx_writer* w, uint32_t level) {
+  if (!w) return MTBLX_E_INVAL;
+  w->level = level;
+  return MTBLX_OK;
 }
 
 extern "C" void mtblx_writer_free(mtblx_writer* w) { delete w; }
@@ -260,7 +271,7 @@ extern "C" int mtblx_writer_insert_batch(mtblx_writer* w, const uint8_t* keys, c
 
 extern "C" int mtblx_writer_finish(mtblx_writer* w, uint8_t** out, uint64_t* out_len) {  // into_inner (:155-181)
   if (!w || w->poisoned || !out || !out_len) return MTBLX_E_INVAL;
-  if (!w->flush()) return MTBLX_E_FORMAT;
+  if (!w->flush() || w->failed) return MTBLX_E_FORMAT;
   if (w->pending_index_entry) {
     uint8_t enc[10];
     uint32_t el = venc64(enc, w->last_offset);

@@ -173,7 +173,8 @@ struct mtblx_pipe {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   Pool pool;
-  explicit mtblx_pipe(uint32_t threads) : pool(threads) {}
+  uint32_t threads;
+  explicit mtblx_pipe(uint32_t nthreads) : pool(nthreads), threads(nthreads) {}
 };
 
 namespace {
@@ -291,9 +292,43 @@ extern "C" void mtblx_pipe_free(mtblx_pipe* p) {
 extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t file_len, uint32_t compression,
                                  const uint64_t* blk_off, const uint32_t* blk_len, uint32_t nblk,
                                  const mtblx_decoded* out, mtblx_pipe_stats* stats) {
-  if (!p || !out || (nblk && (!file || !blk_off || !blk_len)) || compression > 1) return MTBLX_E_INVAL;
+  if (!p || !out || (nblk && (!file || !blk_off || !blk_len)) || compression > 5) return MTBLX_E_INVAL;
   if (nblk && (!out->nrec || !out->rec_base || !out->key_base || !out->val_base || !out->status || !out->totals))
     return MTBLX_E_INVAL;
+  if (compression >= 2) {
+    // Zlib / Zstd (and Lz4 / Lz4hc, every block Err): the decompressed lengths are not in the
+    // stored bytes, so the whole directory is decompressed first on the host (16 threads,
+    // codecs_host.cpp), then streamed as CompressionType::None; failed blocks are
+    // MTBLX_ST_DECOMPRESS (Reader::block's Err(Error::Io), src/reader.rs:166)
+    const double t0 = now_s();
+    std::vector<uint64_t> doff(nblk ? nblk : 1), dlen(nblk ? nblk : 1);
+    std::vector<int32_t> zst(nblk ? nblk : 1);
+    uint8_t* dbuf = nullptr;
+    mtblx_decompress_blocks(compression, file, blk_off, blk_len, nblk, p->threads, &dbuf, doff.data(), dlen.data(),
+                            zst.data());
+    if (!dbuf) return MTBLX_E_INVAL;
+    std::vector<uint32_t> dl(nblk ? nblk : 1);
+    uint64_t dtotal = 0;
+    for (uint32_t b = 0; b < nblk; ++b) {
+      if (dlen[b] > 0xFFFFFFFFull) { free(dbuf); return MTBLX_E_INVAL; }   // >= 4 GiB decompressed block
+      dl[b] = (uint32_t)dlen[b];
+      dtotal = std::max(dtotal, doff[b] + dlen[b]);
+    }
+    const double t_dz = now_s() - t0;
+    const int rc = mtblx_pipe_decode(p, dbuf, dtotal, 0, doff.data(), dl.data(), nblk, out, stats);
+    if (rc == MTBLX_OK) {
+      uint32_t bad = 0;
+      for (uint32_t b = 0; b < nblk; ++b)
+        if (zst[b] != MTBLX_CODEC_OK) { out->status[b] = MTBLX_ST_DECOMPRESS; ++bad; }
+      if (stats) {
+        stats->stage_seconds += t_dz;
+        stats->seconds += t_dz;
+        stats->decompress_errors = bad;
+      }
+    }
+    free(dbuf);
+    return rc;
+  }
   if (hipSetDevice(p->dev) != hipSuccess) return MTBLX_E_HIP;
   const double t_start = now_s();
   mtblx_pipe_stats st{};

@@ -20,6 +20,7 @@ i32p = C.POINTER(C.c_int32)
 MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT, MTBLX_E_TIMEOUT = 0, -1, -2, -3, -4, -5
 ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW, ST_DECOMPRESS = range(7)
 SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL = range(3)
+CODEC_OK, CODEC_CORRUPT, CODEC_UNSUPPORTED = range(3)
 DIR_OK, DIR_PANIC, DIR_UNSUPPORTED = range(3)
 GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP = range(5)
 
@@ -34,6 +35,7 @@ EXPORTS = [
     "mtblx_pipe_decode", "mtblx_pipe_set", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
+    "mtblx_codec_available", "mtblx_decompress", "mtblx_compress", "mtblx_decompress_blocks", "mtblx_writer_set_level",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
@@ -156,6 +158,17 @@ def lib() -> C.CDLL:
                                          C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, u64p,
                                          C.c_void_p]
         L.mtblx_encode_index.restype = C.c_int
+        L.mtblx_codec_available.argtypes = [C.c_uint32]
+        L.mtblx_codec_available.restype = C.c_int
+        L.mtblx_decompress.argtypes = [C.c_uint32, C.c_void_p, C.c_uint64, C.POINTER(u8p), u64p]
+        L.mtblx_decompress.restype = C.c_int
+        L.mtblx_compress.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.POINTER(u8p), u64p]
+        L.mtblx_compress.restype = C.c_int
+        L.mtblx_decompress_blocks.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                              C.POINTER(u8p), C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mtblx_decompress_blocks.restype = C.c_uint64
+        L.mtblx_writer_set_level.argtypes = [C.c_void_p, C.c_uint32]
+        L.mtblx_writer_set_level.restype = C.c_int
         L.mtblx_stream_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
         L.mtblx_stream_copy.restype = C.c_int
         L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]

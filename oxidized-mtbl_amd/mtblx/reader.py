@@ -115,9 +115,7 @@ class Reader:
             raise MtblError(int(f.err))
         self.meta = list(f.meta)
         self.version = int(f.version)
-        self.compression = int(self.meta[2])
-        if self.compression not in (0, 1):
-            raise NotImplementedError("zlib / zstd files are out of scope (DESIGN.md §9); None and Snappy only")
+        self.compression = int(self.meta[2])   # 0..5 (read_footer rejects others: InvalidCompressionAlgorithm)
         idx_off = int(self.meta[0])
         if host is None:   # index block bytes to the host (framing + checksum)
             hi = self.len - METADATA_SIZE
@@ -175,10 +173,10 @@ class Reader:
     def _decode_all(self):
         off, ln, st, bad = self.directory()
         self.zerr = None
-        if self.compression == 1 and self.nent:
+        if self.compression != 0 and self.nent:
             # Reader::block decompresses after the checksum (src/reader.rs:166-170): on the
             # host, as the north star keeps src/compression.rs there; then one device decode
-            buf, uoff, uln, self.zerr = self._snappy_stage(off, ln, st)
+            buf, uoff, uln, self.zerr = self._host_stage(off, ln, st)
             ml = int(uln.max()) if uln.size else 0
             self._dbatch = codec.DeviceBatch.from_host(buf, uoff, uln, device=self.file.device)
         else:
@@ -188,7 +186,11 @@ class Reader:
         torch.cuda.synchronize()
         return off, ln, st, bad
 
-    def _snappy_stage(self, off, ln, st):
+    def _host_stage(self, off, ln, st):
+        """Reader::block's decompression step (src/reader.rs:166-170 -> src/compression.rs:57-68)
+        on the host for every block the directory frames, any CompressionType:
+        mtblx_decompress_blocks (16 threads; codecs_host.cpp).  A decoder error is the crate's
+        Err(Error::Io); Lz4 / Lz4hc are its Err "unsupported" (also Error::Io)."""
         L = _lib.lib()
         host = self.file.cpu().numpy()
         o = off.cpu().numpy().view(np.uint64).copy()
@@ -196,31 +198,22 @@ class Reader:
         ok = st.cpu().numpy() == _lib.DIR_OK
         n[~ok] = 0
         o[~ok] = 0
-        ulen = np.zeros(o.size, np.uint64)
-        zerr = np.zeros(o.size, np.int32)
-        for i in np.nonzero(ok)[0]:
-            u = C.c_uint64(0)
-            if L.mtblx_snappy_uncompressed_len(host.ctypes.data + int(o[i]), int(n[i]), C.byref(u)) != 0 or \
-                    u.value > 0xFFFFFFFF:
-                zerr[i] = _lib.SNAPPY_CORRUPT
-            else:
-                ulen[i] = u.value
-        uoff = np.zeros(o.size, np.uint64)
-        if o.size > 1:
-            uoff[1:] = np.cumsum(ulen[:-1], dtype=np.uint64)
-        total = int(ulen.sum(dtype=np.uint64))
-        buf = np.zeros(max(total, 1), np.uint8)
-        zst = np.zeros(o.size, np.int32)
-        todo = np.nonzero(ok & (zerr == 0))[0]
-        if todo.size:
-            sel = lambda a: np.ascontiguousarray(a[todo])  # noqa: E731
-            so, sn, su, sl = sel(o), sel(n), sel(uoff), sel(ulen)
-            L.mtblx_snappy_decompress_blocks(host.ctypes.data, so.ctypes.data, sn.ctypes.data, buf.ctypes.data,
-                                             su.ctypes.data, sl.ctypes.data, zst.ctypes.data, todo.size, 16)
-            zerr[todo] = zst[: todo.size]
-        uln = ulen.astype(np.uint32)
-        uln[zerr != 0] = 0
-        return buf, uoff, uln, zerr
+        nb = o.size
+        dst = _lib.u8p()
+        doff = np.zeros(max(nb, 1), np.uint64)
+        dlen = np.zeros(max(nb, 1), np.uint64)
+        zst = np.zeros(max(nb, 1), np.int32)
+        L.mtblx_decompress_blocks(self.compression, host.ctypes.data, o.ctypes.data, n.ctypes.data, nb, 16,
+                                  C.byref(dst), doff.ctypes.data, dlen.ctypes.data, zst.ctypes.data)
+        total = int(doff[nb - 1]) + ((int(dlen[nb - 1]) + 15) & ~15) if nb else 0
+        buf = np.empty(max(total, 16), np.uint8)
+        C.memmove(buf.ctypes.data, dst, total)
+        L.mtblx_free(dst)
+        zerr = zst[:nb].copy()
+        zerr[~ok] = 0
+        if (dlen[:nb] > 0xFFFFFFFF).any():
+            raise NotImplementedError("decompressed block >= 4 GiB")
+        return buf, doff[:nb].copy(), dlen[:nb].astype(np.uint32), zerr
 
     def iter(self) -> Scan:
         """ReaderIntoIter (mode Iter) to the end: the records yielded and how it ends."""

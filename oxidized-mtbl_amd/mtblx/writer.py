@@ -55,19 +55,21 @@ class WriterBuilder:
         return self
 
     def memory(self) -> "Writer":
-        return Writer(self._block_size, self._interval, self._compression)
+        return Writer(self._block_size, self._interval, self._compression, self._level)
 
     build = memory
 
 
 class Writer:
     def __init__(self, block_size=DEFAULT_BLOCK_SIZE, restart_interval=DEFAULT_BLOCK_RESTART_INTERVAL,
-                 compression=CompressionType.None_):
+                 compression=CompressionType.None_, level=0):
         L = _lib.lib()
         self._w = L.mtblx_writer_new(int(block_size), int(restart_interval), int(compression))
         if not self._w:
-            raise NotImplementedError("CompressionType.None_ and CompressionType.Snappy only (zlib / zstd are out "
-                                      "of scope, DESIGN.md §9)")
+            # Lz4 / Lz4hc: the crate's compress returns Err "unsupported" (src/compression.rs:70-81)
+            raise NotImplementedError(f"compression {compression}: None, Snappy, Zlib and Zstd only "
+                                      "(Zstd needs libzstd.so.1 on this host)")
+        L.mtblx_writer_set_level(self._w, int(level))
         self.block_dir = None
 
     @staticmethod

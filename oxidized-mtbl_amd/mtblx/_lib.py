@@ -76,6 +76,14 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libmtblx.so not built ({LIB_PATH}); run `make -C oxidized-mtbl_amd` "
                               "(no CPU fallback exists for the device codec)")
+        # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's): whichever loads
+        # first serves the whole process.  Load torch first, so the device pointers and streams
+        # torch hands us and libmtblx's kernels live in one HIP runtime (the order every
+        # product path takes); without torch, libmtblx uses the system runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         L.mtblx_abi_version.restype = C.c_int
         L.mtblx_device_ok.restype = C.c_int

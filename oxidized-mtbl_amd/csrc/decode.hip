@@ -363,6 +363,7 @@ struct TileArgs {
   uint32_t par;     // launch parity: aggregates live in slot `par` of each tile entry
   uint32_t hw_other;
   unsigned long long inject;   // debug: bits ORed into totals[3] (MTBLX_DEBUG_FLAGS, mtblx_impl_run)
+  uint32_t flags_direct;       // k_decode_pipe: flags go straight to totals[3] (pipe_zero_flags)
 };
 
 // Workspace header (byte 128 of the workspace).  The workspace carries state from call to
@@ -407,7 +408,9 @@ __device__ __forceinline__ void ws_begin(TileArgs& a) {
     a.lbw[kTileWords * t + (a.par ^ 1u)] = 0;
 }
 
-__device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bit) { atomicOr(&a.hdr->flags, bit); }
+__device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bit) {
+  atomicOr(a.flags_direct ? reinterpret_cast<unsigned long long*>(a.totals + 3) : &a.hdr->flags, bit);
+}
 
 // Bounded waits.  A wait on another workgroup (look-back) or on another wave gives up after
 // kWaitTicks of wall time (s_memrealtime, 100 MHz) and the launch reports a timeout (totals[3]
@@ -443,18 +446,35 @@ __device__ __forceinline__ void ws_end(const TileArgs& a) {
     const uint32_t old = __hip_atomic_fetch_add(&a.hdr->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 #endif
     if (old == gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const unsigned long long f = __hip_atomic_load(&a.hdr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long f = __hip_atomic_exchange(&a.hdr->flags, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       a.totals[3] = f | a.inject;
-      __hip_atomic_store(&a.hdr->flags, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t h = __hip_atomic_load(&a.hdr->hw[a.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.ntiles > h) __hip_atomic_store(&a.hdr->hw[a.par], a.ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_max(&a.hdr->hw[a.par], a.ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_exchange(&a.hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(&a.hdr->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
+
+// k_decode_pipe's launch bookkeeping needs no end-of-launch fan-in (a returning atomic that
+// every workgroup waits on took up to ~15 us under the launch's own store traffic, measured):
+//  - totals[3] is zeroed by the walker of tile 0 right before it publishes A(0), and every
+//    flag is ORed straight into totals[3] (a.flags_direct).  Every look-back -- where
+//    overflow flags are set -- waits, directly or through its workgroup's previous tile, on
+//    A(0); so every OR lands after the zeroing.
+//  - the workgroup owning the last tile bumps the epoch and the high-water mark at its own
+//    end: that tile's look-back waited on the aggregate of the G-1 tiles before it, one from
+//    every other workgroup (G <= ntiles), so all of them have passed ws_begin by then.
+__device__ __forceinline__ void pipe_zero_flags(const TileArgs& a) {   // walker of tile 0, lane 0
+  __hip_atomic_store(a.totals + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // performed before A(0) is published
+}
+
+__device__ __forceinline__ void pipe_close(const TileArgs& a) {   // last tile's workgroup, thread 0, at its end
+  if (a.inject) __hip_atomic_fetch_or(a.totals + 3, a.inject, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(&a.hdr->hw[a.par], a.ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(&a.hdr->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Contiguous range of tile t: [r0, r1) of the data buffer (r0 16-aligned), or r1 = 0 if the
 // tile's blocks do not sit in one range that fits the staging buffer.
@@ -1478,6 +1498,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)ik, 63) + wave_sum32(gk);
   const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)iv, 63) + wave_sum32(gv);
   if (lane == 0) {
+    if (t == 0) pipe_zero_flags(a);
     lb_publish(a, t, tr, tk, tv);
     B.ttot[0] = tr; B.ttot[1] = tk; B.ttot[2] = tv;
     B.nint = nint;
@@ -1956,6 +1977,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   ST.init();
   TL(0);
   ws_begin(a);
+  a.flags_direct = 1;
   if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; }
   if constexpr (P::VERIFY) {
     for (int i = tid; i < 256; i += kPipeThreads) {   // slicing-by-4 tables from the byte table
@@ -2112,7 +2134,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wv >= P::COPY0) TLW(12 + (wv & 1));   // copy waves' drains (two of them)
   TLW(14 + (wv == 1));                       // wave 0 / wave 1 drains (the slots race; diagnostic)
-  ws_end(a);
+  if (g == (a.ntiles - 1) % G && tid == 0) pipe_close(a);
   TL(5);
 #ifdef MTBLX_STAMPS
   if (tid == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][6] = nloc;

@@ -184,6 +184,80 @@ int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int veri
               uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
               uint64_t* val_off, uint64_t* val_len, void* stream);
 
+/* ---- seek-based iteration (ReaderIntoIter::new_from / seek, src/reader.rs:256-335) ----
+ * Three device primitives; the host drives the iterator state (block_offset quirk, first /
+ * valid, index position) exactly as src/reader.rs:219-405 does, and decodes the blocks after
+ * the sought one with mtblx_decode_blocks -- only the blocks the iteration touches.
+ *
+ * (1) index_iter.seek(key) + the landed entry's block_at_index / Reader::block
+ *     (src/block.rs:154-194, src/reader.rs:139-186), one wave per query, on a fresh index
+ *     iterator.  All fields are outputs. */
+#define MTBLX_SEEK_OK 0
+#define MTBLX_SEEK_ERR 1          /* Err(InvalidBlock) from Block::init                       */
+#define MTBLX_SEEK_PANIC 2        /* the reference panics                                     */
+#define MTBLX_SEEK_LOOP 3         /* the reference never returns (zero-progress entry)        */
+#define MTBLX_SEEK_UNSUPPORTED 4  /* block >= 4 GiB, or a key > 64 KiB in the emitting seek    */
+typedef struct mtblx_index_seek {
+  int32_t status;          /* of the index seek: OK / PANIC / LOOP                               */
+  int32_t valid;           /* index_iter.get() is Some after the seek                             */
+  uint64_t entry;          /* the index iterator's current entry offset in the index block        */
+  uint64_t block_off;      /* varint_decode64(entry value): the file offset ReaderIntoIter keeps  */
+  int32_t block_status;    /* Reader::block(block_off): OK / ERR / PANIC (UNSUPPORTED >= 4 GiB);
+                              ERR / UNSUPPORTED come from Block::init on the stored bytes, which
+                              is only meaningful for uncompressed files                        */
+  int32_t pad;
+  uint64_t data_off, data_len;   /* the block content (framed; crc32c checked when verify)       */
+} mtblx_index_seek;
+int mtblx_index_seek_batch(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
+                           uint64_t index_off, uint64_t index_len, const uint8_t* keys, const uint64_t* key_end,
+                           uint32_t nq, mtblx_index_seek* out, void* stream);
+
+/* (2) BlockIter::seek(key) (or seek_to_first) on one block content, then the records the
+ *     iterator yields from there (get / next until get() is None), keys materialised.  One
+ *     workgroup per query.  kcap = the iterator's key Vec capacity (src/block.rs:132 asserts
+ *     on it): 0 for a fresh BlockIter::init, or a re-seeked iterator's.  Query q writes its
+ *     records to out_keys + q*keys_cap, out_vals + q*vals_cap, and END offsets (relative to
+ *     the query's base) to key_end_out/val_end_out + q*rec_cap, plus the iterator's key
+ *     capacity at each record to kcap_out + q*rec_cap (may be NULL).  On OVERFLOW the counts
+ *     are what is needed.  keys: the seek targets (ignored for first). */
+#define MTBLX_EMIT_END 0        /* get() returned None: the block is exhausted                 */
+#define MTBLX_EMIT_PANIC 1      /* next() / get() panics after the emitted records             */
+#define MTBLX_EMIT_LOOP 2       /* next() never returns after the emitted records              */
+#define MTBLX_EMIT_MAX 3        /* max_records emitted                                         */
+#define MTBLX_EMIT_OVERFLOW 4   /* a capacity was too small (counts = needed)                  */
+typedef struct mtblx_block_seek {
+  uint64_t data_off, data_len;   /* in: block content in `data`                                  */
+  uint64_t kcap;                 /* in: key capacity (0 = fresh); out: after the emitted records  */
+  uint64_t max_records;          /* in                                                            */
+  int32_t first;                 /* in: 1 = seek_to_first instead of seek(key)                    */
+  int32_t status;                /* out: MTBLX_SEEK_* of Block::init / BlockIter::init / the seek */
+  int32_t end;                   /* out: MTBLX_EMIT_*                                             */
+  int32_t has_val;               /* out: an entry was parsed (BlockIter::val is Some)             */
+  uint64_t entry;                /* out: the iterator's current entry offset after the seek       */
+  uint64_t nrec, key_bytes, val_bytes;   /* out                                                   */
+  uint64_t last_voff, last_vlen; /* out: `val` of the last parsed entry (content offsets) -- what
+                                    Reader::get returns when next() hits Err (src/reader.rs:111-122) */
+} mtblx_block_seek;
+int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end, uint32_t nq,
+                           mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
+                           uint64_t vals_cap, uint64_t* key_end_out, uint64_t* val_end_out, uint64_t* kcap_out,
+                           uint64_t rec_cap, void* stream);
+
+/* (3) the offsets of the entries seek_to_first + next visit in a block (the index block: entry
+ *     i <-> index record i <-> directory entry i), so a seek's landed entry maps to its index
+ *     position.  Parallel over restart intervals when every interval's chain lands on the next
+ *     restart point; otherwise one serial walk.  Writes min(count, cap) offsets; *count (device)
+ *     = entries up to the end of the block or the first entry the scan cannot decode. */
+int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t* offs, uint64_t cap, uint64_t* count,
+                        void* stream);
+
+/* (4) ReaderIntoIter's stop rules (src/reader.rs:385-402) over decoded records: the index of
+ *     the first record whose key fails (type 1 Get: != k, 2 GetPrefix: !starts_with(k), 3
+ *     GetRange: > k), or n.  key_end: absolute END offsets (int64).  *first_fail (device) is
+ *     min-reduced: set it to n before the call. */
+int mtblx_key_filter(const uint8_t* keys, const uint64_t* key_end, uint64_t n, int32_t type, const uint8_t* k,
+                     uint64_t klen, uint64_t* first_fail, void* stream);
+
 /* ---- encode side on the device: Writer's block cut + BlockBuilder + write_block framing ----
  * Records (device): key r = keys[r ? key_end[r-1] : 0 .. key_end[r]), value likewise (u64 END
  * offsets from record 0), in Writer::insert order (strictly increasing keys). */

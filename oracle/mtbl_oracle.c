@@ -1014,6 +1014,151 @@ out:
   return 0;
 }
 
+/* ============ ReaderIntoIter with mid-iteration seek: src/reader.rs:219-405 ============
+ * The iterator as a state machine, driven by a script of next() / seek() calls, so the
+ * stateful parts of the reference are pinned: ReaderIntoIter::seek (:302-335) re-loads the
+ * block only when the landed index entry's offset differs from `block_offset` -- a field
+ * that new/new_from set to 0 and next() never updates (:244-246, :269-271, :362-366) -- so a
+ * seek can re-seek whatever block the iterator currently holds; the re-seeked BlockIter
+ * keeps its key Vec capacity (:327-329, src/block.rs:106-112). */
+typedef struct {
+  oreader r;
+  oiter idx, bi;
+  int have_bi, first, valid, type;   /* type: 0 Iter, 1 Get, 2 GetPrefix, 3 GetRange */
+  const uint8_t* k; uint64_t kl;     /* ReaderIntoIter::k */
+  uint64_t block_offset;
+} ostate;
+
+enum { OS_SOME = 1, OS_NONE = 0, OS_LOOP = -2 };   /* + PANIC (-1), -(10 + err) = Some(Err) / Err */
+
+/* ReaderIntoIter::next (:337-405) */
+static int ostate_next(ostate* s, const uint8_t** k, uint64_t* kl, const uint8_t** v, uint64_t* vl) {
+  if (!s->valid) return OS_NONE;
+  if (!s->have_bi) return OS_NONE;
+  if (!s->first && ovalid(&s->bi)) {
+    if (s->bi.has_next && s->bi.next == s->bi.current) return OS_LOOP;
+    if (oparse_next_key(&s->bi) < 0) return PANIC;
+  }
+  s->first = 0;
+  int g = oget(&s->bi);
+  if (g < 0) return PANIC;
+  if (g == 0) {
+    s->valid = 0;
+    if (!ovalid(&s->idx)) return OS_NONE;                      /* index_iter.next() == false */
+    if (oparse_next_key(&s->idx) < 0) return PANIC;
+    if (!ovalid(&s->idx)) return OS_NONE;
+    oiter nb;
+    int b = oblock_at_index(&s->r, &s->idx, &nb);
+    if (b == PANIC) return PANIC;
+    if (b <= -10) return b;                                   /* Some(Err(e)), valid stays false */
+    if (b == 0) return OS_NONE;
+    oiter_free(&s->bi);
+    s->bi = nb;
+    oseek_to_restart_point(&s->bi, 0);
+    if (oparse_next_key(&s->bi) < 0) return PANIC;
+    g = oget(&s->bi);
+    if (g < 0) return PANIC;
+    s->valid = g == 1;
+    if (!s->valid) return OS_NONE;
+  }
+  *k = s->bi.key; *kl = s->bi.klen; *v = s->bi.d + s->bi.voff; *vl = s->bi.vlen;
+  if (s->type == 1) { if (obytes_cmp(*k, *kl, s->k, s->kl) != 0) s->valid = 0; }
+  else if (s->type == 2) { if (!(s->kl <= *kl && (s->kl == 0 || memcmp(*k, s->k, s->kl) == 0))) s->valid = 0; }
+  else if (s->type == 3) { if (obytes_cmp(*k, *kl, s->k, s->kl) > 0) s->valid = 0; }
+  return s->valid ? OS_SOME : OS_NONE;
+}
+
+/* ReaderIntoIter::seek (:302-335): 0 = Ok(true), PANIC, -(10 + err) = Err */
+static int ostate_seek(ostate* s, const uint8_t* key, uint64_t kl) {
+  if (oseek(&s->idx, key, kl) < 0) return PANIC;
+  int g = oget(&s->idx);
+  if (g < 0) return PANIC;
+  if (g == 0) { s->valid = 0; return 0; }                     /* past the last key */
+  uint64_t off = 0;
+  if (oracle_varint_decode64(s->idx.d + s->idx.voff, s->idx.vlen, &off) < 0) return PANIC;
+  if (s->block_offset != off) {
+    s->block_offset = off;                                    /* updated before the load (:322) */
+    const uint8_t* blk; uint64_t blen, ro; uint8_t* owned;
+    int e = oreader_block(&s->r, off, &blk, &blen, &ro, &owned);
+    if (e == PANIC) return PANIC;
+    if (e > 0) return -10 - e;                                /* `?`: bi, first, valid unchanged */
+    oiter nb;
+    if (oiter_init(&nb, blk, blen, ro)) { free(owned); return PANIC; }
+    nb.owned = owned;
+    if (s->have_bi) oiter_free(&s->bi);
+    s->bi = nb;
+    s->have_bi = 1;
+  }
+  if (s->have_bi && oseek(&s->bi, key, kl) < 0) return PANIC;
+  s->first = 1;
+  s->valid = 1;
+  return 0;
+}
+
+int32_t oracle_iter_script(const uint8_t* data, uint64_t len, int32_t verify, int32_t mode, const uint8_t* key,
+                           uint64_t klen, const uint8_t* key2, uint64_t klen2, const int64_t* ops, uint64_t nops,
+                           const uint8_t* op_keys, const uint64_t* op_key_end, int64_t* op_res,
+                           oracle_scan_result* res) {
+  memset(res, 0, sizeof(*res));
+  for (uint64_t i = 0; i < nops; i++) op_res[2 * i] = op_res[2 * i + 1] = 0;
+  oscan_out o = {res, 0, 0, 0};
+  ostate s;
+  memset(&s, 0, sizeof(s));
+  int e = oreader_open(&s.r, data, len, verify);
+  memcpy(res->meta, s.r.meta, sizeof(s.r.meta));
+  res->version = s.r.version;
+  if (e == PANIC) { res->end = ORC_END_PANIC; return 0; }
+  if (e > 0) { res->end = ORC_END_ERR_OPEN; res->err = e; return 0; }
+  if (oiter_init(&s.idx, s.r.index, s.r.index_len, s.r.ro_index)) { res->end = ORC_END_PANIC; return 0; }
+  s.first = 1; s.valid = 1;
+  s.type = mode == 1 ? 1 : mode == 2 ? 2 : mode == 3 ? 3 : 0;
+  s.k = mode == 3 ? key2 : key;
+  s.kl = mode == 3 ? klen2 : klen;
+  if (mode == 0) {                                            /* new (:231-254) */
+    oseek_to_restart_point(&s.idx, 0);
+    if (oparse_next_key(&s.idx) < 0) { res->end = ORC_END_PANIC; goto out; }
+  } else if (oseek(&s.idx, key, klen) < 0) {                  /* new_from (:256-279) */
+    res->end = ORC_END_PANIC; goto out;
+  }
+  {
+    int b = oblock_at_index(&s.r, &s.idx, &s.bi);
+    if (b == PANIC) { res->end = ORC_END_PANIC; goto out; }
+    if (b <= -10) { res->end = ORC_END_ERR_OPEN; res->err = -10 - b; goto out; }
+    if (b == 1) {
+      s.have_bi = 1;
+      int r = (mode == 0) ? (oseek_to_restart_point(&s.bi, 0), oparse_next_key(&s.bi)) : oseek(&s.bi, key, klen);
+      if (r < 0) { res->end = ORC_END_PANIC; goto out; }
+    }
+  }
+  /* ops: n >= 0 = up to n next() calls (stops at the first None / Err); -1 - j = seek(op key j).
+   * op_res[2i] = records yielded (next) / 0; op_res[2i+1] = 0 Some..., 1 None, 2 Err (res->err),
+   * for seek 0 Ok / 2 Err.  A panic or loop ends the script (res->end). */
+  for (uint64_t i = 0; i < nops; i++) {
+    if (ops[i] >= 0) {
+      for (int64_t n = 0; n < ops[i]; n++) {
+        const uint8_t *k, *v; uint64_t kl, vl;
+        int r = ostate_next(&s, &k, &kl, &v, &vl);
+        if (r == OS_SOME) { oscan_push(&o, k, kl, v, vl); op_res[2 * i]++; continue; }
+        if (r == OS_NONE) { op_res[2 * i + 1] = 1; break; }
+        if (r == PANIC) { res->end = ORC_END_PANIC; goto out; }
+        if (r == OS_LOOP) { res->end = ORC_END_LOOP; goto out; }
+        op_res[2 * i + 1] = 2; res->err = -10 - r; break;
+      }
+    } else {
+      const uint64_t j = (uint64_t)(-1 - ops[i]);
+      const uint64_t a = j ? op_key_end[j - 1] : 0;
+      int r = ostate_seek(&s, op_keys + a, op_key_end[j] - a);
+      if (r == PANIC) { res->end = ORC_END_PANIC; goto out; }
+      if (r <= -10) { op_res[2 * i + 1] = 2; res->err = -10 - r; }
+    }
+  }
+  res->end = ORC_END_NONE;
+out:
+  oiter_free(&s.idx);
+  if (s.have_bi) oiter_free(&s.bi);
+  return 0;
+}
+
 void oracle_scan_free(oracle_scan_result* r) {
   free(r->keys); free(r->vals); free(r->key_end); free(r->val_end);
   memset(r, 0, sizeof(*r));

@@ -135,6 +135,14 @@ typedef struct {
 int32_t oracle_file_scan(const uint8_t* data, uint64_t len, int32_t verify_checksums, int32_t mode,
                          const uint8_t* key, uint64_t klen, const uint8_t* key2, uint64_t klen2,
                          uint64_t max_records, oracle_scan_result* res);
+/* ReaderIntoIter driven by a script (src/reader.rs:219-405 incl. seek :302-335): built like
+ * file_scan's mode, then ops[i] >= 0 = up to ops[i] next() calls, ops[i] = -1 - j = seek(op key j)
+ * (op keys concatenated, op_key_end = END offsets).  op_res[2i] = records the op yielded,
+ * op_res[2i+1] = 0 / 1 None / 2 Err (res->err).  Records of all ops in res, in order. */
+int32_t oracle_iter_script(const uint8_t* data, uint64_t len, int32_t verify, int32_t mode, const uint8_t* key,
+                           uint64_t klen, const uint8_t* key2, uint64_t klen2, const int64_t* ops, uint64_t nops,
+                           const uint8_t* op_keys, const uint64_t* op_key_end, int64_t* op_res,
+                           oracle_scan_result* res);
 void oracle_scan_free(oracle_scan_result* res);
 
 /* zlib / zstd block decompression (src/compression.rs:85-92, :140-145): 0 ok, *out malloc'd */

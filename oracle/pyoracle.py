@@ -288,3 +288,46 @@ def file_scan(data: bytes, mode="iter", key=b"", key2=b"", verify=True, max_reco
     out = dict(end=r.end, err=ERR_NAMES[r.err], records=recs, meta=list(r.meta), version=r.version)
     lib().oracle_scan_free(C.byref(r))
     return out
+
+
+def iter_script(data: bytes, mode="iter", key=b"", key2=b"", ops=(), verify=True):
+    """ReaderIntoIter driven by a script (oracle_iter_script): ops items are ints (up to n next()
+    calls) or ("seek", key).  -> dict(end, err, records, ops=[(yielded, code)], ...) with code
+    0 = ok, 1 = None, 2 = Err."""
+    L = lib()
+    if not hasattr(L.oracle_iter_script, "_set"):
+        L.oracle_iter_script.argtypes = [C.POINTER(C.c_uint8), C.c_uint64, C.c_int32, C.c_int32, C.c_void_p,
+                                         C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_iter_script.restype = C.c_int32
+        L.oracle_iter_script._set = True
+    a = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    kb = (C.c_uint8 * max(1, len(key))).from_buffer_copy(key or b"\0")
+    k2 = (C.c_uint8 * max(1, len(key2))).from_buffer_copy(key2 or b"\0")
+    seeks = [bytes(o[1]) for o in ops if not isinstance(o, int)]
+    code, j = [], 0
+    for o in ops:
+        if isinstance(o, int):
+            code.append(o)
+        else:
+            code.append(-1 - j)
+            j += 1
+    opa = np.array(code or [0], np.int64)
+    blob = b"".join(seeks) or b"\0"
+    okb = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+    oke = np.cumsum([len(x) for x in seeks] or [0]).astype(np.uint64)
+    ores = np.zeros(2 * max(1, len(code)), np.int64)
+    r = _ScanRes()
+    L.oracle_iter_script(_u8(a), len(data), 1 if verify else 0, MODES[mode], kb, len(key), k2, len(key2),
+                         opa.ctypes.data, len(code), okb, oke.ctypes.data, ores.ctypes.data, C.byref(r))
+    recs = []
+    pk = pv = 0
+    for i in range(r.nrec):
+        ke, ve = r.key_end[i], r.val_end[i]
+        recs.append((C.string_at(C.addressof(r.keys.contents) + pk, ke - pk) if ke > pk else b"",
+                     C.string_at(C.addressof(r.vals.contents) + pv, ve - pv) if ve > pv else b""))
+        pk, pv = ke, ve
+    out = dict(end=r.end, err=ERR_NAMES[r.err], records=recs, meta=list(r.meta), version=r.version,
+               ops=[(int(ores[2 * i]), int(ores[2 * i + 1])) for i in range(len(code))])
+    lib().oracle_scan_free(C.byref(r))
+    return out

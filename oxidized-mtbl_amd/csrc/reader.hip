@@ -360,6 +360,340 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
   }
 }
 
+// ------------------------------------------------------------------------------------
+// seek-based iteration (ReaderIntoIter::new_from / seek, src/reader.rs:256-335)
+// ------------------------------------------------------------------------------------
+
+// Reader::block (src/reader.rs:139-175) at a block_at_index offset: framing, checksum and
+// Block::init.  MTBLX_SEEK_OK / _ERR / _PANIC / _UNSUPPORTED.
+__device__ int frame_block(const FileCtx& f, uint64_t off, uint64_t& start, uint64_t& sz) {
+  if (!(off < f.len)) return MTBLX_SEEK_PANIC;
+  uint64_t ll;
+  if (f.version == 0) {
+    if (off + 4 > f.len) return MTBLX_SEEK_PANIC;
+    ll = 4; sz = rd32g(f.file + off);
+  } else {
+    const int k = dec64(f.file + off, f.len - off, sz);
+    if (k < 0) return MTBLX_SEEK_PANIC;
+    ll = (uint64_t)k;
+  }
+  start = off + ll + 4;
+  if (start > f.len || sz > f.len - start) return MTBLX_SEEK_PANIC;
+  if (f.verify && mtblx_crc::wave_crc32c(f.file + start, sz, f.T, f.lane) != rd32g(f.file + off + ll))
+    return MTBLX_SEEK_PANIC;
+  if (sz > kU32) return MTBLX_SEEK_UNSUPPORTED;
+  Blk b;
+  const int bi = block_init(f.file + start, sz, b);
+  return bi == 1 ? MTBLX_SEEK_ERR : bi < 0 ? MTBLX_SEEK_PANIC : MTBLX_SEEK_OK;
+}
+
+__global__ void __launch_bounds__(256) k_index_seek(const uint8_t* file, uint64_t file_len, uint32_t version,
+                                                    int verify, uint64_t idx_off, uint64_t idx_len,
+                                                    const uint8_t* qkeys, const uint64_t* qend, uint32_t nq,
+                                                    mtblx_index_seek* out) {
+  __shared__ uint32_t T[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = mtblx_crc::kTab.byte[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves = gridDim.x * (blockDim.x / 64);
+  const FileCtx f{file, file_len, version, verify, T, lane};
+  for (uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); q < nq; q += waves) {
+    const uint64_t k0 = q ? qend[q - 1] : 0;
+    const uint8_t* t = qkeys + k0;
+    const uint64_t tl = qend[q] - k0;
+    mtblx_index_seek r{};
+    r.block_status = MTBLX_SEEK_OK;
+    Blk ib{};
+    It ii{};
+    do {
+      const int ibi = block_init(file + idx_off, idx_len, ib);
+      if (ibi != 0) { r.status = ibi == 1 ? MTBLX_SEEK_ERR : MTBLX_SEEK_PANIC; break; }
+      if (iter_init(ib, ii) != R_OK) { r.status = MTBLX_SEEK_PANIC; break; }
+      const int s = seek(ib, ii, t, tl);                          // index_iter.seek(key)
+      if (s != R_OK) { r.status = s == R_LOOP ? MTBLX_SEEK_LOOP : MTBLX_SEEK_PANIC; break; }
+      r.entry = ii.current;
+      if (!valid(ib, ii)) break;                                   // get() -> None
+      if (ii.voff + ii.vlen > ib.L) { r.status = MTBLX_SEEK_PANIC; break; }   // get()'s slice
+      r.valid = 1;
+      uint64_t off = 0;
+      if (dec64(ib.d + ii.voff, ii.vlen, off) < 0) { r.status = MTBLX_SEEK_PANIC; break; }
+      r.block_off = off;
+      uint64_t start = 0, sz = 0;
+      r.block_status = frame_block(f, off, start, sz);
+      r.data_off = start;
+      r.data_len = sz;
+    } while (false);
+    if (lane == 0) out[q] = r;
+  }
+}
+
+// BlockIter over one block with the key materialised in LDS (the emitting seek)
+constexpr uint32_t kSeekStage = 65536;   // blocks up to this size are staged in LDS
+constexpr uint32_t kSeekKey = 65536;     // longest key the emitting seek carries
+enum { R_TOOLONG = -3 };
+
+struct SIt {
+  uint64_t current, next, klen, kcap, voff, vlen;
+  bool has_next, has_val;
+};
+
+// Ord of K[0..kl) vs t[0..tl), the wave together
+__device__ int wave_cmp(const uint8_t* K, uint64_t kl, const uint8_t* t, uint64_t tl, int lane) {
+  const uint64_t m = kl < tl ? kl : tl;
+  for (uint64_t c0 = 0; c0 < m; c0 += 64) {
+    const uint64_t c = c0 + (uint64_t)lane;
+    const bool diff = c < m && K[c] != t[c];
+    const uint64_t bal = __ballot(diff);
+    if (bal) {
+      const uint64_t cc = c0 + (uint64_t)__builtin_ctzll(bal);
+      return K[cc] < t[cc] ? -1 : 1;
+    }
+  }
+  return kl < tl ? -1 : (kl > tl ? 1 : 0);
+}
+
+// parse_next_key (src/block.rs:119-143): R_OK / R_END / R_PANIC / R_TOOLONG
+__device__ int s_parse(const Blk& b, SIt& it, uint8_t* K, int lane) {
+  it.current = it.has_next ? it.next : 0;
+  if (it.current >= b.R) { it.current = b.R; return R_END; }
+  uint32_t sh, ns, vl;
+  uint64_t p;
+  if (decode_entry(b, it.current, b.R, sh, ns, vl, p) != R_OK) return R_PANIC;
+  if (!(it.kcap >= sh)) return R_PANIC;                       // Vec capacity assert (:132)
+  const uint64_t m = sh < it.klen ? sh : it.klen;             // truncate (:134)
+  if (p + ns > b.L) return R_PANIC;
+  if (ns > 0 && it.kcap - m < ns) {                           // Vec growth (:135)
+    uint64_t c = it.kcap * 2, req = m + ns;
+    if (req > c) c = req;
+    if (c < 8) c = 8;
+    it.kcap = c;
+  }
+  if (m + ns > kSeekKey) return R_TOOLONG;
+  for (uint32_t j = (uint32_t)lane; j < ns; j += 64) K[m + j] = b.d[p + j];
+  __syncthreads();   // one-wave workgroup: orders the LDS writes before other lanes read K
+  it.klen = m + ns;
+  it.has_next = true;
+  it.next = p + ns + vl;
+  it.voff = p + ns;
+  it.vlen = vl;
+  it.has_val = true;
+  return R_OK;
+}
+
+// BlockIter::seek (src/block.rs:154-194) with the key materialised
+__device__ int s_seek(const Blk& b, SIt& it, uint8_t* K, const uint8_t* t, uint64_t tl, int lane) {
+  uint32_t left = 0, right = b.n - 1;
+  while (left < right) {
+    const uint32_t mid = (uint32_t)(((uint64_t)left + right + 1) / 2);
+    uint32_t sh, ns, vl;
+    uint64_t ko;
+    if (decode_entry(b, restart_point(b, mid), b.R, sh, ns, vl, ko) != R_OK) return R_PANIC;
+    if (sh != 0) return R_OK;                                 // "corruption": early return
+    if (ko + ns > b.L) return R_PANIC;
+    if (wave_cmp(b.d + ko, ns, t, tl, lane) < 0) left = mid;
+    else right = mid - 1;
+  }
+  it.klen = 0;                                                // seek_to_restart_point(left)
+  it.has_next = true;
+  it.next = restart_point(b, left);
+  for (;;) {
+    const int r = s_parse(b, it, K, lane);
+    if (r != R_OK) return r == R_END ? R_OK : r;
+    if (wave_cmp(K, it.klen, t, tl, lane) >= 0) return R_OK;
+    if (it.next == it.current) return R_LOOP;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const uint8_t* qkeys, const uint64_t* qend,
+                                                   uint32_t nq, mtblx_block_seek* qs, uint8_t* okeys,
+                                                   uint64_t keys_cap, uint8_t* ovals, uint64_t vals_cap,
+                                                   uint64_t* oke, uint64_t* ove, uint64_t* okcap, uint64_t rec_cap) {
+  __shared__ uint8_t stage[kSeekStage];
+  __shared__ uint8_t K[kSeekKey];
+  const int lane = threadIdx.x;
+  for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    mtblx_block_seek Q = qs[q];
+    const uint64_t k0 = q ? qend[q - 1] : 0;
+    const uint8_t* t = qkeys + k0;
+    const uint64_t tl = qend[q] - k0;
+    Q.status = MTBLX_SEEK_OK;
+    Q.end = MTBLX_EMIT_END;
+    Q.nrec = Q.key_bytes = Q.val_bytes = 0;
+    Q.entry = 0;
+    const uint64_t L = Q.data_len;
+    const uint8_t* src = data + Q.data_off;
+    const uint8_t* d = src;
+    Blk b{};
+    SIt it{};
+    do {
+      if (L > kU32) { Q.status = MTBLX_SEEK_UNSUPPORTED; break; }
+      __syncthreads();
+      if (L <= kSeekStage) {
+        for (uint64_t i = (uint64_t)lane; i < L; i += 64) stage[i] = src[i];
+        __syncthreads();
+        d = stage;
+      }
+      const int bi = block_init(d, L, b);                          // Block::init
+      if (bi != 0) { Q.status = bi == 1 ? MTBLX_SEEK_ERR : MTBLX_SEEK_PANIC; break; }
+      if (b.n == 0) { Q.status = MTBLX_SEEK_PANIC; break; }        // BlockIter::init assert
+      it.current = b.R;
+      it.has_next = false;
+      it.kcap = Q.kcap;
+      int r;
+      if (Q.first) {                                               // seek_to_first
+        it.klen = 0;
+        it.has_next = true;
+        it.next = restart_point(b, 0);
+        r = s_parse(b, it, K, lane);
+        if (r == R_END) r = R_OK;
+      } else {
+        r = s_seek(b, it, K, t, tl, lane);
+      }
+      if (r != R_OK) {
+        Q.status = r == R_LOOP ? MTBLX_SEEK_LOOP : r == R_TOOLONG ? MTBLX_SEEK_UNSUPPORTED : MTBLX_SEEK_PANIC;
+        break;
+      }
+      Q.entry = it.current;
+      // the records: get(), then next() until get() is None (ReaderIntoIter::next within a block)
+      bool ovf = false;
+      uint8_t* kd = okeys + (uint64_t)q * keys_cap;
+      uint8_t* vd = ovals + (uint64_t)q * vals_cap;
+      for (;;) {
+        if (Q.nrec >= Q.max_records) { Q.end = MTBLX_EMIT_MAX; break; }
+        if (!(it.current < b.R)) break;                            // get() -> None
+        if (it.voff + it.vlen > b.L) { Q.end = MTBLX_EMIT_PANIC; break; }   // get()'s slice
+        const uint64_t kb = Q.key_bytes + it.klen, vb = Q.val_bytes + it.vlen;
+        if (!ovf && (Q.nrec >= rec_cap || kb > keys_cap || vb > vals_cap)) ovf = true;
+        if (!ovf) {
+          for (uint64_t j = (uint64_t)lane; j < it.klen; j += 64) kd[Q.key_bytes + j] = K[j];
+          for (uint64_t j = (uint64_t)lane; j < it.vlen; j += 64) vd[Q.val_bytes + j] = d[it.voff + j];
+          if (lane == 0) {
+            oke[(uint64_t)q * rec_cap + Q.nrec] = kb;
+            ove[(uint64_t)q * rec_cap + Q.nrec] = vb;
+            if (okcap) okcap[(uint64_t)q * rec_cap + Q.nrec] = it.kcap;
+          }
+        }
+        Q.nrec++;
+        Q.key_bytes = kb;
+        Q.val_bytes = vb;
+        if (it.has_next && it.next == it.current) { Q.end = MTBLX_EMIT_LOOP; break; }
+        r = s_parse(b, it, K, lane);                               // BlockIter::next
+        if (r == R_PANIC) { Q.end = MTBLX_EMIT_PANIC; break; }
+        if (r == R_TOOLONG) { Q.status = MTBLX_SEEK_UNSUPPORTED; break; }
+      }
+      if (ovf && Q.status == MTBLX_SEEK_OK) Q.end = MTBLX_EMIT_OVERFLOW;
+    } while (false);
+    Q.kcap = it.kcap;
+    Q.has_val = it.has_val ? 1 : 0;
+    Q.last_voff = it.voff;
+    Q.last_vlen = it.vlen;
+    if (lane == 0) qs[q] = Q;
+  }
+}
+
+// chain of entry offsets from restart 0 (seek_to_first + next), see mtblx_entry_offsets
+__device__ __forceinline__ bool chain_step(const Blk& b, uint64_t cur, uint64_t& nxt) {
+  uint32_t sh, ns, vl;
+  uint64_t p;
+  if (decode_entry(b, cur, b.R, sh, ns, vl, p) != R_OK) return false;
+  if (p + ns > b.L) return false;
+  nxt = p + ns + vl;
+  return true;
+}
+
+__global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint64_t L, uint64_t* offs, uint64_t cap,
+                                                        uint64_t* count, uint64_t* scratch) {
+  __shared__ int irregular;
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t carry;
+  Blk b{};
+  const int tid = threadIdx.x;
+  if (tid == 0) { irregular = 0; carry = 0; }
+  __syncthreads();
+  if (block_init(blk, L, b) != 0 || b.n == 0) {
+    if (tid == 0) *count = 0;
+    return;
+  }
+  const uint32_t n = b.n;
+  // pass 1: count each restart interval's chain; it must land exactly on the next restart point
+  for (uint32_t r = tid; r < n; r += blockDim.x) {
+    const uint64_t s0 = restart_point(b, r), e0 = (r + 1 < n) ? restart_point(b, r + 1) : b.R;
+    uint64_t c = 0, cur = s0;
+    bool ok = s0 < e0 || (r + 1 == n && s0 == b.R);
+    while (ok && cur < e0) {
+      uint64_t nx;
+      if (!chain_step(b, cur, nx)) { ok = false; break; }
+      cur = nx;
+      ++c;
+    }
+    if (!ok || cur != e0) irregular = 1;
+    scratch[r] = c;
+  }
+  __syncthreads();
+  if (!irregular) {
+    // exclusive scan of scratch[0..n) in chunks of blockDim.x
+    for (uint32_t base = 0; base < n; base += blockDim.x) {
+      const uint32_t r = base + tid;
+      const uint64_t v = r < n ? scratch[r] : 0;
+      uint64_t x = v;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if ((tid & 63) >= o) x += y;
+      }
+      if ((tid & 63) == 63) wsum[tid >> 6] = x;
+      __syncthreads();
+      uint64_t wp = 0;
+      for (int w = 0; w < (tid >> 6); ++w) wp += wsum[w];
+      const uint64_t c0 = carry;
+      __syncthreads();
+      if (r < n) scratch[r] = c0 + wp + x - v;
+      if (tid == (int)blockDim.x - 1) carry = c0 + wp + x;
+      __syncthreads();
+    }
+    for (uint32_t r = tid; r < n; r += blockDim.x) {
+      const uint64_t e0 = (r + 1 < n) ? restart_point(b, r + 1) : b.R;
+      uint64_t i = scratch[r], cur = restart_point(b, r);
+      while (cur < e0) {
+        if (i < cap) offs[i] = cur;
+        uint64_t nx;
+        chain_step(b, cur, nx);
+        cur = nx;
+        ++i;
+      }
+    }
+    if (tid == 0) *count = carry;
+    return;
+  }
+  // irregular block (corruption): the scan's own walk, serial
+  if (tid != 0) return;
+  uint64_t i = 0, cur = restart_point(b, 0);
+  while (cur < b.R) {
+    if (i < cap) offs[i] = cur;
+    ++i;
+    uint64_t nx;
+    if (!chain_step(b, cur, nx) || nx <= cur) break;
+    cur = nx;
+  }
+  *count = i;
+}
+
+__global__ void k_key_filter(const uint8_t* keys, const uint64_t* key_end, uint64_t n, int32_t type, const uint8_t* k,
+                             uint64_t kl, unsigned long long* first_fail) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t a = i ? key_end[i - 1] : 0, l = key_end[i] - a;
+  const uint8_t* key = keys + a;
+  const uint64_t m = l < kl ? l : kl;
+  uint64_t c = 0;
+  while (c < m && key[c] == k[c]) ++c;
+  const int cmp = (c < m) ? (key[c] < k[c] ? -1 : 1) : (l < kl ? -1 : (l > kl ? 1 : 0));
+  bool fail = false;
+  if (type == 1) fail = cmp != 0;
+  else if (type == 2) fail = !(kl <= l && c == kl);
+  else if (type == 3) fail = cmp > 0;
+  if (fail) atomicMin(first_fail, (unsigned long long)i);
+}
+
 }  // namespace mtblx_rd
 
 extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, const uint8_t* vals,
@@ -390,5 +724,54 @@ extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t versio
   hipLaunchKernelGGL(mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len, keys,
                      key_end, nq, status, val_off, val_len);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_index_seek_batch(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
+                                      uint64_t index_off, uint64_t index_len, const uint8_t* keys,
+                                      const uint64_t* key_end, uint32_t nq, mtblx_index_seek* out, void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!file || !keys || !key_end || !out || version > 1) return MTBLX_E_INVAL;
+  const uint32_t need = (nq + 3u) / 4u;
+  hipLaunchKernelGGL(mtblx_rd::k_index_seek, dim3(need < 2048u ? need : 2048u), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
+                     keys, key_end, nq, out);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end, uint32_t nq,
+                                      mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
+                                      uint64_t vals_cap, uint64_t* key_end_out, uint64_t* val_end_out,
+                                      uint64_t* kcap_out, uint64_t rec_cap, void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out) return MTBLX_E_INVAL;
+  hipLaunchKernelGGL(mtblx_rd::k_block_seek, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
+                     vals_cap, key_end_out, val_end_out, kcap_out, rec_cap);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t* offs, uint64_t cap, uint64_t* count,
+                                   void* stream) {
+  if (!block || !count || (cap && !offs)) return MTBLX_E_INVAL;
+  if (len > mtblx_rd::kU32) return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t nr = len / 4 + 1;   // restart count bound: 4 bytes per restart point
+  uint64_t* scratch = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&scratch), nr * sizeof(uint64_t), s) != hipSuccess) return MTBLX_E_HIP;
+  hipLaunchKernelGGL(mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch);
+  const bool ok = hipGetLastError() == hipSuccess;
+  (void)hipFreeAsync(scratch, s);
+  return ok ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_key_filter(const uint8_t* keys, const uint64_t* key_end, uint64_t n, int32_t type,
+                                const uint8_t* k, uint64_t klen, uint64_t* first_fail, void* stream) {
+  if (n == 0) return MTBLX_OK;
+  if (!keys || !key_end || !first_fail || (klen && !k) || type < 1 || type > 3) return MTBLX_E_INVAL;
+  const uint64_t blocks = (n + 255) / 256;
+  if (blocks > 0x7FFFFFFFull) return MTBLX_E_INVAL;
+  hipLaunchKernelGGL(mtblx_rd::k_key_filter, dim3((uint32_t)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     keys, key_end, n, type, k, klen, reinterpret_cast<unsigned long long*>(first_fail));
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

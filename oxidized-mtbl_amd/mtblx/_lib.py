@@ -23,6 +23,8 @@ SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL = range(3)
 CODEC_OK, CODEC_CORRUPT, CODEC_UNSUPPORTED = range(3)
 DIR_OK, DIR_PANIC, DIR_UNSUPPORTED = range(3)
 GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP = range(5)
+SEEK_OK, SEEK_ERR, SEEK_PANIC, SEEK_LOOP, SEEK_UNSUPPORTED = range(5)
+EMIT_END, EMIT_PANIC, EMIT_LOOP, EMIT_MAX, EMIT_OVERFLOW = range(5)
 
 # every symbol the public headers declare (checked by tests/test_abi.py)
 EXPORTS = [
@@ -36,6 +38,7 @@ EXPORTS = [
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
     "mtblx_codec_available", "mtblx_decompress", "mtblx_compress", "mtblx_decompress_blocks", "mtblx_writer_set_level",
+    "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_entry_offsets", "mtblx_key_filter",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
@@ -61,6 +64,18 @@ class PipeStats(C.Structure):
     _fields_ = [("seconds", C.c_double), ("stage_seconds", C.c_double), ("decode_ms", C.c_double),
                 ("block_bytes", C.c_uint64), ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64),
                 ("chunks", C.c_uint32), ("decompress_errors", C.c_uint32)]
+
+
+class IndexSeek(C.Structure):   # mtblx_index_seek
+    _fields_ = [("status", C.c_int32), ("valid", C.c_int32), ("entry", C.c_uint64), ("block_off", C.c_uint64),
+                ("block_status", C.c_int32), ("pad", C.c_int32), ("data_off", C.c_uint64), ("data_len", C.c_uint64)]
+
+
+class BlockSeek(C.Structure):   # mtblx_block_seek
+    _fields_ = [("data_off", C.c_uint64), ("data_len", C.c_uint64), ("kcap", C.c_uint64), ("max_records", C.c_uint64),
+                ("first", C.c_int32), ("status", C.c_int32), ("end", C.c_int32), ("has_val", C.c_int32),
+                ("entry", C.c_uint64), ("nrec", C.c_uint64), ("key_bytes", C.c_uint64), ("val_bytes", C.c_uint64),
+                ("last_voff", C.c_uint64), ("last_vlen", C.c_uint64)]
 
 
 class Footer(C.Structure):
@@ -179,6 +194,18 @@ def lib() -> C.CDLL:
         L.mtblx_writer_set_level.restype = C.c_int
         L.mtblx_stream_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
         L.mtblx_stream_copy.restype = C.c_int
+        L.mtblx_index_seek_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint64,
+                                             C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        L.mtblx_index_seek_batch.restype = C.c_int
+        L.mtblx_block_seek_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                             C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_uint64, C.c_void_p]
+        L.mtblx_block_seek_batch.restype = C.c_int
+        L.mtblx_entry_offsets.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.mtblx_entry_offsets.restype = C.c_int
+        L.mtblx_key_filter.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64,
+                                       C.c_void_p, C.c_void_p]
+        L.mtblx_key_filter.restype = C.c_int
         L.mtblx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_uint64]
         L.mtblx_host_alloc.restype = C.c_int
         L.mtblx_host_free.argtypes = [C.c_void_p]

@@ -17,9 +17,10 @@ prefix of the device output arrays, plus how the iteration ends (`end`: NONE / E
 ERR_NEXT / PANIC / LOOP, the oracle's codes).  Errors the reference returns from
 ReaderBuilder::read raise `MtblError` here.
 
-get / get_prefix / get_range / iter_from are answered from the decoded records with a binary
-search over the (sorted) keys -- identical to the reference's index + block seek on well-formed
-files; malformed files are only defined for iter() in this round (documented in DESIGN.md).
+Seek-based iteration -- iter_from / iter_prefix / iter_range (src/reader.rs:128-138) and the
+stateful ReaderIntoIter with next() / seek() (:219-405) -- goes through the device index seek,
+block_at_index and block seek, decoding only the blocks the iteration reaches (iterator.py).
+get() is the device Reader::get (mtblx_get).
 """
 from __future__ import annotations
 
@@ -47,6 +48,10 @@ class MtblError(RuntimeError):
 
 class ReferencePanic(RuntimeError):
     """Where the reference panics (assert / unwrap / slice out of range)."""
+
+
+class ReferenceLoop(RuntimeError):
+    """Where the reference never returns (an entry that does not advance)."""
 
 
 @dataclass
@@ -140,13 +145,32 @@ class Reader:
         self.index_status = ist
         self.nent = int(self.index.totals_host()[0])
         self._dir = None
+        self._dir3 = None
         self._scan = None
+        self._eoffs = None
+        self._ikeys = None
 
     # ------------------------------------------------------------------ directory
     def directory(self):
         """(blk_off int64, blk_len int32, dir_status int32, crc_bad uint8|None) on the device,
         one entry per index record."""
         if self._dir is None:
+            off, ln, st = self._framing()
+            self._dir = (off, ln, st, self._bad_range(0, self.nent))
+        return self._dir
+
+    def _bad_range(self, i0: int, i1: int):
+        """Reader::block's checksum assert for directory entries [i0, i1) (device uint8), or
+        None when not verifying"""
+        if not self.verify or i1 <= i0:
+            return None
+        off, ln, _ = self._framing()
+        batch = codec.DeviceBatch(self.file, off[i0:i1], ln[i0:i1], int(ln[i0:i1].max().item()))
+        return codec.crc32c_blocks(batch, framed=True)[1]
+
+    def _framing(self):
+        """block_at_index + Reader::block framing of every index entry: (off, len, status)"""
+        if self._dir3 is None:
             n = max(self.nent, 1)
             dev = self.file.device
             off = torch.zeros(n, dtype=torch.int64, device=dev)
@@ -160,14 +184,8 @@ class Reader:
                                        C.c_void_p(st.data_ptr()), C.c_void_p(codec._stream_handle(None)))
                 if rc != 0:
                     raise RuntimeError(f"mtblx_block_dir failed: {rc}")
-            off, ln, st = off[: self.nent], ln[: self.nent], st[: self.nent]
-            bad = None
-            if self.verify and self.nent:
-                ml = int(ln.max().item())
-                batch = codec.DeviceBatch(self.file, off, ln, ml)
-                _, bad = codec.crc32c_blocks(batch, framed=True)
-            self._dir = (off, ln, st, bad)
-        return self._dir
+            self._dir3 = (off[: self.nent], ln[: self.nent], st[: self.nent])
+        return self._dir3
 
     # ------------------------------------------------------------------ iteration
     def _decode_all(self):
@@ -269,12 +287,14 @@ class Reader:
         return self._scan
 
     def _cut(self, nblk_full: int, take_last: int, end: int, err: str) -> Scan:
+        return self._cut_data(self.data, nblk_full, take_last, end, err)
+
+    def _cut_data(self, d, nblk_full: int, take_last: int, end: int, err: str) -> Scan:
         dev = self.file.device
-        if self.data is None or (nblk_full == 0 and take_last == 0):
+        if d is None or (nblk_full == 0 and take_last == 0):
             z = torch.zeros(0, dtype=torch.uint8, device=dev)
             e = torch.zeros(0, dtype=torch.int64, device=dev)
             return Scan(end, err, 0, z, z, e, e)
-        d = self.data
         nr = d.nrec[: d.nblk].to(torch.int64)
         # records of the first nblk_full blocks + take_last records of the next block
         nrec = int(nr[:nblk_full].sum().item()) + take_last
@@ -322,11 +342,20 @@ class Reader:
     def get(self, key: bytes):
         """Reader::get (src/reader.rs:111-122): the value of `key`, or None; raises where the
         reference panics / returns Err."""
-        if self.compression != 0:   # values live in decompressed blocks: search the decoded records
-            recs = self._sorted_keys()[1]
-            import bisect
-            i = bisect.bisect_left([k for k, _ in recs], bytes(key))
-            return recs[i][1] if i < len(recs) and recs[i][0] == bytes(key) else None
+        if self.compression != 0:   # values live in decompressed blocks: the seek-based iterator
+            from . import iterator
+            it = iterator.ReaderIntoIter(self, "get", bytes(key))
+            held = it.bi
+            try:
+                rec = it.next()
+            except MtblError:
+                # next() returned Some(Err): Reader::get matches Some(_) and returns the OLD
+                # block iterator's `val` (src/reader.rs:111-122, :376-379), or None
+                return held.last_val if held is not None else None
+            if rec is None:
+                return None
+            # Some((k, v)) with k != key is still Some(_): ReaderIntoGet over bi's val
+            return rec[1] if rec[0] == bytes(key) else it.bi.recs[it.bi.pos][1]
         st, vo, vl = self.get_batch([key])
         s = int(st[0].item())
         if s == _lib.GET_FOUND:
@@ -343,27 +372,154 @@ class Reader:
         return s, s.records()
 
     def get_prefix(self, prefix: bytes):
-        s, recs = self._sorted_keys()
-        import bisect
-        p = bytes(prefix)
-        i = bisect.bisect_left([k for k, _ in recs], p)
-        out = []
-        while i < len(recs) and recs[i][0].startswith(p):
-            out.append(recs[i])
-            i += 1
-        return out
+        """iter_prefix's records on the host"""
+        return self.iter_prefix(prefix).records()
 
     def get_range(self, start: bytes, end: bytes):
-        s, recs = self._sorted_keys()
-        import bisect
-        i = bisect.bisect_left([k for k, _ in recs], bytes(start))
-        out = []
-        while i < len(recs) and recs[i][0] <= bytes(end):
-            out.append(recs[i])
-            i += 1
-        return out
+        """iter_range's records on the host"""
+        return self.iter_range(start, end).records()
 
-    def iter_from(self, key: bytes):
-        s, recs = self._sorted_keys()
-        import bisect
-        return recs[bisect.bisect_left([k for k, _ in recs], bytes(key)):]
+    # ------------------------------------------------------------------ seek-based iteration
+    def iter_from(self, key: bytes) -> Scan:
+        """Reader::iter_from (src/reader.rs:128-130) run to the end, touching only the blocks
+        from the sought one on."""
+        from . import iterator
+        return iterator.bulk(self, "from", bytes(key))
+
+    def iter_prefix(self, prefix: bytes) -> Scan:
+        """Reader::iter_prefix (src/reader.rs:132-134)"""
+        from . import iterator
+        return iterator.bulk(self, "prefix", bytes(prefix))
+
+    def iter_range(self, start: bytes, end: bytes) -> Scan:
+        """Reader::iter_range (src/reader.rs:136-138): start <= key <= end"""
+        from . import iterator
+        return iterator.bulk(self, "range", bytes(start), bytes(end))
+
+    def into_iter(self, kind: str = "iter", key: bytes = b"", key2: bytes = b""):
+        """the stateful ReaderIntoIter (next() / seek()), see iterator.ReaderIntoIter"""
+        from . import iterator
+        return iterator.ReaderIntoIter(self, kind, key, key2)
+
+    def _index_keys(self):
+        if self._ikeys is None:
+            self._ikeys = [k for k, _ in self.index.to_host().records(0)] if self.nent else []
+        return self._ikeys
+
+    def _ordinal(self, entry: int) -> int:
+        """index position of the entry an index seek landed on (mtblx_entry_offsets)"""
+        if self._eoffs is None:
+            dev = self.file.device
+            offs = torch.zeros(max(self.nent, 1), dtype=torch.int64, device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            rc = _lib.lib().mtblx_entry_offsets(C.c_void_p(self.file.data_ptr() + self.index_off), self.index_len,
+                                                C.c_void_p(offs.data_ptr()), self.nent, C.c_void_p(cnt.data_ptr()),
+                                                C.c_void_p(codec._stream_handle(None)))
+            if rc != 0:
+                raise RuntimeError(f"mtblx_entry_offsets failed: {rc}")
+            n = min(int(cnt.item()), self.nent)
+            self._eoffs = offs[:n].cpu().numpy()
+        i = int(np.searchsorted(self._eoffs, entry))
+        if i < self._eoffs.size and int(self._eoffs[i]) == entry:
+            return i
+        raise NotImplementedError("index seek landed off the index block's scan chain (corrupt index)")
+
+    def _seek_content(self, s):
+        """Reader::block of an index seek's landed entry -> (tensor, off, len) of the content
+        BlockIter reads (host-decompressed for compressed files); raises Err / panic."""
+        if s.block_status == _lib.SEEK_PANIC:
+            raise ReferencePanic("Reader::block")
+        if self.compression == 0:
+            if s.block_status == _lib.SEEK_ERR:
+                raise MtblError(6)
+            if s.block_status == _lib.SEEK_UNSUPPORTED:
+                raise NotImplementedError("block >= 4 GiB")
+            return self.file, int(s.data_off), int(s.data_len)
+        # compressed: Block::init runs on the decompressed content (mtblx_block_seek_batch);
+        # block_status's ERR / UNSUPPORTED judged the compressed bytes and do not apply
+        raw = self.file[int(s.data_off): int(s.data_off) + int(s.data_len)].cpu().numpy()
+        L = _lib.lib()
+        out = _lib.u8p()
+        n = C.c_uint64(0)
+        src = raw if raw.size else np.zeros(1, np.uint8)
+        if L.mtblx_decompress(self.compression, src.ctypes.data, raw.size, C.byref(out), C.byref(n)) != 0:
+            raise MtblError(7)
+        b = C.string_at(out, n.value)
+        L.mtblx_free(out)
+        t = torch.frombuffer(bytearray(b or b"\0"), dtype=torch.uint8).to(self.file.device)
+        return t, 0, len(b)
+
+    def _decode_range(self, i0: int, i1: int):
+        """decode directory entries [i0, i1) -> (dir status, crc bad, decompress errors, decoded,
+        (base tensor, content offsets, content lengths)) with host arrays"""
+        off, ln, st = self._framing()
+        n = i1 - i0
+        dst = st[i0:i1].cpu().numpy()
+        bad = self._bad_range(i0, i1)
+        bad = bad.cpu().numpy() if bad is not None else np.zeros(n, np.uint8)
+        if self.compression != 0:
+            buf, uoff, uln, zerr = self._host_stage(off[i0:i1], ln[i0:i1], st[i0:i1])
+            batch = codec.DeviceBatch.from_host(buf, uoff, uln, device=self.file.device)
+            where = (batch.data, uoff.astype(np.int64), uln.astype(np.int64))
+        else:
+            zerr = np.zeros(n, np.int32)
+            batch = codec.DeviceBatch(self.file, off[i0:i1], ln[i0:i1], int(ln[i0:i1].max().item()))
+            where = (self.file, off[i0:i1].cpu().numpy(), ln[i0:i1].cpu().numpy().view(np.uint32).astype(np.int64))
+        data = codec.decode_blocks(batch)
+        return dst, bad, zerr, data, where
+
+    def _walk_range(self, i0: int, i1: int):
+        """ReaderIntoIter::next over directory entries [i0, i1), each block loaded by next()
+        (an empty block ends the iteration, src/reader.rs:362-371) -> ((keys, vals, key_end,
+        val_end, nrec) on the device, end, err, stopped)"""
+        dst, bad, zerr, data, _ = self._decode_range(i0, i1)
+        n = i1 - i0
+        bst = data.status[:n].cpu().numpy()
+        bnr = data.nrec[:n].cpu().numpy().astype(np.int64)
+        end, err, full, last, stopped = END_NONE, "None", n, 0, False
+        for i in range(n):
+            if dst[i] != _lib.DIR_OK or bad[i]:
+                end, full, stopped = END_PANIC, i, True
+                break
+            if zerr[i]:
+                end, err, full, stopped = END_ERR_NEXT, "Io", i, True
+                break
+            s = int(bst[i])
+            if s == _lib.ST_INVALID_BLOCK:
+                end, err, full, stopped = END_ERR_NEXT, "InvalidBlock", i, True
+                break
+            if s == _lib.ST_UNSUPPORTED:
+                raise NotImplementedError("block >= 4 GiB")
+            if s == _lib.ST_OK and bnr[i] == 0:
+                full, stopped = i, True
+                break
+            if s in (_lib.ST_CORRUPT, _lib.ST_LOOP):
+                end = END_PANIC if s == _lib.ST_CORRUPT else END_LOOP
+                full, last, stopped = i, int(bnr[i]), True
+                break
+        sc = self._cut_data(data, full, last, end, err)
+        return (sc.keys, sc.vals, sc.key_end, sc.val_end, sc.nrec), end, err, stopped
+
+    def _host_blocks(self, i0: int, i1: int):
+        """blocks [i0, i1) as next() loads them, for the stateful iterator: per block an
+        exception to raise (Err / panic) or ((tensor, off, len), records, emit end)"""
+        dst, bad, zerr, data, (base, boff, blen) = self._decode_range(i0, i1)
+        h = data.to_host()
+        out = []
+        for i in range(i1 - i0):
+            content = (base, int(boff[i]), int(blen[i]))
+            if dst[i] != _lib.DIR_OK or bad[i]:
+                out.append(ReferencePanic("Reader::block"))
+                continue
+            if zerr[i]:
+                out.append(MtblError(7))
+                continue
+            s = int(h.status[i])
+            if s == _lib.ST_INVALID_BLOCK:
+                out.append(MtblError(6))
+            elif s == _lib.ST_UNSUPPORTED:
+                out.append(NotImplementedError("block >= 4 GiB"))
+            else:
+                end = {_lib.ST_CORRUPT: _lib.EMIT_PANIC, _lib.ST_LOOP: _lib.EMIT_LOOP}.get(s, _lib.EMIT_END)
+                out.append((content, h.records(i), end))
+        return out

@@ -180,3 +180,28 @@ def test_product_block_dir(oracle):
     assert (dec.status == 0).all() and int(dec.nrec.sum()) <= len(r["records"])
     flat = [rec for b in range(off.size) for rec in dec.records(b)]
     assert flat == r["records"][: len(flat)]
+
+
+def test_iter_script_matches_file_scan_and_pins_seek_quirk(oracle):
+    """oracle_iter_script (ReaderIntoIter with seek, src/reader.rs:219-405) agrees with
+    oracle_file_scan for plain runs, and restates ReaderIntoIter::seek's block_offset quirk:
+    block_offset starts at 0 and next() never updates it (:244-246, :269-271, :362-366), so
+    seeking to a key of block 0 (offset 0) re-seeks the block the iterator currently holds."""
+    recs = [(b"k%05d" % i, b"v%d" % i) for i in range(3000)]
+    f = oracle.write_file(recs, 512, 4)
+    for mode, k, k2 in [("iter", b"", b""), ("from", b"k00100", b""), ("prefix", b"k001", b""),
+                        ("range", b"k00500", b"k00700"), ("get", b"k00300", b"")]:
+        a = oracle.file_scan(f, mode, k, k2)
+        b = oracle.iter_script(f, mode, k, k2, [10 ** 9])
+        assert a["records"] == b["records"] and a["end"] == b["end"]
+    r = oracle.iter_script(f, "from", b"k01000", b"", [3, ("seek", b"k00002"), 2, ("seek", b"k02999"), 5,
+                                                       ("seek", b"zzz"), 3])
+    got = [k for k, _ in r["records"]]
+    # k00002 lives in block 0: no reload, the held block (first key k00978) is re-seeked
+    assert got[:3] == [b"k01000", b"k01001", b"k01002"]
+    assert got[3:5] == [b"k00978", b"k00979"]
+    assert got[5:] == [b"k02999"]
+    assert r["ops"] == [(3, 0), (0, 0), (2, 0), (0, 0), (1, 1), (0, 0), (0, 1)]
+    # a seek whose block offset differs reloads: from an iterator built by into_iter
+    r2 = oracle.iter_script(f, "iter", b"", b"", [2, ("seek", b"k02000"), 2])
+    assert [k for k, _ in r2["records"]] == [b"k00000", b"k00001", b"k02000", b"k02001"]

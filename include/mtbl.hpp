@@ -9,10 +9,9 @@
 //                                                                        index, directory, CRC,
 //                                                                        block decode: device)
 //   Reader::get                 src/reader.rs:111-122                   (mtblx_get, batched seek)
-//   ReaderIntoIter::next        src/reader.rs:337-405                   (records decoded on the
-//                                                                        device, served on host)
-//   Reader::iter_prefix / iter_range / iter_from                         (binary search over the
-//                                                                        decoded, sorted keys)
+//   ReaderIntoIter::next / seek src/reader.rs:219-405                   (device seek + decode of the
+//   Reader::into_iter / iter_prefix / iter_range / iter_from             blocks the iteration reaches,
+//                                                                        records served on the host)
 //   Metadata                    src/metadata.rs:11-24
 //   MtblError                   src/error.rs:44-52
 //
@@ -27,6 +26,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -120,6 +120,12 @@ inline std::vector<T> download(const void* src, size_t count) {
   std::vector<T> v(count);
   if (count) hip_check(hipMemcpy(v.data(), src, count * sizeof(T), hipMemcpyDeviceToHost), "D2H");
   return v;
+}
+
+// a key (possibly empty: one readable zero byte) on the device
+inline DevBuf upload_key(const Bytes& k) {
+  static const uint8_t zero = 0;
+  return k.empty() ? upload(&zero, 1) : upload(k.data(), k.size());
 }
 
 // decoded blocks, downloaded to the host (the layout of mtblx_decoded)
@@ -244,17 +250,73 @@ struct Record {   // a (key, value) pair served by the iterators (views into the
 
 class Reader;
 
-// ReaderIntoIter (src/reader.rs:219-405) in its Iter mode; next() throws where the reference
-// returns Err / panics, after yielding the records it yields before that.
+// ReaderIntoIter (src/reader.rs:219-405): built by Reader::into_iter (new), iter_from
+// (new_from), iter_prefix (new_get_prefix), iter_range (new_get_range); next() and the
+// mid-iteration seek() (:302-335).  The device seeks and decodes (mtblx_index_seek_batch,
+// mtblx_block_seek_batch, mtblx_entry_offsets, mtblx_decode_blocks over the blocks the
+// iteration reaches, in growing chunks); the host keeps the reference's state: first, valid,
+// the index position and block_offset (0 from the constructors, never updated by next(), so a
+// seek landing on a block at that offset re-seeks the block the iterator holds, with that
+// iterator's key capacity).  next() returns a view valid until the next next()/seek(); it
+// throws Error where the reference returns Some(Err) (the iterator is then exhausted), Panic
+// where it panics or never returns.  Approximation: the index seek runs on a fresh index
+// iterator (differs from the reference only when the index block's restart entries are
+// corrupt, which the index checksum catches unless verification is off).
 class ReaderIntoIter {
  public:
   std::optional<Record> next();
+  bool seek(const Bytes& key);   // Ok(true), or throws
+  bool seek(const std::string& k) { return seek(Bytes(k.begin(), k.end())); }
+  // drain into owned (key, value) pairs
+  std::vector<std::pair<Bytes, Bytes>> collect() {
+    std::vector<std::pair<Bytes, Bytes>> out;
+    while (auto r = next()) out.emplace_back(r->key_bytes(), r->val_bytes());
+    return out;
+  }
 
  private:
   friend class Reader;
-  ReaderIntoIter(const Reader* r, size_t i, size_t end) : r_(r), i_(i), end_(end) {}
+  enum Kind { kIter = 0, kGet = 1, kPrefix = 2, kRange = 3 };
+  struct Content {   // a block's content on the device (decompressed copy for compressed files)
+    std::shared_ptr<detail::DevBuf> own;
+    const uint8_t* base = nullptr;
+    uint64_t off = 0, len = 0;
+  };
+  struct Bi {        // one BlockIter: the records it yields from its position on (host copies)
+    Content c;
+    Bytes keys, vals;
+    std::vector<uint64_t> ke, ve;   // END offsets
+    int end = MTBLX_EMIT_END;       // after the last record
+    std::vector<uint64_t> kcaps;    // key capacity at each record (empty + !kcaps_known: replay)
+    bool kcaps_known = false;
+    uint64_t kcap_end = 0;
+    size_t pos = 0;
+    std::optional<Bytes> last_val;  // val of the last entry a seek parsed
+    size_t n() const { return ke.size(); }
+    Record rec(size_t i) const {
+      const uint64_t k0 = i ? ke[i - 1] : 0, v0 = i ? ve[i - 1] : 0;
+      return Record{keys.data() + k0, (size_t)(ke[i] - k0), vals.data() + v0, (size_t)(ve[i] - v0)};
+    }
+  };
+  struct Loaded {    // a block as next() loads it: an outcome code or the Bi
+    int code = 0;    // 0 ok, 1 panic (framing / checksum), 2 Err(Io), 3 Err(InvalidBlock), 4 >= 4 GiB
+    Bi bi;
+  };
+  ReaderIntoIter(const Reader* r, Kind t, Bytes k) : r_(r), type_(t), k_(std::move(k)) {}
+  void init_iter();
+  void init_from(const Bytes& key);
+  Bi load(size_t i);
+  Bi seek_block(const Content& c, const Bytes& key, uint64_t kcap);
+  uint64_t kcap_now(Bi& b);
   const Reader* r_;
-  size_t i_, end_;
+  Kind type_;
+  Bytes k_;
+  uint64_t block_offset_ = 0;
+  bool first_ = true, valid_ = true;
+  std::optional<Bi> bi_;
+  int64_t e_ = -1;                  // index position, -1: the index iterator is invalid
+  size_t chunk0_ = 0, grow_ = 1;
+  std::vector<Loaded> chunk_;
 };
 
 class Reader {
@@ -263,39 +325,53 @@ class Reader {
   static Reader open(const Bytes& data);
   static Reader open(const uint8_t* data, size_t len);
   Metadata metadata() const { return meta_; }
-  ReaderIntoIter into_iter() const { return ReaderIntoIter(this, 0, nrec_); }
+  // Reader::into_iter (src/reader.rs:124-126)
+  ReaderIntoIter into_iter() const {
+    ReaderIntoIter it(this, ReaderIntoIter::kIter, {});
+    it.init_iter();
+    return it;
+  }
   // src/reader.rs:111-122, on the device (mtblx_get: index seek -> block_at_index -> BlockIter::seek)
   std::optional<Bytes> get(const uint8_t* key, size_t klen) const;
   std::optional<Bytes> get(const std::string& k) const {
     return get(reinterpret_cast<const uint8_t*>(k.data()), k.size());
   }
-  // ReaderIntoIter's GetPrefix / GetRange / From filters (src/reader.rs:385-402)
-  std::vector<Record> iter_prefix(const Bytes& prefix) const;
-  std::vector<Record> iter_range(const Bytes& start, const Bytes& end) const;   // end inclusive
-  std::vector<Record> iter_from(const Bytes& key) const;
-  size_t len() const { return nrec_; }   // records the full iteration yields before it ends
+  // src/reader.rs:128-138: seek-based, touching only the blocks the iteration reaches
+  ReaderIntoIter iter_from(const Bytes& key) const { return make(ReaderIntoIter::kIter, key, key); }
+  ReaderIntoIter iter_prefix(const Bytes& prefix) const { return make(ReaderIntoIter::kPrefix, prefix, prefix); }
+  ReaderIntoIter iter_range(const Bytes& start, const Bytes& end) const {   // end inclusive
+    return make(ReaderIntoIter::kRange, start, end);
+  }
+  size_t len() const;   // records the full iteration yields before it ends (decodes the file once)
 
  private:
   friend class ReaderBuilder;
   friend class ReaderIntoIter;
   Reader(const uint8_t* data, size_t len, bool verify);
-  Record rec(size_t i) const {
-    const uint64_t k0 = i ? gke_[i - 1] : 0, v0 = i ? gve_[i - 1] : 0;
-    return Record{dec_.keys.data() + k0, (size_t)(gke_[i] - k0), dec_.vals.data() + v0, (size_t)(gve_[i] - v0)};
+  ReaderIntoIter make(ReaderIntoIter::Kind t, const Bytes& seek_key, const Bytes& k) const {
+    ReaderIntoIter it(this, t, k);
+    it.init_from(seek_key);
+    return it;
   }
-  size_t lower_bound(const uint8_t* k, size_t kl) const;
-  enum class End { None, ErrOpen, ErrNext, Panic, Loop };
+  mtblx_index_seek index_seek(const Bytes& key) const;
+  size_t ordinal(uint64_t entry) const;
+  ReaderIntoIter::Content seek_content(const mtblx_index_seek& s) const;
+  std::vector<ReaderIntoIter::Loaded> load_range(size_t i0, size_t i1) const;
   Bytes file_;
   detail::DevBuf dfile_;
   bool verify_;
   uint32_t version_ = 1;
   Metadata meta_{};
   uint64_t index_off_ = 0, index_len_ = 0;
-  detail::Decoded dec_;
-  std::vector<uint64_t> gke_, gve_;   // global END offsets of the yielded records
-  size_t nrec_ = 0;
-  End end_ = End::None;
-  MtblError err_ = MtblError::InvalidBlock;
+  uint32_t nent_ = 0;
+  int32_t index_status_ = MTBLX_ST_OK;
+  std::vector<uint64_t> boff_;
+  std::vector<uint32_t> blen_;
+  std::vector<int32_t> dst_;
+  detail::DevBuf d_off_, d_len_;
+  mutable std::vector<uint64_t> eoffs_;
+  mutable bool eoffs_known_ = false;
+  mutable std::optional<size_t> len_;
 };
 
 class ReaderBuilder {   // src/reader.rs:15-30
@@ -334,132 +410,346 @@ inline Reader::Reader(const uint8_t* data, size_t len, bool verify) : file_(data
   const Decoded idx = decode_batch(dfile_.as<uint8_t>(), file_.size(), d_ioff.as<uint64_t>(), d_ilen.as<uint32_t>(),
                                    1, ilen);
   if (idx.status[0] == MTBLX_ST_INVALID_BLOCK) throw Error(MtblError::InvalidBlock);   // src/reader.rs:76
-  const uint32_t nent = idx.nrec[0];
-  // block_at_index + Reader::block framing for every index entry (device), then the checksums
-  std::vector<uint64_t> boff(nent);
-  std::vector<uint32_t> blen(nent);
-  std::vector<int32_t> dst(nent);
-  std::vector<uint8_t> bad(nent, 0);
-  DevBuf d_off(8ull * nent), d_len(4ull * nent);
-  if (nent) {
-    DevBuf d_vals = upload(idx.vals.data(), idx.vals.size()), d_vend = upload(idx.val_end.data(), nent);
-    DevBuf d_dst(4ull * nent);
+  nent_ = idx.nrec[0];
+  index_status_ = idx.status[0];
+  // block_at_index + Reader::block framing for every index entry (device); checksums are
+  // checked per block when the iteration loads it
+  boff_.assign(nent_, 0);
+  blen_.assign(nent_, 0);
+  dst_.assign(nent_, 0);
+  d_off_ = DevBuf(8ull * nent_);
+  d_len_ = DevBuf(4ull * nent_);
+  if (nent_) {
+    DevBuf d_vals = upload(idx.vals.data(), idx.vals.size()), d_vend = upload(idx.val_end.data(), nent_);
+    DevBuf d_dst(4ull * nent_);
     abi_check(mtblx_block_dir(dfile_.as<uint8_t>(), file_.size(), version_, d_vals.as<uint8_t>(),
-                              d_vend.as<uint32_t>(), 0, nent, d_off.as<uint64_t>(), d_len.as<uint32_t>(),
+                              d_vend.as<uint32_t>(), 0, nent_, d_off_.as<uint64_t>(), d_len_.as<uint32_t>(),
                               d_dst.as<int32_t>(), nullptr),
               "mtblx_block_dir");
     hip_check(hipDeviceSynchronize(), "sync");
-    boff = download<uint64_t>(d_off.p, nent);
-    blen = download<uint32_t>(d_len.p, nent);
-    dst = download<int32_t>(d_dst.p, nent);
-    if (verify) {
-      DevBuf d_bad(nent);
-      mtblx_block_batch in{dfile_.as<uint8_t>(), file_.size(), d_off.as<uint64_t>(), d_len.as<uint32_t>(), nent,
-                           *std::max_element(blen.begin(), blen.end())};
-      abi_check(mtblx_crc32c_blocks(&in, nullptr, d_bad.as<uint8_t>(), 1, nullptr), "mtblx_crc32c_blocks");
-      hip_check(hipDeviceSynchronize(), "sync");
-      bad = download<uint8_t>(d_bad.p, nent);
-    }
+    boff_ = download<uint64_t>(d_off_.p, nent_);
+    blen_ = download<uint32_t>(d_len_.p, nent_);
+    dst_ = download<int32_t>(d_dst.p, nent_);
   }
-  // Reader::block's decompression (src/reader.rs:166-170), any CompressionType, on the host
-  // (compression stays on the host per the north star: mtblx_decompress_blocks); then one
-  // device decode of every block
-  std::vector<uint8_t> zerr(nent, 0);
-  if (nent && meta_.compression_algorithm != 0) {
-    std::vector<uint64_t> so(nent, 0), uoff(nent, 0), ulen(nent, 0);
-    std::vector<uint32_t> sn(nent, 0);
-    std::vector<int32_t> zst(nent, 0);
-    for (uint32_t i = 0; i < nent; ++i)
-      if (dst[i] == MTBLX_DIR_OK) { so[i] = boff[i]; sn[i] = blen[i]; }
-    uint8_t* ubuf = nullptr;
-    mtblx_decompress_blocks(static_cast<uint32_t>(meta_.compression_algorithm), file_.data(), so.data(), sn.data(),
-                            nent, 16, &ubuf, uoff.data(), ulen.data(), zst.data());
-    if (!ubuf) throw std::bad_alloc();
-    std::vector<uint32_t> ul(nent);
-    uint32_t mx = 0;
-    uint64_t tot = 0;
-    for (uint32_t i = 0; i < nent; ++i) {
-      zerr[i] = dst[i] == MTBLX_DIR_OK && zst[i] != MTBLX_CODEC_OK;
-      if (ulen[i] > 0xFFFFFFFFull) { mtblx_free(ubuf); throw std::runtime_error("decompressed block >= 4 GiB"); }
-      ul[i] = zerr[i] ? 0u : (uint32_t)ulen[i];
-      mx = std::max(mx, ul[i]);
-      tot = std::max(tot, uoff[i] + ulen[i]);
-    }
-    DevBuf d_u = upload(ubuf, tot + 1), d_uo = upload(uoff.data(), nent), d_ul = upload(ul.data(), nent);
-    mtblx_free(ubuf);
-    dec_ = decode_batch(d_u.as<uint8_t>(), tot + 1, d_uo.as<uint64_t>(), d_ul.as<uint32_t>(), nent, mx);
-  } else if (nent) {
-    std::vector<uint32_t> l2(blen);
-    for (uint32_t i = 0; i < nent; ++i)
-      if (dst[i] != MTBLX_DIR_OK) l2[i] = 0;   // never decoded: the iteration stops before it
-    DevBuf d_l2 = upload(l2.data(), nent);
-    dec_ = decode_batch(dfile_.as<uint8_t>(), file_.size(), d_off.as<uint64_t>(), d_l2.as<uint32_t>(), nent,
-                        *std::max_element(l2.begin(), l2.end()));
-  }
-  // ReaderIntoIter::next's end rules over the per-block outcomes (src/reader.rs:337-405)
-  size_t take_blocks = 0, take_last = 0;
-  bool stopped = false;
-  if (nent == 0 && idx.status[0] == MTBLX_ST_CORRUPT) end_ = End::Panic;
-  for (uint32_t i = 0; i < nent && !stopped; ++i) {
-    if (dst[i] != MTBLX_DIR_OK || bad[i]) { end_ = End::Panic; take_blocks = i; stopped = true; break; }
-    if (zerr[i]) { end_ = i == 0 ? End::ErrOpen : End::ErrNext; err_ = MtblError::Io; take_blocks = i; stopped = true; break; }
-    const int32_t s = dec_.status[i];
-    if (s == MTBLX_ST_INVALID_BLOCK) {
-      end_ = i == 0 ? End::ErrOpen : End::ErrNext;
-      err_ = MtblError::InvalidBlock;
-      take_blocks = i;
-      stopped = true;
-      break;
-    }
-    if (s == MTBLX_ST_UNSUPPORTED) throw std::runtime_error("block >= 4 GiB");
-    if (s == MTBLX_ST_OK && dec_.nrec[i] == 0 && i > 0) { take_blocks = i; stopped = true; break; }
-    if (s == MTBLX_ST_CORRUPT || s == MTBLX_ST_LOOP) {
-      take_blocks = i;
-      take_last = dec_.nrec[i];
-      end_ = s == MTBLX_ST_CORRUPT ? End::Panic : End::Loop;
-      stopped = true;
-      break;
-    }
-  }
-  if (!stopped && nent) {
-    take_blocks = nent;
-    if (idx.status[0] == MTBLX_ST_CORRUPT) end_ = End::Panic;   // past the index's last entry
-    else if (idx.status[0] == MTBLX_ST_LOOP) end_ = End::Loop;
-  }
-  if (end_ == End::ErrOpen) throw Error(err_);   // ReaderIntoIter::new returns the Err
-  // global END offsets of the yielded records (blocks are laid out in order from record 0)
-  for (size_t b = 0; b < take_blocks + (take_last ? 1 : 0); ++b) {
-    const size_t cnt = b < take_blocks ? dec_.nrec[b] : take_last;
-    for (size_t q = 0; q < cnt; ++q) {
-      const size_t r = dec_.rec_base[b] + q;
-      gke_.push_back(dec_.key_base[b] + dec_.key_end[r]);
-      gve_.push_back(dec_.val_base[b] + dec_.val_end[r]);
-    }
-  }
-  nrec_ = gke_.size();
 }
 
-inline std::optional<Record> ReaderIntoIter::next() {
-  if (i_ < end_) return r_->rec(i_++);
-  switch (r_->end_) {
-    case Reader::End::None: return std::nullopt;
-    case Reader::End::ErrOpen:
-    case Reader::End::ErrNext: throw Error(r_->err_);
-    case Reader::End::Panic: throw Panic("corrupt block: the reference panics here");
-    case Reader::End::Loop: throw Panic("zero-progress entry: the reference never returns");
+// blocks [i0, i1) as next() loads them: Reader::block (framing, checksum, host decompression
+// -- compression stays on the host per the north star) + one device decode of the range
+inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t i1) const {
+  using namespace detail;
+  const uint32_t n = (uint32_t)(i1 - i0);
+  std::vector<ReaderIntoIter::Loaded> out(n);
+  std::vector<uint8_t> bad(n, 0);
+  std::vector<uint32_t> l2(blen_.begin() + i0, blen_.begin() + i1);
+  for (uint32_t i = 0; i < n; ++i)
+    if (dst_[i0 + i] != MTBLX_DIR_OK) l2[i] = 0;   // never decoded: the iteration stops before it
+  DevBuf d_l2 = upload(l2.data(), n);
+  const uint64_t* d_o = d_off_.as<uint64_t>() + i0;
+  const uint32_t mx = n ? *std::max_element(l2.begin(), l2.end()) : 0;
+  if (verify_ && n) {
+    DevBuf d_bad(n);
+    mtblx_block_batch in{dfile_.as<uint8_t>(), file_.size(), d_o, d_l2.as<uint32_t>(), n, mx};
+    abi_check(mtblx_crc32c_blocks(&in, nullptr, d_bad.as<uint8_t>(), 1, nullptr), "mtblx_crc32c_blocks");
+    hip_check(hipDeviceSynchronize(), "sync");
+    bad = download<uint8_t>(d_bad.p, n);
   }
-  return std::nullopt;
+  std::vector<uint8_t> zerr(n, 0);
+  std::shared_ptr<DevBuf> ubuf;
+  std::vector<uint64_t> uoff(n, 0);
+  std::vector<uint32_t> ul(n, 0);
+  Decoded dec;
+  if (meta_.compression_algorithm != 0) {
+    std::vector<uint64_t> so(n, 0), ulen(n, 0);
+    std::vector<uint32_t> sn(n, 0);
+    std::vector<int32_t> zst(n, 0);
+    for (uint32_t i = 0; i < n; ++i)
+      if (dst_[i0 + i] == MTBLX_DIR_OK && !bad[i]) { so[i] = boff_[i0 + i]; sn[i] = blen_[i0 + i]; }
+    uint8_t* hb = nullptr;
+    mtblx_decompress_blocks(static_cast<uint32_t>(meta_.compression_algorithm), file_.data(), so.data(), sn.data(), n,
+                            16, &hb, uoff.data(), ulen.data(), zst.data());
+    if (!hb) throw std::bad_alloc();
+    uint32_t umx = 0;
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      zerr[i] = sn[i] && zst[i] != MTBLX_CODEC_OK;
+      if (ulen[i] > 0xFFFFFFFFull) { mtblx_free(hb); throw std::runtime_error("decompressed block >= 4 GiB"); }
+      ul[i] = zerr[i] ? 0u : (uint32_t)ulen[i];
+      umx = std::max(umx, ul[i]);
+      tot = std::max(tot, uoff[i] + ulen[i]);
+    }
+    ubuf = std::make_shared<DevBuf>(upload(hb, tot + 1));
+    mtblx_free(hb);
+    DevBuf d_uo = upload(uoff.data(), n), d_ul = upload(ul.data(), n);
+    dec = decode_batch(ubuf->as<uint8_t>(), tot + 1, d_uo.as<uint64_t>(), d_ul.as<uint32_t>(), n, umx);
+  } else {
+    dec = decode_batch(dfile_.as<uint8_t>(), file_.size(), d_o, d_l2.as<uint32_t>(), n, mx);
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    auto& L = out[i];
+    if (dst_[i0 + i] != MTBLX_DIR_OK || bad[i]) { L.code = 1; continue; }
+    if (zerr[i]) { L.code = 2; continue; }
+    const int32_t s = dec.status[i];
+    if (s == MTBLX_ST_INVALID_BLOCK) { L.code = 3; continue; }
+    if (s == MTBLX_ST_UNSUPPORTED) { L.code = 4; continue; }
+    auto& b = L.bi;
+    if (ubuf) b.c = ReaderIntoIter::Content{ubuf, ubuf->as<uint8_t>(), uoff[i], ul[i]};
+    else b.c = ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), boff_[i0 + i], blen_[i0 + i]};
+    b.end = s == MTBLX_ST_CORRUPT ? MTBLX_EMIT_PANIC : s == MTBLX_ST_LOOP ? MTBLX_EMIT_LOOP : MTBLX_EMIT_END;
+    const uint64_t r0 = dec.rec_base[i], kb = dec.key_base[i], vb = dec.val_base[i];
+    uint64_t kend = 0, vend = 0;
+    for (uint32_t q = 0; q < dec.nrec[i]; ++q) {
+      kend = dec.key_end[r0 + q];
+      vend = dec.val_end[r0 + q];
+      b.ke.push_back(kend);
+      b.ve.push_back(vend);
+    }
+    b.keys.assign(dec.keys.begin() + kb, dec.keys.begin() + kb + kend);
+    b.vals.assign(dec.vals.begin() + vb, dec.vals.begin() + vb + vend);
+  }
+  return out;
+}
+
+inline size_t Reader::len() const {
+  if (!len_) {
+    ReaderIntoIter it = into_iter();
+    size_t n = 0;
+    try {
+      while (it.next()) ++n;
+    } catch (const std::exception&) {   // the records before an Err / panic count
+    }
+    len_ = n;
+  }
+  return *len_;
+}
+
+inline mtblx_index_seek Reader::index_seek(const Bytes& key) const {
+  using namespace detail;
+  const uint64_t kend = key.size();
+  DevBuf d_key = upload_key(key), d_kend = upload(&kend, 1);
+  DevBuf d_out(sizeof(mtblx_index_seek));
+  abi_check(mtblx_index_seek_batch(dfile_.as<uint8_t>(), file_.size(), version_, verify_ ? 1 : 0, index_off_,
+                                   index_len_, d_key.as<uint8_t>(), d_kend.as<uint64_t>(), 1,
+                                   d_out.as<mtblx_index_seek>(), nullptr),
+            "mtblx_index_seek_batch");
+  hip_check(hipDeviceSynchronize(), "sync");
+  return download<mtblx_index_seek>(d_out.p, 1)[0];
+}
+
+inline size_t Reader::ordinal(uint64_t entry) const {
+  using namespace detail;
+  if (!eoffs_known_) {
+    DevBuf d_offs(8ull * std::max<uint32_t>(nent_, 1)), d_cnt(8);
+    abi_check(mtblx_entry_offsets(dfile_.as<uint8_t>() + index_off_, index_len_, d_offs.as<uint64_t>(), nent_,
+                                  d_cnt.as<uint64_t>(), nullptr),
+              "mtblx_entry_offsets");
+    hip_check(hipDeviceSynchronize(), "sync");
+    const uint64_t cnt = std::min<uint64_t>(download<uint64_t>(d_cnt.p, 1)[0], nent_);
+    eoffs_ = download<uint64_t>(d_offs.p, cnt);
+    eoffs_known_ = true;
+  }
+  const auto it = std::lower_bound(eoffs_.begin(), eoffs_.end(), entry);
+  if (it == eoffs_.end() || *it != entry) throw std::runtime_error("index seek landed off the index scan chain");
+  return (size_t)(it - eoffs_.begin());
+}
+
+inline ReaderIntoIter::Content Reader::seek_content(const mtblx_index_seek& s) const {
+  using namespace detail;
+  if (s.block_status == MTBLX_SEEK_PANIC) throw Panic("Reader::block");
+  if (meta_.compression_algorithm == 0) {
+    if (s.block_status == MTBLX_SEEK_ERR) throw Error(MtblError::InvalidBlock);
+    if (s.block_status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("block >= 4 GiB");
+    return ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), s.data_off, s.data_len};
+  }
+  // compressed: decompress on the host, Block::init runs on the result (mtblx_block_seek_batch)
+  uint8_t* out = nullptr;
+  uint64_t n = 0;
+  if (mtblx_decompress(static_cast<uint32_t>(meta_.compression_algorithm), file_.data() + s.data_off, s.data_len, &out,
+                       &n) != MTBLX_CODEC_OK)
+    throw Error(MtblError::Io);
+  auto own = std::make_shared<DevBuf>(upload(out, n ? n : 1));
+  mtblx_free(out);
+  return ReaderIntoIter::Content{own, own->as<uint8_t>(), 0, n};
+}
+
+inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Bytes& key, uint64_t kcap) {
+  using namespace detail;
+  mtblx_block_seek q{};
+  q.data_off = c.off;
+  q.data_len = c.len;
+  q.kcap = kcap;
+  q.max_records = ~0ull >> 2;
+  q.first = 0;
+  uint64_t rec_cap = c.len / 3 + 1, keys_cap = 2 * c.len + 64, vals_cap = c.len + 16;
+  const uint64_t kend = key.size();
+  DevBuf d_key = upload_key(key), d_kend = upload(&kend, 1);
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    DevBuf d_q = upload(&q, 1), d_k(keys_cap + 1), d_v(vals_cap + 1), d_ke(8 * rec_cap + 8), d_ve(8 * rec_cap + 8),
+        d_kc(8 * rec_cap + 8);
+    abi_check(mtblx_block_seek_batch(c.base, d_key.as<uint8_t>(), d_kend.as<uint64_t>(), 1, d_q.as<mtblx_block_seek>(),
+                                     d_k.as<uint8_t>(), keys_cap, d_v.as<uint8_t>(), vals_cap, d_ke.as<uint64_t>(),
+                                     d_ve.as<uint64_t>(), d_kc.as<uint64_t>(), rec_cap, nullptr),
+              "mtblx_block_seek_batch");
+    hip_check(hipDeviceSynchronize(), "sync");
+    const mtblx_block_seek res = download<mtblx_block_seek>(d_q.p, 1)[0];
+    if (res.end == MTBLX_EMIT_OVERFLOW) {
+      rec_cap = res.nrec;
+      keys_cap = res.key_bytes;
+      vals_cap = res.val_bytes;
+      continue;
+    }
+    if (res.status == MTBLX_SEEK_ERR) throw Error(MtblError::InvalidBlock);
+    if (res.status == MTBLX_SEEK_PANIC) throw Panic("BlockIter::seek");
+    if (res.status == MTBLX_SEEK_LOOP) throw Panic("BlockIter::seek never returns");
+    if (res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: block >= 4 GiB or key > 64 KiB");
+    Bi b;
+    b.c = c;
+    b.end = res.end;
+    b.ke = download<uint64_t>(d_ke.p, res.nrec);
+    b.ve = download<uint64_t>(d_ve.p, res.nrec);
+    b.kcaps = download<uint64_t>(d_kc.p, res.nrec);
+    b.kcaps_known = true;
+    b.kcap_end = res.kcap;
+    b.keys = download<uint8_t>(d_k.p, res.key_bytes);
+    b.vals = download<uint8_t>(d_v.p, res.val_bytes);
+    if (res.has_val) b.last_val = download<uint8_t>(c.base + c.off + res.last_voff, res.last_vlen);
+    return b;
+  }
+  throw std::runtime_error("mtblx_block_seek_batch: output sizes did not converge");
+}
+
+// the key Vec's capacity of the held iterator now (parse_next_key's END leaves it unchanged)
+inline uint64_t ReaderIntoIter::kcap_now(Bi& b) {
+  using namespace detail;
+  if (b.n() == 0) return b.kcap_end;
+  if (!b.kcaps_known) {   // records from the bulk decoder: replay seek_to_first + next on the device
+    mtblx_block_seek q{};
+    q.data_off = b.c.off;
+    q.data_len = b.c.len;
+    q.max_records = b.n();
+    q.first = 1;
+    const uint64_t kend = 0;
+    const uint8_t z = 0;
+    DevBuf d_key = upload(&z, 1), d_kend = upload(&kend, 1), d_q = upload(&q, 1);
+    DevBuf d_k(2 * b.c.len + 65), d_v(b.c.len + 17), d_ke(8 * b.n() + 8), d_ve(8 * b.n() + 8), d_kc(8 * b.n() + 8);
+    abi_check(mtblx_block_seek_batch(b.c.base, d_key.as<uint8_t>(), d_kend.as<uint64_t>(), 1,
+                                     d_q.as<mtblx_block_seek>(), d_k.as<uint8_t>(), 2 * b.c.len + 64,
+                                     d_v.as<uint8_t>(), b.c.len + 16, d_ke.as<uint64_t>(), d_ve.as<uint64_t>(),
+                                     d_kc.as<uint64_t>(), b.n(), nullptr),
+              "mtblx_block_seek_batch");
+    hip_check(hipDeviceSynchronize(), "sync");
+    b.kcaps = download<uint64_t>(d_kc.p, b.n());
+    b.kcaps_known = true;
+  }
+  return b.kcaps[std::min(b.pos, b.n() - 1)];
+}
+
+inline ReaderIntoIter::Bi ReaderIntoIter::load(size_t i) {
+  if (chunk_.empty() || i < chunk0_ || i >= chunk0_ + chunk_.size()) {
+    const size_t n = std::min<size_t>(r_->nent_ - i, grow_);
+    grow_ = std::min<size_t>(2 * grow_, 256);
+    chunk_ = r_->load_range(i, i + n);
+    chunk0_ = i;
+  }
+  Loaded& L = chunk_[i - chunk0_];
+  switch (L.code) {
+    case 1: throw Panic("Reader::block: framing / checksum");
+    case 2: throw Error(MtblError::Io);
+    case 3: throw Error(MtblError::InvalidBlock);
+    case 4: throw std::runtime_error("block >= 4 GiB");
+  }
+  return L.bi;
+}
+
+inline void ReaderIntoIter::init_iter() {   // new (src/reader.rs:231-254)
+  if (r_->nent_ == 0) {
+    if (r_->index_status_ == MTBLX_ST_CORRUPT) throw Panic("index block: first entry");
+    return;
+  }
+  e_ = 0;
+  bi_ = load(0);
+}
+
+inline void ReaderIntoIter::init_from(const Bytes& key) {   // new_from (src/reader.rs:256-279)
+  const mtblx_index_seek s = r_->index_seek(key);
+  if (s.status == MTBLX_SEEK_PANIC) throw Panic("index seek");
+  if (s.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
+  if (!s.valid) return;
+  e_ = (int64_t)r_->ordinal(s.entry);
+  bi_ = seek_block(r_->seek_content(s), key, 0);
+}
+
+inline std::optional<Record> ReaderIntoIter::next() {   // src/reader.rs:337-405
+  if (!valid_ || !bi_) return std::nullopt;
+  Bi* b = &*bi_;
+  if (!first_ && b->pos < b->n()) ++b->pos;   // bi.next()
+  first_ = false;
+  if (b->pos == b->n() && b->end == MTBLX_EMIT_PANIC) throw Panic("BlockIter::next / get");
+  if (b->pos == b->n() && b->end == MTBLX_EMIT_LOOP) throw Panic("zero-progress entry: the reference never returns");
+  if (b->pos == b->n()) {
+    valid_ = false;
+    if (e_ < 0) return std::nullopt;
+    if ((size_t)e_ + 1 >= r_->nent_) {       // index_iter.next() past the last entry
+      e_ = -1;
+      if (r_->index_status_ == MTBLX_ST_CORRUPT) throw Panic("index block: next entry");
+      if (r_->index_status_ == MTBLX_ST_LOOP) throw Panic("index block never returns");
+      return std::nullopt;
+    }
+    ++e_;
+    Bi nb = load((size_t)e_);                // Some(Err(e)) throws; valid stays false
+    bi_ = std::move(nb);
+    b = &*bi_;
+    if (b->n() == 0 && b->end == MTBLX_EMIT_PANIC) throw Panic("BlockIter::seek_to_first / get");
+    if (b->n() == 0) return std::nullopt;
+    valid_ = true;
+  }
+  const Record rec = b->rec(b->pos);
+  const size_t kl = k_.size();
+  const int c = std::memcmp(rec.key, k_.data(), std::min(rec.key_len, kl));
+  if (type_ == kGet) valid_ = c == 0 && rec.key_len == kl;
+  else if (type_ == kPrefix) valid_ = rec.key_len >= kl && (kl == 0 || std::memcmp(rec.key, k_.data(), kl) == 0);
+  else if (type_ == kRange) valid_ = !(c > 0 || (c == 0 && rec.key_len > kl));
+  if (!valid_) return std::nullopt;
+  return rec;
+}
+
+inline bool ReaderIntoIter::seek(const Bytes& key) {   // src/reader.rs:302-335
+  const mtblx_index_seek s = r_->index_seek(key);
+  if (s.status == MTBLX_SEEK_PANIC) throw Panic("index seek");
+  if (s.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
+  if (!s.valid) {   // past the last key: next() returns None
+    valid_ = false;
+    e_ = -1;
+    return true;
+  }
+  e_ = (int64_t)r_->ordinal(s.entry);
+  if (block_offset_ != s.block_off) {
+    block_offset_ = s.block_off;   // updated before the load (:322)
+    Bi nb = seek_block(r_->seek_content(s), key, 0);
+    bi_ = std::move(nb);
+  } else if (bi_) {                 // the held block, whatever it is
+    Bi nb = seek_block(bi_->c, key, kcap_now(*bi_));
+    bi_ = std::move(nb);
+  }
+  first_ = true;
+  valid_ = true;
+  return true;
 }
 
 inline std::optional<Bytes> Reader::get(const uint8_t* key, size_t klen) const {
   using namespace detail;
-  if (meta_.compression_algorithm != 0) {   // values live in decompressed blocks: the decoded records
-    const size_t i = lower_bound(key, klen);
-    if (i < nrec_) {
-      const Record r = rec(i);
-      if (r.key_len == klen && std::memcmp(r.key, key, klen) == 0) return r.val_bytes();
+  if (meta_.compression_algorithm != 0) {   // values live in decompressed blocks: the seek iterator
+    ReaderIntoIter it(this, ReaderIntoIter::kGet, Bytes(key, key + klen));
+    it.init_from(Bytes(key, key + klen));
+    std::optional<Bytes> held = it.bi_ ? it.bi_->last_val : std::nullopt;
+    try {
+      auto r = it.next();
+      if (!r) return std::nullopt;
+      return r->val_bytes();
+    } catch (const Error&) {
+      // next() returned Some(Err): Reader::get returns the OLD block iterator's val
+      // (src/reader.rs:111-122, :376-379), or None
+      return held;
     }
-    return std::nullopt;
   }
   const uint64_t kend = klen;
   DevBuf d_key = upload(key, klen ? klen : 1), d_kend = upload(&kend, 1);
@@ -477,45 +767,6 @@ inline std::optional<Bytes> Reader::get(const uint8_t* key, size_t klen) const {
   if (st == MTBLX_GET_NONE) return std::nullopt;
   if (st == MTBLX_GET_ERR) throw Error(MtblError::InvalidBlock);
   throw Panic(st == MTBLX_GET_LOOP ? "Reader::get never returns" : "Reader::get panics");
-}
-
-inline size_t Reader::lower_bound(const uint8_t* k, size_t kl) const {
-  size_t lo = 0, hi = nrec_;
-  while (lo < hi) {   // first record whose key >= k (keys are sorted)
-    const size_t mid = (lo + hi) / 2;
-    const Record r = rec(mid);
-    const int c = std::memcmp(r.key, k, std::min(r.key_len, kl));
-    if (c < 0 || (c == 0 && r.key_len < kl)) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-inline std::vector<Record> Reader::iter_prefix(const Bytes& p) const {
-  std::vector<Record> out;
-  for (size_t i = lower_bound(p.data(), p.size()); i < nrec_; ++i) {
-    const Record r = rec(i);
-    if (r.key_len < p.size() || std::memcmp(r.key, p.data(), p.size()) != 0) break;
-    out.push_back(r);
-  }
-  return out;
-}
-
-inline std::vector<Record> Reader::iter_range(const Bytes& s, const Bytes& e) const {
-  std::vector<Record> out;
-  for (size_t i = lower_bound(s.data(), s.size()); i < nrec_; ++i) {
-    const Record r = rec(i);
-    const int c = std::memcmp(r.key, e.data(), std::min(r.key_len, e.size()));
-    if (c > 0 || (c == 0 && r.key_len > e.size())) break;   // key > end (end is inclusive)
-    out.push_back(r);
-  }
-  return out;
-}
-
-inline std::vector<Record> Reader::iter_from(const Bytes& k) const {
-  std::vector<Record> out;
-  for (size_t i = lower_bound(k.data(), k.size()); i < nrec_; ++i) out.push_back(rec(i));
-  return out;
 }
 
 }  // namespace mtbl

@@ -104,14 +104,37 @@ static void test_cfg1(mtbl::CompressionType c) {   // examples/dump.rs + get-key
   for (size_t q : {size_t(0), size_t(1), size_t(4095), size_t(9999)}) CHECK(reader.get(recs[q].first).value() == B(recs[q].second));
   CHECK(!reader.get("0000000000x").has_value() && !reader.get("x").has_value() && !reader.get("").has_value());
   // GetPrefix: "00000012" -> keys 1200..1299
-  auto p = reader.iter_prefix(B("00000012"));
-  CHECK(p.size() == 100 && S(p[0].key, p[0].key_len) == "0000001200" && S(p[99].key, p[99].key_len) == "0000001299");
+  auto p = reader.iter_prefix(B("00000012")).collect();
+  CHECK(p.size() == 100 && p[0].first == B("0000001200") && p[99].first == B("0000001299"));
   // GetRange (end inclusive)
-  auto g = reader.iter_range(B("0000000500"), B("0000000600"));
-  CHECK(g.size() == 101 && S(g.back().val, 10) == "0000000600");
+  auto g = reader.iter_range(B("0000000500"), B("0000000600")).collect();
+  CHECK(g.size() == 101 && Bytes(g.back().second.begin(), g.back().second.begin() + 10) == B("0000000600"));
   // From
-  auto f = reader.iter_from(B("0000009990"));
-  CHECK(f.size() == 10);
+  auto f = reader.iter_from(B("0000009990")).collect();
+  CHECK(f.size() == 10 && f[0].first == B("0000009990"));
+  CHECK(reader.iter_prefix(B("x")).collect().empty() && reader.iter_from(B("1")).collect().empty());
+  // ReaderIntoIter::seek (src/reader.rs:302-335)
+  auto it = reader.iter_from(B("0000005000"));
+  auto r0 = it.next();
+  CHECK(r0 && S(r0->key, r0->key_len) == "0000005000");
+  CHECK(it.seek(B("0000009000")));                 // another block: loaded and seeked
+  auto r1 = it.next();
+  CHECK(r1 && S(r1->key, r1->key_len) == "0000009000");
+  auto r2 = it.next();
+  CHECK(r2 && S(r2->key, r2->key_len) == "0000009001");
+  // block_offset is still 0 (next() never sets it, the seek above set it to 9000's block):
+  // a seek into block 0 now reloads block 0
+  CHECK(it.seek(B("0000000003")));
+  auto r3 = it.next();
+  CHECK(r3 && S(r3->key, r3->key_len) == "0000000003");
+  // the block_offset quirk: a fresh iter_from keeps block_offset 0, so seeking into block 0
+  // (offset 0) re-seeks the block it holds instead of loading block 0
+  auto q = reader.iter_from(B("0000005000"));
+  (void)q.next();
+  CHECK(q.seek(B("0000000003")));
+  auto r4 = q.next();
+  CHECK(r4 && S(r4->key, r4->key_len) != "0000000003" && S(r4->key, r4->key_len) <= "0000005000");
+  CHECK(q.seek(B("zzz")) && !q.next().has_value());   // past the last key
 }
 
 static void test_errors() {

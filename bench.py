@@ -688,9 +688,21 @@ def main():
         hv = out.totals_host()
         if hv != (nrec, kbytes, vbytes, 0) or int(vbad.sum().item()) != 0:
             raise RuntimeError(f"fused verify decode mismatch: {hv}")
+        # the default mtblx_decode_blocks_verify: the decode, then k_crc32c_blocks, one stream
+        vbad.zero_()
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=False)
+            d_ms = _timed(lambda: codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=False),
+                          stream, 20)
+        hv = out.totals_host()
+        if hv != (nrec, kbytes, vbytes, 0) or int(vbad.sum().item()) != 0:
+            raise RuntimeError(f"decode+verify mismatch: {hv}")
         crc_info = {"kernel": "k_crc32c_blocks", "ms": round(crc_ms, 4),
                     "GiB_per_s": round(block_bytes / (crc_ms * 1e-3) / 2**30, 1),
                     "bad_blocks": int(bad.sum().item()),
+                    "decode_blocks_verify": {"kernels": "k_decode_pipe<PipeSmall> + k_crc32c_blocks", "ms": round(d_ms, 4),
+                                             "GiB_per_s": round(block_bytes / (d_ms * 1e-3) / 2**30, 1)},
                     "fused_decode_verify": {"kernel": "k_decode_pipe<PipeSmallV>", "ms": round(v_ms, 4),
                                             "GiB_per_s": round(block_bytes / (v_ms * 1e-3) / 2**30, 1),
                                             "vs_decode_then_crc_GiB_per_s": None}}

@@ -2,14 +2,11 @@
 // before it decodes a block (/root/reference/src/reader.rs:159-164, crate crc32c 0.4:
 // CRC-32C Castagnoli, reflected polynomial 0x82F63B78, init/xorout 0xFFFFFFFF).
 //
-// One wave per block.  The block is cut into 64-byte chunks counted from its END; lane j
-// computes the raw (init 0, no xorout) table-driven CRC of chunk j, then shifts it to its
-// place by a GF(2) multiply with x^(8*64*j) mod P:
+// One wave per block: 64-byte windows counted from the block's END, one per lane, staged through
+// LDS so every global load instruction reads 1 KiB contiguous; each window's raw CRC
+// (slicing-by-8) is shifted into place with a GF(2) multiply by x^(512 k) mod P:
 //   crc_raw(A || B) = multmodp(x^(8|B|), crc_raw(A)) ^ crc_raw(B)
-// and the wave XOR-reduces.  The 0xFFFFFFFF init is folded in by complementing the first 4
-// content bytes (equivalent for blocks of >= 4 bytes); the result is complemented at the end.
-// x^(512 m) for any chunk index m comes from three 512-entry tables (9 bits each), computed
-// at compile time (crc_dev.h).
+// and the wave XOR-reduces; see k_crc32c_blocks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -18,21 +15,98 @@
 
 namespace mtblx_crc {
 
-__global__ void __launch_bounds__(kThreads) k_crc32c_blocks(const uint8_t* data, uint64_t data_len, const uint64_t* blk_off,
-                                                            const uint32_t* blk_len, uint32_t nblk, uint32_t* crc_out,
-                                                            uint8_t* bad, int framed) {
-  __shared__ uint32_t T[256];
-  for (int i = threadIdx.x; i < 256; i += kThreads) T[i] = kTab.byte[i];
+constexpr int kCrcThreads = 256;   // 4 waves per workgroup
+
+// Slicing-by-8 tables: T8[k][i] = CRC of byte i followed by k zero bytes.
+struct Slice8 {
+  uint32_t t[8][256];
+};
+
+// raw CRC (init 0) of the 64-byte window ending at block position hi: bytes before the block
+// start (positions < 0) count as zeros, which leave a zero-init CRC unchanged; the 0xFFFFFFFF
+// init is folded into block bytes 0..3.  16 words -> 8 slicing-by-8 steps.
+__device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, const uint32_t (*T)[256], bool safe) {
+  const int64_t lo = hi - kChunk;
+  uint32_t w[16];
+  if (safe) {   // d + lo is readable (inside the buffer) even where lo < 0
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
+      w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+    }
+  } else {      // the window starts before the buffer: byte loads of the in-block part only
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int64_t p = lo + 4 * m + b;
+        v |= (p >= 0 ? (uint32_t)d[p] : 0u) << (8 * b);
+      }
+      w[m] = v;
+    }
+  }
+  if (lo < 4) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int64_t pos = lo + 4 * m;   // block position of the word's first byte
+      if (pos < 4) {
+        const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+        const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8 * (uint32_t)pos);
+        w[m] = (w[m] & keep) ^ fold;
+      }
+    }
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int m = 0; m < 16; m += 2) {
+    const uint32_t x = c ^ w[m], y = w[m + 1];
+    c = T[7][x & 0xFFu] ^ T[6][(x >> 8) & 0xFFu] ^ T[5][(x >> 16) & 0xFFu] ^ T[4][x >> 24] ^
+        T[3][y & 0xFFu] ^ T[2][(y >> 8) & 0xFFu] ^ T[1][(y >> 16) & 0xFFu] ^ T[0][y >> 24];
+  }
+  return c;
+}
+
+// One wave per block: lane j takes the 64-byte windows j, j + 64, ... counted from the block's
+// END (window k = block bytes [L - 64 (k + 1), L - 64 k)), each a raw CRC shifted into place
+// by x^(512 k) (a GF(2) multiply; k < 64 from an LDS table), XOR-reduced over the wave.
+__global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* data, uint64_t data_len,
+                                                               const uint64_t* blk_off, const uint32_t* blk_len,
+                                                               uint32_t nblk, uint32_t* crc_out, uint8_t* bad,
+                                                               int framed) {
+  __shared__ Slice8 S;
+  __shared__ uint32_t XP[kWave];   // x^(512 k), k < 64
+  for (int i = threadIdx.x; i < 4 * 256; i += kCrcThreads) S.t[i >> 8][i & 255] = kTab.slice[i >> 8][i & 255];
+  for (int i = threadIdx.x; i < kWave; i += kCrcThreads) XP[i] = kTab.x0[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * 256; i += kCrcThreads) {   // tables 4..7 from table 3
+    uint32_t t = S.t[3][i & 255];
+    for (int k = 0; k <= (i >> 8); ++k) t = (t >> 8) ^ S.t[0][t & 0xFFu];
+    S.t[4 + (i >> 8)][i & 255] = t;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const uint32_t waves = gridDim.x * (kThreads / kWave);
-  for (uint32_t b = blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6); b < nblk; b += waves) {
+  const uint32_t waves = gridDim.x * (kCrcThreads / kWave);
+  for (uint32_t b = blockIdx.x * (kCrcThreads / kWave) + (threadIdx.x >> 6); b < nblk; b += waves) {
     const uint64_t off = blk_off[b];
     const uint64_t L = blk_len[b];
     const uint8_t* d = data + off;
     // a window past the buffer: the reference's slice panics before the checksum (bad = 1)
     const bool oob = off + L > data_len;
-    const uint32_t acc = oob ? 0u : wave_crc32c(d, L, T, lane);
+    uint32_t acc = 0;
+    if (!oob && L >= (uint64_t)kChunk) {
+      for (uint64_t k = lane; k * kChunk < L; k += kWave) {
+        const int64_t hi = (int64_t)(L - k * kChunk);
+        const bool safe = (int64_t)off + hi - kChunk >= 0;
+        const uint32_t c = window_crc(d, hi, S.t, safe);
+        acc ^= dmultmodp(k < (uint64_t)kWave ? XP[k] : xpow512(k), c);
+      }
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, sh, kWave);
+      acc ^= 0xFFFFFFFFu;
+    } else if (!oob) {
+      acc = wave_crc32c(d, L, S.t[0], lane);   // < 64 bytes: byte-wise
+    }
     if (lane == 0) {
       if (crc_out) crc_out[b] = acc;
       if (bad && oob) {
@@ -59,11 +133,11 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = (ncu > 0 ? ncu : 256) * 8;   // 32 waves per CU in flight
+    grid = (ncu > 0 ? ncu : 256) * 8;   // 32 waves per CU
   }
   const uint32_t need = (in->nblk + 3u) / 4u;
   hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, dim3(need < (uint32_t)grid ? need : (uint32_t)grid),
-                     dim3(mtblx_crc::kThreads), 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len, in->blk_off,
-                     in->blk_len, in->nblk, crc, bad, framed);
+                     dim3(mtblx_crc::kCrcThreads), 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
+                     in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -24,18 +24,35 @@ constexpr uint32_t multmodp(uint32_t a, uint32_t b) {  // a * b mod P, reflected
 
 struct Tables {
   uint32_t byte[256];   // byte-wise table
+  uint32_t slice[4][256];   // slicing-by-4: slice[k][i] = CRC of byte i followed by k zero bytes
+  uint32_t xb[64];      // x^(8 * r)              r < 64
   uint32_t x0[512];     // x^(512 * m)            m < 512
   uint32_t x1[512];     // x^(512 * 512 * m)
   uint32_t x2[512];     // x^(512 * 512 * 512 * m)
-  constexpr Tables() : byte(), x0(), x1(), x2() {
+  static constexpr uint32_t x8_1() {   // x^8
+    uint32_t v = 0x80000000u;
+    for (int k = 0; k < 8; ++k) v = (v & 1u) ? (v >> 1) ^ kPoly : v >> 1;
+    return v;
+  }
+  constexpr Tables() : byte(), slice(), xb(), x0(), x1(), x2() {
     for (uint32_t i = 0; i < 256; ++i) {
       uint32_t c = i;
       for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
       byte[i] = c;
     }
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t t = byte[i];
+      slice[0][i] = t;
+      for (int k = 1; k < 4; ++k) {
+        t = (t >> 8) ^ byte[t & 0xFFu];
+        slice[k][i] = t;
+      }
+    }
     // x^8 = one byte of shift; x^(512) = 64 bytes
     uint32_t x8 = 0x80000000u;                                   // x^0
     for (int k = 0; k < 8; ++k) x8 = (x8 & 1u) ? (x8 >> 1) ^ kPoly : x8 >> 1;   // x^8
+    xb[0] = 0x80000000u;
+    for (int r = 1; r < 64; ++r) xb[r] = multmodp(x8_1(), xb[r - 1]);
     uint32_t x512 = 0x80000000u;
     for (int k = 0; k < kChunk; ++k) x512 = multmodp(x8, x512);
     x0[0] = 0x80000000u;
@@ -66,6 +83,11 @@ __device__ __forceinline__ uint32_t xpow512(uint64_t m) {  // x^(512 m) mod P
   if (m >> 9) r = dmultmodp(kTab.x1[(m >> 9) & 511], r);
   if (m >> 18) r = dmultmodp(kTab.x2[(m >> 18) & 511], r);
   return r;
+}
+
+__device__ __forceinline__ uint32_t xpow8(uint64_t n) {  // x^(8 n) mod P: n bytes of shift
+  const uint32_t r = kTab.xb[n & 63];
+  return (n >> 6) ? dmultmodp(xpow512(n >> 6), r) : r;
 }
 
 // CRC-32C of d[0..L) by one wave (all 64 lanes call it with the same arguments; the result

@@ -1980,15 +1980,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   a.flags_direct = 1;
   if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; }
   if constexpr (P::VERIFY) {
-    for (int i = tid; i < 256; i += kPipeThreads) {   // slicing-by-4 tables from the byte table
-      uint32_t t = mtblx_crc::kTab.byte[i];
-      S.crcT[0][i] = t;
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
-        S.crcT[k][i] = t;
-      }
-    }
+    for (int i = tid; i < 4 * 256; i += kPipeThreads) S.crcT[i >> 8][i & 255] = mtblx_crc::kTab.slice[i >> 8][i & 255];
     for (int i = tid; i < 2 * P::MAXBLK; i += kPipeThreads) S.cacc[i / P::MAXBLK][i % P::MAXBLK] = 0;
   }
 

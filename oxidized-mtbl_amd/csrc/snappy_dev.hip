@@ -56,6 +56,18 @@ struct alignas(16) WaveLds {
 
 __device__ __forceinline__ void lds_fence() { __asm__ volatile("" ::: "memory"); }
 
+#ifdef MTBLX_SNAP_STAMPS
+// diagnostic build only: per-phase shader cycles summed over waves (lane 0) --
+// [0] total per block [1] inside flush [2] output store [3] elements [4] flushes [5] blocks
+// [6] restages [7] 64-byte run steps
+__device__ unsigned long long g_snap_dbg[8];
+#define SNAP_T() __builtin_amdgcn_s_memtime()
+#define SNAP_ADD(k, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_snap_dbg[k], (unsigned long long)(v)); } while (0)
+#else
+#define SNAP_T() 0ull
+#define SNAP_ADD(k, v) do { } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 // A window: the block's stored bytes at block positions [wstart, wstart + W) (wstart = p0
@@ -107,12 +119,15 @@ template <class C>
 __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const uint8_t* __restrict__ s, uint32_t n,
                                            const uint8_t* s2, uint32_t n2, uint8_t* __restrict__ dg, uint32_t cap,
                                            int lane, int32_t* st_out, uint32_t* dec_len) {
+  const uint64_t t_blk = SNAP_T();
+  uint64_t t_fl = 0, n_el = 0, n_fl = 0, n_rs = 0, n_st = 0;
   // ---- LDS window over the stored bytes ----
   int32_t wstart = pf.wstart;   // block position of window byte 0 (16-byte aligned in memory; may be < 0)
   uint32_t whi = pf.whi;        // window holds block positions [max(wstart, 0), whi)
   pf.store(S.win, lane);
   pf.load(s2, n2, 0, lane);
   auto restage = [&](uint32_t p0) {
+    ++n_rs;
     Window<C> w;
     w.load(s, n, p0, lane);
     w.store(S.win, lane);
@@ -120,12 +135,15 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     whi = w.whi;
   };
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(S.win);
-  // 8 bytes at block position p (p in the window), wave-uniform
+  // 8 bytes at block position p (p in the window), wave-uniform.  The words are moved to SGPRs
+  // and shifted with 64-bit scalar shifts, so the whole tag parse that follows stays on the
+  // scalar unit (a v_alignbit here put it on the VALU: ~100 vector instructions per element).
   auto hdr8 = [&](uint32_t p, uint32_t& lo, uint32_t& hi) {
     const uint32_t wi = (uint32_t)((int32_t)p - wstart), q = wi >> 2, sh = (wi & 3u) * 8u;
     const uint32_t a = ufl(w32[q]), b = ufl(w32[q + 1]), c = ufl(w32[q + 2]);
-    lo = __builtin_amdgcn_alignbit(b, a, sh);
-    hi = __builtin_amdgcn_alignbit(c, b, sh);
+    const uint64_t ab = ((uint64_t)b << 32 | a) >> sh, bc = ((uint64_t)c << 32 | b) >> sh;
+    lo = ufl((uint32_t)ab);
+    hi = ufl((uint32_t)bc);
   };
 
   // ---- preamble: varint32 uncompressed length ----
@@ -146,7 +164,7 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
   int32_t st = MTBLX_SNAPPY_OK;
   if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
   else if (want > cap) st = MTBLX_SNAPPY_TOO_SMALL;
-  const uint32_t W = (uint32_t)want;
+  const uint32_t W = ufl((uint32_t)want);
   const bool glob = W > (uint32_t)C::OUT;   // assemble in place in HBM
 
   // ---- element runs ----
@@ -159,6 +177,7 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     const uint32_t T = d - D;
     uint32_t k0 = 0;
     for (uint32_t base = 0; base < T; base += kWave) {
+      ++n_st;
       const uint32_t B = D + base;
       const uint32_t i = min(base + (uint32_t)lane, T - 1u), p = D + i;
       const uint32_t m = (uint32_t)__popcll(__ballot(e_d > B && e_d <= B + (kWave - 1)));   // lanes >= ne: ~0
@@ -192,6 +211,8 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
   };
   auto flush = [&]() {
     if (ne == 0) return;
+    const uint64_t t0 = SNAP_T();
+    ++n_fl;
     const uint32_t T = d - D;
     lds_fence();
     if (glob) {
@@ -233,8 +254,10 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     ne = 0;
     D = d;
     e_d = 0xFFFFFFFFu;
+    t_fl += SNAP_T() - t0;
   };
   auto park = [&](uint32_t len, uint32_t lit, uint32_t x) {
+    ++n_el;
     if ((uint32_t)lane == ne) {
       e_d = d;
       e_len = len | (lit << 31);
@@ -245,7 +268,16 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     if (ne == (uint32_t)kWave) flush();
   };
 
+  n = ufl(n);
   while (st == MTBLX_SNAPPY_OK && pos < n) {
+    // the parse state is wave-uniform: pin it to SGPRs so the tag decode runs on the scalar
+    // unit (left to divergence analysis, it lived in VGPRs: ~100 VALU ops per element)
+    pos = ufl(pos);
+    d = ufl(d);
+    D = ufl(D);
+    ne = ufl(ne);
+    wstart = (int32_t)ufl((uint32_t)wstart);
+    whi = ufl(whi);
     const uint32_t need = min(pos + 5u, n);
     if (need > whi) {
       flush();
@@ -316,6 +348,7 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     if (d != W) st = MTBLX_SNAPPY_CORRUPT;
   }
   // ---- LDS output -> HBM ----
+  const uint64_t t_out = SNAP_T();
   if (st == MTBLX_SNAPPY_OK && !glob) {
     lds_fence();
     if (((uintptr_t)dg & 15u) == 0) {
@@ -332,6 +365,14 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     if (dec_len) dec_len[0] = st == MTBLX_SNAPPY_OK ? W : 0u;
   }
   lds_fence();
+  SNAP_ADD(0, SNAP_T() - t_blk);
+  SNAP_ADD(1, t_fl);
+  SNAP_ADD(2, SNAP_T() - t_out);
+  SNAP_ADD(3, n_el);
+  SNAP_ADD(4, n_fl);
+  SNAP_ADD(5, 1);
+  SNAP_ADD(6, n_rs);
+  SNAP_ADD(7, n_st);
 }
 
 template <class C>
@@ -508,3 +549,14 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   }
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
+
+#ifdef MTBLX_SNAP_STAMPS
+extern "C" int mtblx_snap_debug(uint64_t* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mtblx_snap::g_snap_dbg), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (reset) {
+    static const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mtblx_snap::g_snap_dbg), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

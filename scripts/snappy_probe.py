@@ -12,7 +12,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "oxidized-mtbl_amd")]
 
-from mtblx import codec, synth  # noqa: E402
+from mtblx import _lib, codec, synth  # noqa: E402
 from mtblx.writer import Writer  # noqa: E402
 
 
@@ -59,6 +59,17 @@ def main():
     out_bytes = int(dl.sum().item())
     print(f"decompress {ms:.4f} ms  {out_bytes / ms / 1e6:.1f} GB/s out  stored {int(zln.sum()) / ms / 1e6:.1f} GB/s in"
           f"  bad={int((st != 0).sum().item())}", flush=True)
+    L = _lib.lib()
+    if hasattr(L, "mtblx_snap_debug"):   # the snapstamps diagnostic build
+        import ctypes as C
+        dbg = (C.c_uint64 * 8)()
+        L.mtblx_snap_debug(dbg, 1)
+        codec.snappy_decompress_into(zb, lay, dst, st, dl, int(tot[1]), s)
+        torch.cuda.synchronize()
+        L.mtblx_snap_debug(dbg, 0)
+        nb = max(int(dbg[5]), 1)
+        print("per block: cycles %.0f  in flush %.0f  store %.0f  elements %.1f  flushes %.1f  restages %.2f  steps %.1f"
+              % (dbg[0] / nb, dbg[1] / nb, dbg[2] / nb, dbg[3] / nb, dbg[4] / nb, dbg[6] / nb, dbg[7] / nb), flush=True)
 
 
 if __name__ == "__main__":

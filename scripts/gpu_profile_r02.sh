@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_r02
-rm -rf $OUT; mkdir -p $OUT
+mkdir -p $OUT
 run() {  # name cmd...
   local name=$1; shift
   echo "=== $name ($(date +%T))"
@@ -17,7 +17,7 @@ run() {  # name cmd...
 }
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
 SQ2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
-for lib in cur r01; do
+for lib in ${LIBS:-cur r01}; do
   LIBARG=""; [ $lib = r01 ] && LIBARG="--lib oxidized-mtbl_amd/build/libmtblx_r01.so"
   for cfg in small large; do
     BA="--no-cpu-baseline --no-e2e --no-crc --no-ceiling $LIBARG"

@@ -306,7 +306,7 @@ class ReaderIntoIter {
   void init_iter();
   void init_from(const Bytes& key);
   Bi load(size_t i);
-  Bi seek_block(const Content& c, const Bytes& key, uint64_t kcap);
+  static Bi seek_block(const Content& c, const Bytes* key, uint64_t kcap);   // key null: seek_to_first
   uint64_t kcap_now(Bi& b);
   const Reader* r_;
   Kind type_;
@@ -357,6 +357,7 @@ class Reader {
   size_t ordinal(uint64_t entry) const;
   ReaderIntoIter::Content seek_content(const mtblx_index_seek& s) const;
   std::vector<ReaderIntoIter::Loaded> load_range(size_t i0, size_t i1) const;
+  void load_big(size_t i, ReaderIntoIter::Loaded& L) const;
   Bytes file_;
   detail::DevBuf dfile_;
   bool verify_;
@@ -369,6 +370,7 @@ class Reader {
   std::vector<uint32_t> blen_;
   std::vector<int32_t> dst_;
   detail::DevBuf d_off_, d_len_;
+  std::vector<std::pair<uint32_t, uint64_t>> big_;   // entries whose content is >= 4 GiB: block offset
   mutable std::vector<uint64_t> eoffs_;
   mutable bool eoffs_known_ = false;
   mutable std::optional<size_t> len_;
@@ -430,6 +432,13 @@ inline Reader::Reader(const uint8_t* data, size_t len, bool verify) : file_(data
     boff_ = download<uint64_t>(d_off_.p, nent_);
     blen_ = download<uint32_t>(d_len_.p, nent_);
     dst_ = download<int32_t>(d_dst.p, nent_);
+    for (uint32_t i = 0; i < nent_; ++i) {   // block_at_index's offset of >= 4 GiB blocks (host)
+      if (dst_[i] != MTBLX_DIR_UNSUPPORTED) continue;
+      const uint32_t v0 = i ? idx.val_end[i - 1] : 0;
+      uint64_t o = 0;
+      mtblx_varint_decode64(idx.vals.data() + v0, idx.val_end[i] - v0, &o);
+      big_.emplace_back(i, o);
+    }
   }
 }
 
@@ -486,6 +495,10 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t 
   }
   for (uint32_t i = 0; i < n; ++i) {
     auto& L = out[i];
+    if (dst_[i0 + i] == MTBLX_DIR_UNSUPPORTED) {   // content >= 4 GiB (u64 restart array)
+      load_big(i0 + i, L);
+      continue;
+    }
     if (dst_[i0 + i] != MTBLX_DIR_OK || bad[i]) { L.code = 1; continue; }
     if (zerr[i]) { L.code = 2; continue; }
     const int32_t s = dec.status[i];
@@ -507,6 +520,28 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t 
     b.vals.assign(dec.vals.begin() + vb, dec.vals.begin() + vb + vend);
   }
   return out;
+}
+
+// Reader::block + Block::init + the scan of a block >= 4 GiB: framing and checksum on the host
+// (mtblx_frame_block), the scan on the device (the emitting block seek, seek_to_first)
+inline void Reader::load_big(size_t i, ReaderIntoIter::Loaded& L) const {
+  if (meta_.compression_algorithm != 0) throw std::runtime_error("compressed block >= 4 GiB");
+  uint64_t boff = 0;
+  for (const auto& e : big_)
+    if (e.first == i) boff = e.second;
+  uint64_t coff = 0, clen = 0;
+  int panic = 0;
+  if (mtblx_frame_block(file_.data(), file_.size(), version_, boff, verify_ ? 1 : 0, &coff, &clen, &panic) != MTBLX_OK) {
+    L.code = 1;
+    return;
+  }
+  try {
+    L.bi = ReaderIntoIter::seek_block(ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), coff, clen}, nullptr, 0);
+  } catch (const Error&) {
+    L.code = 3;
+  } catch (const Panic&) {
+    L.code = 1;
+  }
 }
 
 inline size_t Reader::len() const {
@@ -571,17 +606,21 @@ inline ReaderIntoIter::Content Reader::seek_content(const mtblx_index_seek& s) c
   return ReaderIntoIter::Content{own, own->as<uint8_t>(), 0, n};
 }
 
-inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Bytes& key, uint64_t kcap) {
+inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Bytes* key, uint64_t kcap) {
   using namespace detail;
   mtblx_block_seek q{};
   q.data_off = c.off;
   q.data_len = c.len;
   q.kcap = kcap;
   q.max_records = ~0ull >> 2;
-  q.first = 0;
-  uint64_t rec_cap = c.len / 3 + 1, keys_cap = 2 * c.len + 64, vals_cap = c.len + 16;
-  const uint64_t kend = key.size();
-  DevBuf d_key = upload_key(key), d_kend = upload(&kend, 1);
+  q.first = key ? 0 : 1;
+  // output sized exactly from a first counting pass when the block is big (>= 4 GiB blocks)
+  const bool big = c.len > (64ull << 20);
+  uint64_t rec_cap = big ? 4096 : c.len / 3 + 1, keys_cap = big ? 1 << 20 : 2 * c.len + 64,
+           vals_cap = big ? 1 << 20 : c.len + 16;
+  const Bytes none;
+  const uint64_t kend = key ? key->size() : 0;
+  DevBuf d_key = upload_key(key ? *key : none), d_kend = upload(&kend, 1);
   for (int attempt = 0; attempt < 3; ++attempt) {
     DevBuf d_q = upload(&q, 1), d_k(keys_cap + 1), d_v(vals_cap + 1), d_ke(8 * rec_cap + 8), d_ve(8 * rec_cap + 8),
         d_kc(8 * rec_cap + 8);
@@ -675,7 +714,7 @@ inline void ReaderIntoIter::init_from(const Bytes& key) {   // new_from (src/rea
   if (s.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
   if (!s.valid) return;
   e_ = (int64_t)r_->ordinal(s.entry);
-  bi_ = seek_block(r_->seek_content(s), key, 0);
+  bi_ = seek_block(r_->seek_content(s), &key, 0);
 }
 
 inline std::optional<Record> ReaderIntoIter::next() {   // src/reader.rs:337-405
@@ -724,10 +763,10 @@ inline bool ReaderIntoIter::seek(const Bytes& key) {   // src/reader.rs:302-335
   e_ = (int64_t)r_->ordinal(s.entry);
   if (block_offset_ != s.block_off) {
     block_offset_ = s.block_off;   // updated before the load (:322)
-    Bi nb = seek_block(r_->seek_content(s), key, 0);
+    Bi nb = seek_block(r_->seek_content(s), &key, 0);
     bi_ = std::move(nb);
   } else if (bi_) {                 // the held block, whatever it is
-    Bi nb = seek_block(bi_->c, key, kcap_now(*bi_));
+    Bi nb = seek_block(bi_->c, &key, kcap_now(*bi_));
     bi_ = std::move(nb);
   }
   first_ = true;

@@ -51,7 +51,8 @@ extern "C" {
 #define MTBLX_ST_CORRUPT 2       /* the reference panics (assert/unwrap/slice, src/block.rs:59,79,131-135,217-235);
                                     nrec[b] = records the reference yielded before the panic          */
 #define MTBLX_ST_LOOP 3          /* zero-progress entry: the reference yields it forever; emitted once */
-#define MTBLX_ST_UNSUPPORTED 4   /* block >= 4 GiB (u64 restart arrays): not decoded on the device    */
+#define MTBLX_ST_UNSUPPORTED 4   /* block >= 4 GiB (u64 restart arrays): not decoded by this batched
+                                    call (u32 lengths); mtblx_block_seek_batch decodes such blocks    */
 #define MTBLX_ST_OVERFLOW 5      /* caller's key/value/record capacity exceeded; block not written    */
 #define MTBLX_ST_DECOMPRESS 6    /* (mtblx_pipe_decode) host decompression failed: Reader::block returns
                                     Err(Error::Io) (src/reader.rs:166, src/compression.rs:57-68)      */
@@ -158,7 +159,8 @@ int mtblx_decode_blocks_verify(const mtblx_block_batch* in, const mtblx_decoded*
                                    mtblx_crc32c_blocks (framed) and mtblx_decode_blocks */
 #define MTBLX_DIR_PANIC 1       /* the reference panics: offset >= file length, varint on an
                                    empty value, content slice past the end of the file   */
-#define MTBLX_DIR_UNSUPPORTED 2 /* content >= 4 GiB                                       */
+#define MTBLX_DIR_UNSUPPORTED 2 /* content >= 4 GiB: blk_off = the content start, blk_len 0 (a batch
+                                   cannot carry it); decode it with mtblx_block_seek_batch, first=1 */
 int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, const uint8_t* vals,
                     const uint32_t* val_end, uint64_t val_base, uint32_t nent, uint64_t* blk_off,
                     uint32_t* blk_len, int32_t* dir_st, void* stream);
@@ -196,7 +198,8 @@ int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int veri
 #define MTBLX_SEEK_ERR 1          /* Err(InvalidBlock) from Block::init                       */
 #define MTBLX_SEEK_PANIC 2        /* the reference panics                                     */
 #define MTBLX_SEEK_LOOP 3         /* the reference never returns (zero-progress entry)        */
-#define MTBLX_SEEK_UNSUPPORTED 4  /* block >= 4 GiB, or a key > 64 KiB in the emitting seek    */
+#define MTBLX_SEEK_UNSUPPORTED 4  /* a key > 64 KiB in the emitting seek (blocks >= 4 GiB with u64
+                                     restart arrays are handled: src/block.rs:25-42, :95-104)   */
 typedef struct mtblx_index_seek {
   int32_t status;          /* of the index seek: OK / PANIC / LOOP                               */
   int32_t valid;           /* index_iter.get() is Some after the seek                             */

@@ -158,7 +158,7 @@ def write_file(records, block_size=8192, restart_interval=16, compression=0) -> 
         n = C.c_uint64(0)
         if L.oracle_writer_finish(w, C.byref(out), C.byref(n)) != 0:
             raise RuntimeError("reference panics in Writer::into_inner")
-        data = C.string_at(out, n.value)
+        data = _take(C.addressof(out.contents), n.value) if n.value else b""
         L.oracle_free(out)
         return data
     finally:
@@ -178,7 +178,7 @@ def build_block(records, restart_interval=16) -> bytes:
                                  _ptr(ve, C.c_uint64), C.byref(out), C.byref(n))
     if r != 0:
         raise RuntimeError("reference panics in BlockBuilder::add")
-    data = C.string_at(out, n.value)
+    data = _take(C.addressof(out.contents), n.value) if n.value else b""
     lib().oracle_free(out)
     return data
 
@@ -260,6 +260,15 @@ def bench_scan(data: np.ndarray, blk_off, blk_len, nthreads=1, iters=1):
     return ns.value * 1e-9, nr.value, h
 
 
+def _take(addr: int, n: int) -> bytes:
+    """n bytes at addr (ctypes.string_at takes a C int size: copy larger ranges with memmove)"""
+    if n < (1 << 31):
+        return C.string_at(addr, n)
+    a = np.empty(n, np.uint8)
+    C.memmove(a.ctypes.data, addr, n)
+    return a.tobytes()
+
+
 # ---------------- file-level iteration ----------------
 class _ScanRes(C.Structure):
     _fields_ = [("end", C.c_int32), ("err", C.c_int32), ("nrec", C.c_uint64), ("keys", C.POINTER(C.c_uint8)),
@@ -282,8 +291,8 @@ def file_scan(data: bytes, mode="iter", key=b"", key2=b"", verify=True, max_reco
     pk = pv = 0
     for i in range(r.nrec):
         ke, ve = r.key_end[i], r.val_end[i]
-        recs.append((C.string_at(C.addressof(r.keys.contents) + pk, ke - pk) if ke > pk else b"",
-                     C.string_at(C.addressof(r.vals.contents) + pv, ve - pv) if ve > pv else b""))
+        recs.append((_take(C.addressof(r.keys.contents) + pk, ke - pk) if ke > pk else b"",
+                     _take(C.addressof(r.vals.contents) + pv, ve - pv) if ve > pv else b""))
         pk, pv = ke, ve
     out = dict(end=r.end, err=ERR_NAMES[r.err], records=recs, meta=list(r.meta), version=r.version)
     lib().oracle_scan_free(C.byref(r))
@@ -324,8 +333,8 @@ def iter_script(data: bytes, mode="iter", key=b"", key2=b"", ops=(), verify=True
     pk = pv = 0
     for i in range(r.nrec):
         ke, ve = r.key_end[i], r.val_end[i]
-        recs.append((C.string_at(C.addressof(r.keys.contents) + pk, ke - pk) if ke > pk else b"",
-                     C.string_at(C.addressof(r.vals.contents) + pv, ve - pv) if ve > pv else b""))
+        recs.append((_take(C.addressof(r.keys.contents) + pk, ke - pk) if ke > pk else b"",
+                     _take(C.addressof(r.vals.contents) + pv, ve - pv) if ve > pv else b""))
         pk, pv = ke, ve
     out = dict(end=r.end, err=ERR_NAMES[r.err], records=recs, meta=list(r.meta), version=r.version,
                ops=[(int(ores[2 * i]), int(ores[2 * i + 1])) for i in range(len(code))])

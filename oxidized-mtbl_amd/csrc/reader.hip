@@ -84,7 +84,7 @@ __global__ void k_block_dir(const uint8_t* file, uint64_t file_len, uint32_t ver
     if (start > file_len || sz > file_len - start) st = MTBLX_DIR_PANIC;   // BytesView::slice assert
     else if (sz > 0xFFFFFFFFull) st = MTBLX_DIR_UNSUPPORTED;
   }
-  blk_off[i] = st == MTBLX_DIR_OK ? start : 0;
+  blk_off[i] = (st == MTBLX_DIR_OK || st == MTBLX_DIR_UNSUPPORTED) ? start : 0;   // >= 4 GiB: start only
   blk_len[i] = st == MTBLX_DIR_OK ? (uint32_t)sz : 0u;
   dir_st[i] = st;
 }
@@ -108,6 +108,7 @@ struct Blk {
   const uint8_t* d;
   uint64_t L, R;
   uint32_t n;
+  bool wide;   // u64 restart array (blocks >= 4 GiB)
 };
 
 struct It {
@@ -135,7 +136,8 @@ __device__ __forceinline__ uint32_t dec32g(const uint8_t* d, uint64_t n, uint32_
   return l;
 }
 
-// Block::init (src/block.rs:16-49): 0 ok, 1 InvalidBlock, -1 panic
+// Block::init (src/block.rs:16-49): 0 ok, 1 InvalidBlock, -1 panic.  A restart offset past
+// u32::MAX means a u64 restart array (blocks >= 4 GiB, src/block.rs:25-42).
 __device__ __forceinline__ int block_init(const uint8_t* d, uint64_t L, Blk& b) {
   if (L < 4) return 1;
   if (L < 8) return -1;
@@ -146,12 +148,16 @@ __device__ __forceinline__ int block_init(const uint8_t* d, uint64_t L, Blk& b) 
     if (ro <= kU32) return 1;
   }
   if (ro > L - 4) return 1;
-  if (ro > kU32) return -1;   // u64 restart arrays (>= 4 GiB): not supported on the device
-  b.d = d; b.L = L; b.R = ro; b.n = n;
+  b.d = d; b.L = L; b.R = ro; b.n = n; b.wide = ro > kU32;
   return 0;
 }
 
-__device__ __forceinline__ uint64_t restart_point(const Blk& b, uint32_t i) { return rd32g(b.d + b.R + 4ull * i); }
+// BlockIter::restart_point (src/block.rs:95-104): a u64 array keeps the 4-byte stride of the
+// u32 one (the reference indexes `restarts + idx * 4` either way)
+__device__ __forceinline__ uint64_t restart_point(const Blk& b, uint32_t i) {
+  const uint8_t* p = b.d + b.R + 4ull * i;
+  return b.wide ? ((uint64_t)rd32g(p) | ((uint64_t)rd32g(p + 4) << 32)) : (uint64_t)rd32g(p);
+}
 
 // decode_entry (src/block.rs:216-238): R_OK or R_PANIC
 __device__ __forceinline__ int decode_entry(const Blk& b, uint64_t p, uint64_t limit, uint32_t& sh, uint32_t& ns,
@@ -381,7 +387,6 @@ __device__ int frame_block(const FileCtx& f, uint64_t off, uint64_t& start, uint
   if (start > f.len || sz > f.len - start) return MTBLX_SEEK_PANIC;
   if (f.verify && mtblx_crc::wave_crc32c(f.file + start, sz, f.T, f.lane) != rd32g(f.file + off + ll))
     return MTBLX_SEEK_PANIC;
-  if (sz > kU32) return MTBLX_SEEK_UNSUPPORTED;
   Blk b;
   const int bi = block_init(f.file + start, sz, b);
   return bi == 1 ? MTBLX_SEEK_ERR : bi < 0 ? MTBLX_SEEK_PANIC : MTBLX_SEEK_OK;
@@ -526,7 +531,6 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
     Blk b{};
     SIt it{};
     do {
-      if (L > kU32) { Q.status = MTBLX_SEEK_UNSUPPORTED; break; }
       __syncthreads();
       if (L <= kSeekStage) {
         for (uint64_t i = (uint64_t)lane; i < L; i += 64) stage[i] = src[i];
@@ -566,7 +570,15 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
         if (!ovf && (Q.nrec >= rec_cap || kb > keys_cap || vb > vals_cap)) ovf = true;
         if (!ovf) {
           for (uint64_t j = (uint64_t)lane; j < it.klen; j += 64) kd[Q.key_bytes + j] = K[j];
-          for (uint64_t j = (uint64_t)lane; j < it.vlen; j += 64) vd[Q.val_bytes + j] = d[it.voff + j];
+          uint64_t j0 = 0;
+          if (it.vlen >= 4096) {   // big values (blocks >= 4 GiB hold values of GiBs): 16 B per lane
+            typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
+            const uint64_t nv = it.vlen / 16;
+            for (uint64_t c = (uint64_t)lane; c < nv; c += 64)
+              *reinterpret_cast<v4u*>(vd + Q.val_bytes + 16 * c) = *reinterpret_cast<const v4u*>(d + it.voff + 16 * c);
+            j0 = 16 * nv;
+          }
+          for (uint64_t j = j0 + (uint64_t)lane; j < it.vlen; j += 64) vd[Q.val_bytes + j] = d[it.voff + j];
           if (lane == 0) {
             oke[(uint64_t)q * rec_cap + Q.nrec] = kb;
             ove[(uint64_t)q * rec_cap + Q.nrec] = vb;

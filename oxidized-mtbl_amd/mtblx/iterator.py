@@ -83,9 +83,12 @@ class Emitted:
         return out
 
 
-def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 << 62) -> Emitted:
+def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 << 62,
+               small_caps: bool = False) -> Emitted:
     """BlockIter::seek(key) (key None: seek_to_first) on content = (tensor, off, len) with the
-    given key capacity, then the records it yields until get() is None."""
+    given key capacity, then the records it yields until get() is None.  small_caps: start
+    from small output buffers and size them exactly from the first pass's counts (blocks of
+    GiBs)."""
     data, off, ln = content
     dev = data.device
     kb = _dev_bytes(key or b"", dev)
@@ -93,6 +96,8 @@ def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 <
     q = _lib.BlockSeek(data_off=off, data_len=ln, kcap=kcap, max_records=max_records, first=1 if key is None else 0)
     rec_cap = min(max_records, ln // 3 + 1)
     keys_cap, vals_cap = 2 * ln + 64, ln + 16
+    if small_caps:
+        rec_cap, keys_cap, vals_cap = min(rec_cap, 1 << 16), min(keys_cap, 1 << 20), min(vals_cap, 1 << 20)
     for _ in range(3):
         qt = torch.frombuffer(bytearray(bytes(q)), dtype=torch.uint8).to(dev)
         okeys = torch.empty(max(keys_cap, 1), dtype=torch.uint8, device=dev)

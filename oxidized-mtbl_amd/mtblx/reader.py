@@ -188,22 +188,6 @@ class Reader:
         return self._dir3
 
     # ------------------------------------------------------------------ iteration
-    def _decode_all(self):
-        off, ln, st, bad = self.directory()
-        self.zerr = None
-        if self.compression != 0 and self.nent:
-            # Reader::block decompresses after the checksum (src/reader.rs:166-170): on the
-            # host, as the north star keeps src/compression.rs there; then one device decode
-            buf, uoff, uln, self.zerr = self._host_stage(off, ln, st)
-            ml = int(uln.max()) if uln.size else 0
-            self._dbatch = codec.DeviceBatch.from_host(buf, uoff, uln, device=self.file.device)
-        else:
-            ml = int(ln.max().item()) if self.nent else 0
-            self._dbatch = codec.DeviceBatch(self.file, off, ln, ml)
-        self.data = codec.decode_blocks(self._dbatch) if self.nent else None
-        torch.cuda.synchronize()
-        return off, ln, st, bad
-
     def _host_stage(self, off, ln, st):
         """Reader::block's decompression step (src/reader.rs:166-170 -> src/compression.rs:57-68)
         on the host for every block the directory frames, any CompressionType:
@@ -237,81 +221,169 @@ class Reader:
         """ReaderIntoIter (mode Iter) to the end: the records yielded and how it ends."""
         if self._scan is not None:
             return self._scan
-        off, ln, st, bad = self._decode_all()
+        from . import iterator
         n = self.nent
-        dst = st.cpu().numpy() if n else np.zeros(0, np.int32)
-        cbad = bad.cpu().numpy() if (bad is not None and n) else np.zeros(n, np.uint8)
-        if n:
-            h = self.data.to_host()
-            bst, bnr = h.status, h.nrec.astype(np.int64)
-        else:
-            bst = bnr = np.zeros(0, np.int64)
-        end, err, take_blocks, take_last = END_NONE, "None", 0, 0
-        # ReaderIntoIter::new: block_at_index(first entry) -- errors here are Err at open
-        i = 0
-        if n == 0:
-            end = END_PANIC if self.index_status in (_lib.ST_CORRUPT,) else END_NONE
-        while i < n:
-            # Reader::block for entry i
-            if dst[i] != _lib.DIR_OK or cbad[i]:
-                end = END_PANIC if dst[i] != _lib.DIR_UNSUPPORTED else END_PANIC
-                break
-            if self.zerr is not None and self.zerr[i]:   # decompress -> Err(Error::Io) (src/reader.rs:166)
-                end, err = (END_ERR_OPEN if i == 0 else END_ERR_NEXT), "Io"
-                break
-            s = int(bst[i])
-            if s == _lib.ST_INVALID_BLOCK:
-                end, err = (END_ERR_OPEN if i == 0 else END_ERR_NEXT), "InvalidBlock"
-                break
-            if s == _lib.ST_UNSUPPORTED:
-                raise NotImplementedError("block >= 4 GiB")
-            # an empty block ends the iteration, except the first one (src/reader.rs:362-371)
-            if s == _lib.ST_OK and bnr[i] == 0 and i > 0:
-                break
-            if s in (_lib.ST_CORRUPT, _lib.ST_LOOP):   # records before the panic / loop, then stop
-                take_blocks, take_last = i, int(bnr[i])
-                end = END_PANIC if s == _lib.ST_CORRUPT else END_LOOP
-                i = -1
-                break
-            i += 1
-        if i == n and n:
-            take_blocks = n
+        end, err = END_NONE, "None"
+        if n == 0:   # ReaderIntoIter::new with no index entry; a corrupt index panics at its first
+            end = END_PANIC if self.index_status == _lib.ST_CORRUPT else END_NONE
+            self._scan = iterator._assemble([], end, err, self.file.device)
+            return self._scan
+        parts, end, err, stopped = self._walk_blocks(0, n, first_exempt=True)
+        if not stopped:
             if self.index_status == _lib.ST_CORRUPT:
                 end = END_PANIC          # the index iterator panics advancing past its last entry
             elif self.index_status == _lib.ST_LOOP:
                 end = END_LOOP
-        elif i >= 0:
-            take_blocks = i
-        nblk_full = take_blocks
-        self._scan = self._cut(nblk_full, take_last, end, err)
+        self._scan = iterator._assemble(parts, end, err, self.file.device)
         return self._scan
 
-    def _cut(self, nblk_full: int, take_last: int, end: int, err: str) -> Scan:
-        return self._cut_data(self.data, nblk_full, take_last, end, err)
+    def _walk_blocks(self, i0: int, i1: int, first_exempt: bool):
+        """ReaderIntoIter::next over directory entries [i0, i1) (src/reader.rs:337-405):
+        Reader::block's framing / checksum / decompression, Block::init, the scan; an empty
+        block loaded by next() ends the iteration (first_exempt: block i0 came from
+        ReaderIntoIter::new, whose Err is an Err at open and whose emptiness does not end it).
+        Blocks >= 4 GiB are decoded one by one (_big_block) and spliced in.
+        -> (parts [(keys, vals, key_end, val_end, nrec)], end, err, stopped)"""
+        dst, bad, zerr, data, _ = self._decode_range(i0, i1)
+        n = i1 - i0
+        bst = data.status[:n].cpu().numpy()
+        bnr = data.nrec[:n].cpu().numpy().astype(np.int64)
+        parts, seg, take_last = [], 0, 0
+        end, err, stopped = END_NONE, "None", False
 
-    def _cut_data(self, d, nblk_full: int, take_last: int, end: int, err: str) -> Scan:
+        def errend(i):
+            return END_ERR_OPEN if (first_exempt and i == 0) else END_ERR_NEXT
+
+        i = 0
+        while i < n:
+            if dst[i] == _lib.DIR_UNSUPPORTED:   # content >= 4 GiB (u64 restart array)
+                parts.append(self._slice(data, seg, i, 0))
+                seg = i + 1
+                kind, em = self._big_block(i0 + i)
+                if kind == "panic":
+                    end, stopped = END_PANIC, True
+                    break
+                if kind == "loop":
+                    end, stopped = END_LOOP, True
+                    break
+                if kind != "ok":
+                    end, err, stopped = errend(i), kind, True
+                    break
+                if em.nrec == 0 and em.end == _lib.EMIT_END and not (first_exempt and i == 0):
+                    stopped = True
+                    break
+                parts.append((em.keys, em.vals, em.key_end, em.val_end, em.nrec))
+                if em.end in (_lib.EMIT_PANIC, _lib.EMIT_LOOP):
+                    end, stopped = (END_PANIC if em.end == _lib.EMIT_PANIC else END_LOOP), True
+                    break
+                i += 1
+                continue
+            if dst[i] != _lib.DIR_OK or bad[i]:        # Reader::block panics (framing / checksum)
+                end, stopped = END_PANIC, True
+                break
+            if zerr[i]:                                # decompress -> Err(Error::Io) (src/reader.rs:166)
+                end, err, stopped = errend(i), "Io", True
+                break
+            st = int(bst[i])
+            if st == _lib.ST_INVALID_BLOCK:
+                end, err, stopped = errend(i), "InvalidBlock", True
+                break
+            if st == _lib.ST_UNSUPPORTED:
+                raise NotImplementedError("decompressed block >= 4 GiB")
+            if st == _lib.ST_OK and bnr[i] == 0 and not (first_exempt and i == 0):
+                stopped = True                         # an empty block ends the iteration (:362-371)
+                break
+            if st in (_lib.ST_CORRUPT, _lib.ST_LOOP):  # the records before the panic / loop, then stop
+                take_last = int(bnr[i])
+                end, stopped = (END_PANIC if st == _lib.ST_CORRUPT else END_LOOP), True
+                break
+            i += 1
+        parts.append(self._slice(data, seg, i, take_last))
+        return parts, end, err, stopped
+
+    def _slice(self, d, i0: int, i1: int, take_last: int):
+        """records of decoded blocks [i0, i1) plus the first take_last records of block i1
+        -> (keys, vals, key_end, val_end, nrec) on the device, END offsets from the slice start"""
         dev = self.file.device
-        if d is None or (nblk_full == 0 and take_last == 0):
-            z = torch.zeros(0, dtype=torch.uint8, device=dev)
-            e = torch.zeros(0, dtype=torch.int64, device=dev)
-            return Scan(end, err, 0, z, z, e, e)
-        nr = d.nrec[: d.nblk].to(torch.int64)
-        # records of the first nblk_full blocks + take_last records of the next block
-        nrec = int(nr[:nblk_full].sum().item()) + take_last
-        nb_used = nblk_full + (1 if take_last else 0)
-        counts = nr[:nb_used].clone()
+        nb_used = i1 - i0 + (1 if take_last else 0)
+        z = torch.zeros(0, dtype=torch.uint8, device=dev)
+        e = torch.zeros(0, dtype=torch.int64, device=dev)
+        if d is None or nb_used <= 0:
+            return z, z, e, e, 0
+        counts = d.nrec[i0: i0 + nb_used].to(torch.int64).clone()
         if take_last:
             counts[-1] = take_last
-        kb = d.key_base[:nb_used]
-        vb = d.val_base[:nb_used]
-        # blocks are laid out in order from record 0, so the yielded records are records 0..nrec
+        nrec = int(counts.sum().item())
+        if nrec == 0:
+            return z, z, e, e, 0
+        r0 = int(d.rec_base[i0].item())
+        kb = d.key_base[i0: i0 + nb_used]
+        vb = d.val_base[i0: i0 + nb_used]
+        k0, v0 = int(kb[0].item()), int(vb[0].item())
         blk_of = torch.repeat_interleave(torch.arange(nb_used, device=dev), counts)
         m32 = 0xFFFFFFFF
-        key_end = kb[blk_of] + (d.key_end[:nrec].to(torch.int64) & m32)
-        val_end = vb[blk_of] + (d.val_end[:nrec].to(torch.int64) & m32)
-        klen = int(key_end[-1].item()) if nrec else 0
-        vlen = int(val_end[-1].item()) if nrec else 0
-        return Scan(end, err, nrec, d.keys[:klen], d.vals[:vlen], key_end, val_end)
+        key_end = kb[blk_of] - k0 + (d.key_end[r0: r0 + nrec].to(torch.int64) & m32)
+        val_end = vb[blk_of] - v0 + (d.val_end[r0: r0 + nrec].to(torch.int64) & m32)
+        klen = int(key_end[-1].item())
+        vlen = int(val_end[-1].item())
+        return d.keys[k0: k0 + klen], d.vals[v0: v0 + vlen], key_end, val_end, nrec
+
+    def _big_frame(self, i: int):
+        """Reader::block framing of directory entry i from its index value (host, a few bytes)
+        -> (block offset, content start, content length, stored crc)"""
+        L = _lib.lib()
+        v = self.index.to_host().records(0)[i][1]
+        off = C.c_uint64(0)
+        vb = np.frombuffer(v or b"\0", np.uint8)
+        L.mtblx_varint_decode64(vb.ctypes.data_as(_lib.u8p), len(v), C.byref(off))
+        off = int(off.value)
+        head = self.file[off: off + 14].cpu().numpy()
+        if self.version == 0:
+            ll, size = 4, int.from_bytes(head[:4].tobytes(), "little")
+        else:
+            sz = C.c_uint64(0)
+            ll = int(L.mtblx_varint_decode64(head.ctypes.data_as(_lib.u8p), head.size, C.byref(sz)))
+            size = int(sz.value)
+        stored = int.from_bytes(head[ll: ll + 4].tobytes(), "little")
+        return off, off + ll + 4, size, stored
+
+    def _crc_big(self, start: int, size: int) -> int:
+        """CRC-32C of file[start, start + size) for size >= 4 GiB: the device CRC of <= 1 GiB
+        pieces, joined on the host with crc(A || B) = x^(8|B|) * crc(A) ^ crc(B) (mod P)"""
+        piece = 1 << 30
+        offs = list(range(start, start + size, piece))
+        lens = [min(piece, start + size - o) for o in offs]
+        dev = self.file.device
+        batch = codec.DeviceBatch(self.file, torch.tensor(offs, dtype=torch.int64, device=dev),
+                                  torch.tensor(lens, dtype=torch.int32, device=dev), max(lens))
+        crcs = codec.crc32c_blocks(batch)[0].cpu().numpy().view(np.uint32)
+        c = int(crcs[0])
+        for k in range(1, len(lens)):
+            c = _gf2_mul(_x8n(lens[k]), c) ^ int(crcs[k])
+        return c
+
+    def _big_block(self, i: int):
+        """Reader::block + Block::init + the scan for a block >= 4 GiB (u64 restart array,
+        src/block.rs:25-42): decoded on the device by the emitting block seek (seek_to_first).
+        -> ("ok", Emitted) | ("panic", None) | ("loop", None) | (error name, None)"""
+        from . import iterator
+        if self.compression != 0:
+            raise NotImplementedError("compressed block >= 4 GiB")
+        off, start, size, stored = self._big_frame(i)
+        if start > self.len or size > self.len - start:
+            return "panic", None
+        if self.verify and self._crc_big(start, size) != stored:
+            return "panic", None                       # assert_eq of the checksum (src/reader.rs:163)
+        em = iterator.block_seek((self.file, start, size), None, 0, small_caps=True)
+        if em.status == _lib.SEEK_ERR:
+            return "InvalidBlock", None
+        if em.status == _lib.SEEK_PANIC:
+            return "panic", None
+        if em.status == _lib.SEEK_LOOP:
+            return "loop", None
+        if em.status == _lib.SEEK_UNSUPPORTED:
+            raise NotImplementedError("a key > 64 KiB in a block >= 4 GiB")
+        return "ok", em
 
     # ------------------------------------------------------------------ point queries
     def get_batch(self, keys, stream=None):
@@ -470,34 +542,10 @@ class Reader:
 
     def _walk_range(self, i0: int, i1: int):
         """ReaderIntoIter::next over directory entries [i0, i1), each block loaded by next()
-        (an empty block ends the iteration, src/reader.rs:362-371) -> ((keys, vals, key_end,
-        val_end, nrec) on the device, end, err, stopped)"""
-        dst, bad, zerr, data, _ = self._decode_range(i0, i1)
-        n = i1 - i0
-        bst = data.status[:n].cpu().numpy()
-        bnr = data.nrec[:n].cpu().numpy().astype(np.int64)
-        end, err, full, last, stopped = END_NONE, "None", n, 0, False
-        for i in range(n):
-            if dst[i] != _lib.DIR_OK or bad[i]:
-                end, full, stopped = END_PANIC, i, True
-                break
-            if zerr[i]:
-                end, err, full, stopped = END_ERR_NEXT, "Io", i, True
-                break
-            s = int(bst[i])
-            if s == _lib.ST_INVALID_BLOCK:
-                end, err, full, stopped = END_ERR_NEXT, "InvalidBlock", i, True
-                break
-            if s == _lib.ST_UNSUPPORTED:
-                raise NotImplementedError("block >= 4 GiB")
-            if s == _lib.ST_OK and bnr[i] == 0:
-                full, stopped = i, True
-                break
-            if s in (_lib.ST_CORRUPT, _lib.ST_LOOP):
-                end = END_PANIC if s == _lib.ST_CORRUPT else END_LOOP
-                full, last, stopped = i, int(bnr[i]), True
-                break
-        sc = self._cut_data(data, full, last, end, err)
+        -> ((keys, vals, key_end, val_end, nrec) on the device, end, err, stopped)"""
+        from . import iterator
+        parts, end, err, stopped = self._walk_blocks(i0, i1, first_exempt=False)
+        sc = iterator._assemble(parts, end, err, self.file.device)
         return (sc.keys, sc.vals, sc.key_end, sc.val_end, sc.nrec), end, err, stopped
 
     def _host_blocks(self, i0: int, i1: int):
@@ -508,6 +556,17 @@ class Reader:
         out = []
         for i in range(i1 - i0):
             content = (base, int(boff[i]), int(blen[i]))
+            if dst[i] == _lib.DIR_UNSUPPORTED:   # content >= 4 GiB
+                kind, em = self._big_block(i0 + i)
+                if kind == "ok":
+                    out.append(((self.file, self._big_frame(i0 + i)[1], self._big_frame(i0 + i)[2]),
+                                em.host_records(), em.end))
+                elif kind in ("panic", "loop"):
+                    out.append(ReferencePanic("Reader::block / BlockIter") if kind == "panic"
+                               else ReferenceLoop("BlockIter::next"))
+                else:
+                    out.append(MtblError(6))
+                continue
             if dst[i] != _lib.DIR_OK or bad[i]:
                 out.append(ReferencePanic("Reader::block"))
                 continue
@@ -523,3 +582,27 @@ class Reader:
                 end = {_lib.ST_CORRUPT: _lib.EMIT_PANIC, _lib.ST_LOOP: _lib.EMIT_LOOP}.get(s, _lib.EMIT_END)
                 out.append((content, h.records(i), end))
         return out
+
+
+# GF(2) arithmetic of CRC-32C (reflected, x^0 = bit 31) for joining piece checksums
+_POLY = 0x82F63B78
+
+
+def _gf2_mul(a: int, b: int) -> int:
+    p = 0
+    for i in range(32):
+        if a & (0x80000000 >> i):
+            p ^= b
+        b = (b >> 1) ^ _POLY if b & 1 else b >> 1
+    return p
+
+
+def _x8n(n: int) -> int:
+    """x^(8 n) mod P"""
+    r, sq, e = 0x80000000, 0x80000000 >> 8, n   # sq = x^8
+    while e:
+        if e & 1:
+            r = _gf2_mul(sq, r)
+        sq = _gf2_mul(sq, sq)
+        e >>= 1
+    return r

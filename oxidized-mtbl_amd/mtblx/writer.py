@@ -117,8 +117,11 @@ class Writer:
         rc = L.mtblx_writer_finish(self._w, C.byref(out), C.byref(n))
         if rc != 0:
             raise RuntimeError(f"mtblx_writer_finish: {rc}")
-        data = C.string_at(out, n.value)
+        arr = np.empty(n.value, np.uint8)   # (ctypes.string_at takes a C int size: no files >= 2 GiB)
+        C.memmove(arr.ctypes.data, out, n.value)
         L.mtblx_free(out)
+        data = arr.tobytes()
+        del arr
         nb = int(L.mtblx_writer_block_count(self._w))
         off = np.zeros(max(nb, 1), np.uint64)
         ln = np.zeros(max(nb, 1), np.uint32)

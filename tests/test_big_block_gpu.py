@@ -1,0 +1,73 @@
+"""Blocks >= 4 GiB (Block::init's u64 restart array, src/block.rs:25-42,
+restart_point's 4-byte stride on it, :95-104; BlockBuilder::finish switches to u64 restarts past
+u32::MAX, src/block_builder.rs:85-97).  A ~4.3 GiB block written by the product Writer (block size
+4 GiB: three small records, two ~2 GiB values, then a second, small block) read by the device
+Reader -- the big block framed from its index entry, checksummed in 1 GiB pieces, decoded by the
+emitting block seek -- against the oracle's restatement; Reader::get into it."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _file():
+    from mtblx.writer import Writer
+    vlen = (1 << 31) + 4099
+    pat = np.tile(np.arange(256, dtype=np.uint8), vlen // 256 + 1)[:vlen]
+    v1 = pat.tobytes()
+    v2 = (pat * np.uint8(7) + np.uint8(3)).tobytes()
+    del pat
+    v3 = bytes(range(256)) * (200 << 12)   # 200 MiB
+    recs = [(b"a0", b"x"), (b"a1", b"yy"), (b"a2", b""), (b"b", v1), (b"c", v2), (b"d", b"small"), (b"e", v3),
+            (b"f", b"tail")]
+    # Writer::insert flushes before a record when the estimate + the record reaches the block
+    # size (src/writer.rs:125-130): 4.4e9 keeps b, c, d in one block (> u32::MAX bytes: u64
+    # restarts) and starts a second, ordinary block at e
+    w = Writer(4_400_000_000, 16)
+    for k, v in recs:
+        w.insert(k, v)
+    return w.into_inner(), recs
+
+
+def test_block_over_4gib(oracle):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if torch.cuda.get_device_properties(0).total_memory < (40 << 30):
+        pytest.skip("needs ~40 GiB of device memory")
+    import time
+    from mtblx import reader
+    t0 = time.time()
+
+    def note(msg):   # progress on stdout (a long silent GPU run reads as hung)
+        print(f"[{time.time() - t0:6.1f}s] {msg}", flush=True)
+
+    data, recs = _file()
+    note(f"file written: {len(data)} bytes")
+    nblk = None
+    for verify in (True, False):
+        exp = oracle.file_scan(data, "iter", verify=verify)
+        note(f"oracle scan (verify={verify}) done")
+        r = reader.ReaderBuilder().verify_checksums(verify).read(data)
+        off, ln, st = r._framing()
+        nblk = int(st.numel())
+        assert int(st[0].item()) == 2 and nblk == 2   # DIR_UNSUPPORTED: the big block, then a small one
+        s = r.iter()
+        assert (s.end, exp["end"]) == (reader.END_NONE, 0)
+        got = s.records()
+        assert [k for k, _ in got] == [k for k, _ in exp["records"]] == [k for k, _ in recs]
+        assert got == exp["records"]
+        note(f"device Reader (verify={verify}) bit-exact")
+        del got, exp, s, r
+        torch.cuda.empty_cache()
+    # Reader::get into the big block (device index seek -> block seek on the u64 restart array)
+    r = reader.ReaderBuilder().verify_checksums(False).read(data)
+    assert r.get(b"a1") == b"yy" and r.get(b"d") == b"small" and r.get(b"b0") is None
+    assert r.get(b"c") == recs[4][1]
+    note("get ok")
+    # a corrupted byte inside the big block: the checksum assert panics (verify on)
+    d2 = bytearray(data)
+    d2[1000] ^= 0x55
+    e2 = oracle.file_scan(bytes(d2), "iter", verify=True)
+    s2 = reader.ReaderBuilder().verify_checksums(True).read(bytes(d2)).iter()
+    assert s2.end == e2["end"] == reader.END_PANIC and s2.nrec == len(e2["records"]) == 0

@@ -38,17 +38,23 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& w, uint32_t t) {
   return (d >> (8 * (t & 3))) & 0xffu;
 }
 
-// 16 bytes starting at byte offset `a` of an LDS byte array: one unaligned ds_read_b128
-// (gfx950 runs LDS in unaligned access mode) instead of five aligned dword reads + alignbit.
-typedef uint32_t lds_v4u __attribute__((ext_vector_type(4), aligned(1)));
-typedef uint32_t __attribute__((aligned(1))) lds_u32u;
-__device__ __forceinline__ uint4 lds_win16(const uint8_t* lds, uint32_t a) {
-  const lds_v4u v = *reinterpret_cast<const lds_v4u*>(lds + a);
-  return make_uint4(v.x, v.y, v.z, v.w);
+// LDS reads at arbitrary byte offsets.  gfx950 runs LDS in unaligned access mode, but a
+// misaligned ds_read_b32 / ds_read_b128 issues at a fraction of the aligned rate (measured with
+// scripts/lds_probe.hip: ~10x and ~7.5x less throughput; a ds_read_b128 needs 16-byte
+// alignment for full rate), so both helpers read aligned dwords and join them with a funnel
+// shift: +4% on PipeSmall and PipeLarge against one misaligned ds_read_b128 / ds_read_b32.
+// `lds` is the 16-byte aligned base of a stage buffer; up to 4 bytes past the window are read.
+__device__ __forceinline__ uint4 lds_win16(const uint8_t* lds, uint32_t a) {   // bytes [a, a + 16)
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (a >> 2);
+  const uint32_t sh = (a & 3u) * 8u;
+  const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+  return make_uint4(__builtin_amdgcn_alignbit(x1, x0, sh), __builtin_amdgcn_alignbit(x2, x1, sh),
+                    __builtin_amdgcn_alignbit(x3, x2, sh), __builtin_amdgcn_alignbit(x4, x3, sh));
 }
 
-__device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t a) {
-  return *reinterpret_cast<const lds_u32u*>(lds + a);
+__device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t a) {   // bytes [a, a + 4)
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (a >> 2);
+  return __builtin_amdgcn_alignbit(w[1], w[0], (a & 3u) * 8u);
 }
 
 // byte mask selecting bytes [lo, hi) of a dword whose first byte is byte `base`

@@ -400,6 +400,265 @@ __global__ void __launch_bounds__(C::WAVES * kWave) k_snappy_blocks(const uint8_
   }
 }
 
+// ---- Small outputs (<= 4.5 KiB): four blocks per wave ----
+//
+// One wave per block leaves the tag chain to the CU's one scalar unit, shared by all 16 waves
+// (~70 scalar instructions per element: profiles/r02/snappy).  Here a wave decodes FOUR blocks
+// at once, one per 16-lane group: the parse state is group-uniform and lives in VGPRs, so one
+// vector instruction advances four chains, and the 16 lanes of a group then write the element
+// (4 bytes per lane, 64 per step) straight into the group's LDS output -- element by element,
+// so an overlapping copy reads only bytes written before it (its period pattern), and no
+// parking or run flushes are needed.  The four blocks of a wave start and end together (a
+// "quad"); the next quad's stored bytes and the one after's offsets are loaded into VGPRs
+// while the current quad decodes, so a quad switch waits on nothing recent.
+namespace quad {
+constexpr int G = 16, NG = kWave / G;
+constexpr int WIN = 4752;               // stored bytes staged per block (>= 4736 from position 0)
+constexpr int OUT = 4608;
+constexpr int NCH = WIN / 16;           // 16-byte chunks per window
+constexpr int NPF = (NCH + G - 1) / G;  // chunks per lane
+constexpr int WG_PER_CU = 4;
+
+struct alignas(16) Blk {
+  uint8_t win[WIN + 16];   // stored bytes at block positions [wbase, wbase + WIN); 16 B slack
+  uint8_t out[OUT + 16];
+};
+constexpr uint32_t kOutOff = WIN + 16;   // Blk::out - Blk::win
+
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
+
+struct Meta {
+  const uint8_t* s;
+  uint8_t* dg;
+  uint32_t n, cap;
+};
+
+__device__ __forceinline__ Meta load_meta(uint32_t b, uint32_t nblk, const uint8_t* src, const uint64_t* src_off,
+                                          const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                          const uint32_t* dst_len) {
+  Meta m{src, dst, 0u, 0u};
+  if (b < nblk) {
+    m.s = src + src_off[b];
+    m.n = src_len[b];
+    m.dg = dst + dst_off[b];
+    m.cap = dst_len[b];
+  }
+  return m;
+}
+
+// the window of a block: its stored bytes from the 16-byte address at or below position 0
+// (wbase = -misalignment), chunk c = lane l + 16 k; bytes past the stream read as 0.  Whole
+// chunks are 16-byte loads; the two partial ones (head, tail) one byte per lane.
+struct Win {
+  uint4 v[NPF];
+  uint32_t hb, tb, ct;   // head chunk byte l, tail chunk ct's byte l
+  __device__ __forceinline__ void load(const Meta& m, bool on, int l) {
+    const int32_t wb = -(int32_t)((uintptr_t)m.s & 15u), n = on ? (int32_t)m.n : 0;
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int32_t c = l + G * k, bp = wb + 16 * c;
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (c < NCH && bp >= 0 && bp + 16 <= n) v[k] = *reinterpret_cast<const uint4*>(m.s + bp);
+    }
+    const int32_t ph = wb + l;
+    hb = (ph >= 0 && ph < n) ? m.s[ph] : 0u;
+    ct = n > 0 ? (uint32_t)(n - 1 - wb) / 16u : 0u;
+    const int32_t pt = wb + 16 * (int32_t)ct + l;
+    tb = (ct < (uint32_t)NCH && pt >= 0 && pt < n) ? m.s[pt] : 0u;
+  }
+  __device__ __forceinline__ void store(uint8_t* win, int l) const {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int c = l + G * k;
+      if (c < NCH) *reinterpret_cast<uint4*>(win + 16 * c) = v[k];
+    }
+    win[l] = (uint8_t)hb;
+    if (ct < (uint32_t)NCH) win[16 * ct + l] = (uint8_t)tb;
+  }
+};
+
+// j mod off for j < 2^20, off >= 1: float quotient (rcp within an ulp), one correction each way
+__device__ __forceinline__ uint32_t umod(uint32_t j, uint32_t off, float rcp) {
+  const int32_t q = (int32_t)((float)j * rcp);
+  int32_t r = (int32_t)j - q * (int32_t)off;
+  r = r < 0 ? r + (int32_t)off : r;
+  r = r >= (int32_t)off ? r - (int32_t)off : r;
+  return (uint32_t)r;
+}
+
+__global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, const uint64_t* src_off,
+                                                        const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                        const uint64_t* dst_off, const uint32_t* dst_len,
+                                                        uint32_t max_out, int32_t* status, uint32_t* dec_len) {
+  __shared__ Blk S[NG];
+  const int lane = threadIdx.x, g = lane >> 4, l = lane & 15;
+  Blk& B = S[g];
+  uint8_t* base = B.win;   // LDS offsets below are relative to B.win (B.out = base + kOutOff)
+  const uint32_t nquad = (nblk + NG - 1) / NG, qstride = gridDim.x;
+  uint32_t q = blockIdx.x;
+  if (q >= nquad) return;
+  const uint32_t cap_lds = min(max_out, (uint32_t)OUT);
+  auto blk_of = [&](uint32_t qq) { return qq * NG + (uint32_t)g; };
+  auto meta = [&](uint32_t qq) {
+    return load_meta(qq < nquad ? blk_of(qq) : nblk, nblk, src, src_off, src_len, dst, dst_off, dst_len);
+  };
+  // prologue: quad q's window into LDS, q+1's window and q+2's offsets in flight
+  Meta cur = meta(q), m1 = meta(q + qstride);
+  Win pf;
+  pf.load(cur, blk_of(q) < nblk, l);
+  pf.store(base, l);
+  pf.load(m1, q + qstride < nquad && blk_of(q + qstride) < nblk, l);
+  Meta m2 = meta(q + 2 * qstride);
+
+  for (;;) {
+    const uint32_t b = blk_of(q);
+    const bool on = b < nblk;
+    const uint8_t* s = cur.s;
+    const uint32_t n = cur.n;
+    const int32_t wb = -(int32_t)((uintptr_t)s & 15u);
+    const uint32_t wend = (uint32_t)(wb + WIN);   // block positions [.., wend) are in the window
+    // 8 stored bytes at position p (p < n): LDS when they are staged (or the stream ends inside
+    // the window: bytes past n are never used), else from HBM byte by byte
+    auto hdr8 = [&](uint32_t p, uint32_t& lo, uint32_t& hi) {
+      if (p + 8u <= wend || n <= wend) {
+        const v2u x = *reinterpret_cast<const v2u*>(base + (p - (uint32_t)wb));
+        lo = x.x;
+        hi = x.y;
+      } else {
+        uint64_t x = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+          if (p + t < n) x |= (uint64_t)s[p + t] << (8 * t);
+        lo = (uint32_t)x;
+        hi = (uint32_t)(x >> 32);
+      }
+    };
+    // ---- preamble ----
+    uint32_t lo = 0, hi = 0, pos = 0, W = 0, d = 0;
+    int32_t st = MTBLX_SNAPPY_OK;
+    if (on) {
+      if (n) hdr8(0, lo, hi);
+      uint64_t want = 0;
+      bool term = false;
+      for (uint32_t i = 0; i < 5 && i < n; ++i) {
+        const uint32_t byte = (i < 4 ? lo >> (8 * i) : hi) & 0xffu;
+        want |= (uint64_t)(byte & 0x7fu) << (7 * i);
+        if (!(byte & 0x80u)) {
+          term = true;
+          pos = i + 1;
+          break;
+        }
+      }
+      if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
+      else if (want > cur.cap || want > cap_lds) st = MTBLX_SNAPPY_TOO_SMALL;
+      W = (uint32_t)want;
+    }
+    // ---- elements: decode one per group, then the groups write them together ----
+    // Software-pipelined: the next element's 8 header bytes are read before this element's
+    // bytes are written, so the two LDS round trips overlap; the decode is select-based (all
+    // three tag kinds computed, one picked) so the four groups do not split into branches.
+    bool work = on && st == MTBLX_SNAPPY_OK && pos < n;
+    if (work) hdr8(pos, lo, hi);
+    while (__ballot(work)) {
+      const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2, avail = n - pos - 1u;
+      const uint32_t raw = (lo >> 8) | (hi << 24);   // the 4 bytes after the tag
+      // literal: len-1 = t2 (< 60) or the next nb = t2 - 59 bytes
+      const bool lg = t2 >= 60u;
+      const uint32_t nb = t2 - 59u;
+      const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * (nb & 3u))) - 1u);
+      const uint32_t llit = lg ? ext + 1u : t2 + 1u, hlit = lg ? 1u + nb : 1u;
+      const bool lbad = lg && (avail < nb || ext == 0xFFFFFFFFu);
+      // copies: copy-1 (1 extra byte), copy-2 (2), copy-4 (4)
+      const uint32_t lc = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
+      const uint32_t off = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
+      const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
+      const bool lit = kind == 0u;
+      const uint32_t L0 = lit ? llit : lc, hl = lit ? hlit : need + 1u, sp = pos + hl;
+      bool bad = lit ? (lbad || n - sp < L0) : (avail < need || off == 0u || off > d);
+      bad = bad || W - d < L0;
+      const bool hbm = lit && sp + L0 > wend;   // literal bytes not staged: read from HBM
+      const uint32_t so = lit ? (hbm ? sp : sp - (uint32_t)wb) : kOutOff + d - off;
+      const uint32_t P = (!lit && off < L0) ? off : 0xFFFFFFFFu;   // overlapping copy: period off
+      const float rcp = __builtin_amdgcn_rcpf((float)(P & 0xffffu));
+      uint32_t L = 0;
+      if (work) {
+        if (bad) {
+          st = MTBLX_SNAPPY_CORRUPT;
+        } else {
+          L = L0;
+          pos = lit ? sp + L0 : sp;
+        }
+      }
+      const bool go = work && !bad;
+      work = go && pos < n;
+      if (work) hdr8(pos, lo, hi);   // next element's header, in flight during the writes below
+      // write the element: lane l covers bytes [4 l, 4 l + 4) of each 64-byte step (bytes past
+      // L land in the next element's space and are overwritten before anything reads them).
+      // The dword accesses are misaligned: gfx950 runs those well below the aligned rate, but
+      // this loop moves few bytes per cycle and is latency-bound -- aligned reads + a funnel
+      // shift and aligned writes with a bytewise lead measured slower (77 -> 59 GB/s).
+      for (uint32_t s0 = 0; __ballot(s0 < L); s0 += 4u * G) {
+        const uint32_t j = s0 + 4u * (uint32_t)l;
+        if (j < L) {
+          uint32_t v;
+          if (!hbm) {
+            uint32_t r = P == 0xFFFFFFFFu ? j : umod(j, P, rcp);
+            if (r + 4u <= P) {
+              v = *reinterpret_cast<const u32u*>(base + so + r);
+            } else {
+              v = 0;
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                v |= (uint32_t)base[so + r] << (8 * t);
+                r = r + 1u == P ? 0u : r + 1u;
+              }
+            }
+          } else {
+            v = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t)
+              if (j + t < L) v |= (uint32_t)s[so + j + t] << (8 * t);
+          }
+          *reinterpret_cast<u32u*>(base + kOutOff + d + j) = v;
+        }
+      }
+      d += L;
+    }
+    if (on && st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
+
+    // ---- quad switch: next window into LDS, this quad's output to HBM, loads for later quads ----
+    const uint32_t qn = q + qstride;
+    const bool more = qn < nquad;   // wave-uniform
+    const bool emit = on && st == MTBLX_SNAPPY_OK;
+    if (emit) {
+      if (((uintptr_t)cur.dg & 15u) == 0) {
+        const uint32_t n16 = W / 16u;
+        for (uint32_t c = (uint32_t)l; c < n16; c += G)
+          reinterpret_cast<uint4*>(cur.dg)[c] = *reinterpret_cast<const uint4*>(B.out + 16 * c);
+        const uint32_t tb = 16u * n16 + (uint32_t)l;
+        if (tb < W) cur.dg[tb] = B.out[tb];
+      } else {
+#pragma unroll 1
+        for (uint32_t j = (uint32_t)l; j < W; j += G) cur.dg[j] = B.out[j];
+      }
+    }
+    if (more) pf.store(base, l);
+    if (on && l == 0) {
+      status[b] = st;
+      if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
+    }
+    if (!more) break;
+    q = qn;
+    cur = m1;
+    m1 = m2;
+    const uint32_t q1 = q + qstride;
+    pf.load(m1, q1 < nquad && blk_of(q1) < nblk, l);
+    m2 = meta(q + 2 * qstride);
+  }
+}
+}  // namespace quad
+
 // ---- directory: preamble lengths, 16-byte aligned exclusive prefix ----
 constexpr int kDirThreads = 256, kDirPer = 8, kDirSpan = kDirThreads * kDirPer;
 
@@ -539,9 +798,9 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   if (nblk == 0) return MTBLX_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !dst_len || !status) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (max_dst_len != 0 && max_dst_len <= (uint32_t)Small::OUT) {
-    hipLaunchKernelGGL(k_snappy_blocks<Small>, dim3(grid_for(4, (nblk + Small::WAVES - 1) / Small::WAVES)),
-                       dim3(Small::WAVES * kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, status,
+  if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
+    hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
+                       dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len);
   } else {
     hipLaunchKernelGGL(k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,

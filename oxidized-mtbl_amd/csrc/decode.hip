@@ -1145,7 +1145,10 @@ struct PipeCfg {
 // (PipeLarge with four loaders and ten copy waves: +0.8 % on 16 B keys, -16 % on cfg3's long
 // Zipf keys, whose copy is the longer half of the iteration)
 using PipeSmall = PipeCfg<49152, 3, 16, 56>;   // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
-using PipeLarge = PipeCfg<65664, 2, 2, 64>;    // blocks up to ~64 KiB (cfg3, cfg4 64 KiB)
+#ifndef MTBLX_LARGE_LOADW
+#define MTBLX_LARGE_LOADW 2
+#endif
+using PipeLarge = PipeCfg<65664, 2, 2, 64, false, MTBLX_LARGE_LOADW>;    // blocks up to ~64 KiB (cfg3, cfg4 64 KiB)
 using PipeSmallV = PipeCfg<49152, 3, 16, 56, true>;
 using PipeLargeV = PipeCfg<65664, 2, 2, 64, true>;
 
@@ -1975,9 +1978,20 @@ __device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, 
   }
 }
 
+#ifdef MTBLX_LARGE_SERIAL
+constexpr bool kLargeSerial = true;   // A/B: the round-2 two-buffer schedule for PipeLarge
+#else
+constexpr bool kLargeSerial = false;
+#endif
+
 template <class P>
 __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   __shared__ PipeLds<P> S;
+  // Two buffers, serial: tile it is walked, looked back and copied in iteration it while the
+  // loaders stage tile it+1 (PipeLargeV: its fused CRC reads the tile being copied).  Otherwise
+  // the three-stage schedule: walk it+1 | look-back + copy it | DMA it+2 -- with two buffers
+  // the DMA of tile it+2 goes into tile it's buffer once the copy waves have left it.
+  constexpr bool serial2 = P::NBUF == 2 && (P::VERIFY || kLargeSerial);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t g = blockIdx.x, G = gridDim.x;
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
@@ -2013,16 +2027,14 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     load_info(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (wv == 1) {
-    if (P::NBUF == 3 && nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
+    if (!serial2 && nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
   }
   __syncthreads();
   TL(1);
   if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
   uint64_t ntl = 0;
 
-  if constexpr (P::NBUF == 2) {
-    // two buffers: tile it is walked, looked back and copied in iteration it while the
-    // loaders stage tile it+1 into the other buffer
+  if constexpr (serial2) {
     for (uint32_t it = 0; it < nloc; ++it) {
       PipeBuf<P>& C = S.buf[it & 1u];
       const uint32_t tc = g + it * G;
@@ -2081,6 +2093,10 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       ST.hit(3);
     } else if (loader) {
       if (k2 < nloc) {
+        if constexpr (P::NBUF == 2) {
+          // tile it+2 goes into tile it's buffer: wait until every copy wave has left it
+          if (it >= 0) wait_flag(a, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
+        }
         pipe_dma(S.buf[k2 % P::NBUF], a, g + k2 * G, ioff, ilen, lane, part);
         load_info(k2 + 1);
       }

@@ -1823,7 +1823,7 @@ __device__ __forceinline__ void wait_flag(const TileArgs& a, const uint32_t* fla
 
 template <class P>
 __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a, int cw, int lane, const uint32_t* ready,
-                                          uint32_t want, Stamps& ST) {
+                                          uint32_t want, Stamps& ST, uint32_t rows = P::ROWS) {
   const uint32_t nint = B.nint, nb = B.nb;
   uint32_t fb = (uint32_t)cw * (kWave / 16);
   if (fb < nint) {
@@ -1832,7 +1832,7 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
     wait_flag(a, ready, want);
     ST.hit(0);
     if (a.write) copy_emit(B, a, r, lane);
-    for (fb += P::ROWS; fb < nint; fb += P::ROWS) {   // wave-uniform
+    for (fb += rows; fb < nint; fb += rows) {   // wave-uniform
       const CopyRow r2 = copy_prepare(B, fb, lane);
       if (a.write) copy_emit(B, a, r2, lane);
     }
@@ -1992,6 +1992,12 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   // the three-stage schedule: walk it+1 | look-back + copy it | DMA it+2 -- with two buffers
   // the DMA of tile it+2 goes into tile it's buffer once the copy waves have left it.
   constexpr bool serial2 = P::NBUF == 2 && (P::VERIFY || kLargeSerial);
+  // Two buffers, three stages: the loaders have nothing to do until the copy waves leave tile
+  // it's buffer, so they copy too (as copy waves NCOPY ..): 56 rows per pass, so a 64 KiB block
+  // (~53 restart intervals) takes one pass instead of 48 + 5.
+  constexpr bool kLoadCopy = P::NBUF == 2 && !serial2;
+  constexpr uint32_t kCopyW = P::NCOPY + (kLoadCopy ? P::LOADW : 0);   // waves that copy a tile
+  constexpr uint32_t kRows = kCopyW * (kWave / 16);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t g = blockIdx.x, G = gridDim.x;
   const uint32_t nloc = (a.ntiles > g) ? (a.ntiles - g + G - 1) / G : 0;  // tiles of this workgroup
@@ -2092,10 +2098,16 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       }
       ST.hit(3);
     } else if (loader) {
+      if constexpr (kLoadCopy) {
+        if (it >= 0) {
+          pipe_copy(S.buf[(uint32_t)it % P::NBUF], a, P::NCOPY + (int)part, lane, &S.ready, (uint32_t)it + 1, ST, kRows);
+          if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
       if (k2 < nloc) {
         if constexpr (P::NBUF == 2) {
           // tile it+2 goes into tile it's buffer: wait until every copy wave has left it
-          if (it >= 0) wait_flag(a, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
+          if (it >= 0) wait_flag(a, &S.cdone, (uint32_t)(it + 1) * kCopyW);
         }
         pipe_dma(S.buf[k2 % P::NBUF], a, g + k2 * G, ioff, ilen, lane, part);
         load_info(k2 + 1);
@@ -2125,11 +2137,11 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
             if (wb.expired()) { ws_flag(a, 2ull); break; }
           }
           pipe_lookback_issue(a, tc + G, G, lbv, lane);
-          pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * P::NCOPY);
+          pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kCopyW);
         }
         ST.hit(1);
       } else {
-        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST);
+        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST, kRows);
         if (wv == P::COPY0 && it + 1 == (int)nloc) TLW(9);   // first copy wave: last tile's stores issued
         if (wv == P::COPY0 + P::NCOPY - 1 && it + 1 == (int)nloc) TLW(10);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

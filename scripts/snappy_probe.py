@@ -47,8 +47,12 @@ def main():
     st = torch.zeros(zb.nblk, dtype=torch.int32, device="cuda")
     dl = torch.zeros(zb.nblk, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
-    for _ in range(3):
-        codec.snappy_decompress_into(zb, lay, dst, st, dl, int(tot[1]), s)
+    # ~40 ms of untimed launches first: the GPU drops its clocks when idle (bench.py _preload)
+    t_pre = time.perf_counter()
+    while time.perf_counter() - t_pre < 0.04:
+        for _ in range(5):
+            codec.snappy_decompress_into(zb, lay, dst, st, dl, int(tot[1]), s)
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(a.reps):

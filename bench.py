@@ -653,6 +653,9 @@ def main():
     if not args.no_crc:
         with torch.cuda.stream(stream):
             crc, bad = codec.crc32c_blocks(batch, framed=True, stream=stream)
+        torch.cuda.synchronize()
+        _preload(lambda: codec.crc32c_blocks(batch, framed=True, stream=stream), stream, args.preload_ms)
+        with torch.cuda.stream(stream):
             c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             c0.record(stream)
             for _ in range(10):
@@ -672,6 +675,9 @@ def main():
             raise RuntimeError(f"fused verify decode mismatch: {hv}")
         # the default mtblx_decode_blocks_verify: the decode, then k_crc32c_blocks, one stream
         vbad.zero_()
+        torch.cuda.synchronize()
+        _preload(lambda: codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=False), stream,
+                 args.preload_ms)
         with torch.cuda.stream(stream):
             for _ in range(3):
                 codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=False)

@@ -6,6 +6,8 @@
 // LDS so every global load instruction reads 1 KiB contiguous; each window's raw CRC
 // (slicing-by-8) is shifted into place with a GF(2) multiply by x^(512 k) mod P:
 //   crc_raw(A || B) = multmodp(x^(8|B|), crc_raw(A)) ^ crc_raw(B)
+// through nibble tables of the constants x^(512 k) (crc_dev.h MulTabs: 8 lookups instead of a
+// 32-step bitwise multiply, which was ~190 of ~510 vector instructions per 4 KiB block)
 // and the wave XOR-reduces; see k_crc32c_blocks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,7 +17,7 @@
 
 namespace mtblx_crc {
 
-constexpr int kCrcThreads = 256;   // 4 waves per workgroup
+constexpr int kCrcThreads = 1024;   // 16 waves per workgroup, 2 workgroups per CU (LDS: 48 KiB each)
 
 // Slicing-by-8 tables: T8[k][i] = CRC of byte i followed by k zero bytes.
 struct Slice8 {
@@ -75,9 +77,13 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
                                                                uint32_t nblk, uint32_t* crc_out, uint8_t* bad,
                                                                int framed) {
   __shared__ Slice8 S;
-  __shared__ uint32_t XP[kWave];   // x^(512 k), k < 64
+  __shared__ MulLds M;   // window shifts x^(512 k) as nibble tables
   for (int i = threadIdx.x; i < 4 * 256; i += kCrcThreads) S.t[i >> 8][i & 255] = kTab.slice[i >> 8][i & 255];
-  for (int i = threadIdx.x; i < kWave; i += kCrcThreads) XP[i] = kTab.x0[i];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&kMul);
+    uint4* dst = reinterpret_cast<uint4*>(&M);
+    for (int i = threadIdx.x; i < (int)(sizeof(MulLds) / 16); i += kCrcThreads) dst[i] = src[i];
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < 4 * 256; i += kCrcThreads) {   // tables 4..7 from table 3
     uint32_t t = S.t[3][i & 255];
@@ -99,7 +105,9 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
         const int64_t hi = (int64_t)(L - k * kChunk);
         const bool safe = (int64_t)off + hi - kChunk >= 0;
         const uint32_t c = window_crc(d, hi, S.t, safe);
-        acc ^= dmultmodp(k < (uint64_t)kWave ? XP[k] : xpow512(k), c);
+        if (k < 64) acc ^= mul_nib(c, M.a[k]);
+        else if (k < 1024) acc ^= mul_nib(mul_nib(c, M.a[k & 63]), M.b[k >> 6]);
+        else acc ^= dmultmodp(xpow512(k), c);
       }
 #pragma unroll
       for (int sh = 32; sh >= 1; sh >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, sh, kWave);
@@ -133,9 +141,9 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = (ncu > 0 ? ncu : 256) * 8;   // 32 waves per CU
+    grid = (ncu > 0 ? ncu : 256) * 2;   // 32 waves per CU
   }
-  const uint32_t need = (in->nblk + 3u) / 4u;
+  const uint32_t need = (in->nblk + 15u) / 16u;
   hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, dim3(need < (uint32_t)grid ? need : (uint32_t)grid),
                      dim3(mtblx_crc::kCrcThreads), 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
                      in->blk_off, in->blk_len, in->nblk, crc, bad, framed);

@@ -68,6 +68,59 @@ struct Tables {
 
 static __constant__ Tables kTab = Tables();
 
+// Multiplication by the constants x^(512 k) through nibble tables: multmodp(c, K) is linear in
+// c, so it is the XOR over c's eight nibbles of a[k][j][nibble j] = multmodp(nibble << 4j, K).
+// a: K = x^(512 k), k < 64 (the windows of a 4 KiB block); b: K = x^(32768 m), m < 16 (with a,
+// every window of a block up to 512 KiB).  Built from K·x^i, i < 32 (bit 31 - i of c is x^i).
+struct MulTabs {
+  uint32_t a[64][8][16];
+  uint32_t b[16][8][16];
+  static constexpr uint32_t mulx(uint32_t v) { return (v & 1u) ? (v >> 1) ^ kPoly : v >> 1; }
+  static constexpr void fill(uint32_t (&t)[8][16], uint32_t K) {
+    uint32_t base[32] = {};
+    base[0] = K;
+    for (int i = 1; i < 32; ++i) base[i] = mulx(base[i - 1]);
+    for (int j = 0; j < 8; ++j)
+      for (uint32_t v = 0; v < 16; ++v) {
+        uint32_t p = 0;
+        for (int u = 0; u < 4; ++u)
+          if ((v >> u) & 1u) p ^= base[31 - 4 * j - u];
+        t[j][v] = p;
+      }
+  }
+  constexpr MulTabs() : a(), b() {
+    uint32_t x512 = 0x80000000u;   // x^0 -> x^512: 512 single-bit shifts
+    for (int i = 0; i < 512; ++i) x512 = mulx(x512);
+    uint32_t K = 0x80000000u;
+    for (int k = 0; k < 64; ++k) {
+      fill(a[k], K);
+      K = multmodp(x512, K);
+    }
+    // K = x^(512 * 64) = x^32768 now
+    const uint32_t x32768 = K;
+    uint32_t M = 0x80000000u;
+    for (int m = 0; m < 16; ++m) {
+      fill(b[m], M);
+      M = multmodp(x32768, M);
+    }
+  }
+};
+
+static __constant__ MulTabs kMul = MulTabs();
+struct MulLds {   // the same layout, trivially constructible (an LDS copy of kMul)
+  uint32_t a[64][8][16];
+  uint32_t b[16][8][16];
+};
+static_assert(sizeof(MulLds) == sizeof(MulTabs), "MulLds mirrors MulTabs");
+
+// c * K through one [8][16] nibble table (LDS)
+__device__ __forceinline__ uint32_t mul_nib(uint32_t c, const uint32_t (*T)[16]) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p ^= T[j][(c >> (4 * j)) & 15u];
+  return p;
+}
+
 __device__ __forceinline__ uint32_t dmultmodp(uint32_t a, uint32_t b) {
   uint32_t p = 0;
 #pragma unroll

@@ -2,11 +2,10 @@
 // before it decodes a block (/root/reference/src/reader.rs:159-164, crate crc32c 0.4:
 // CRC-32C Castagnoli, reflected polynomial 0x82F63B78, init/xorout 0xFFFFFFFF).
 //
-// One wave per block: 64-byte windows counted from the block's END, one per lane, staged through
-// LDS so every global load instruction reads 1 KiB contiguous; each window's raw CRC
-// (slicing-by-8) is shifted into place with a GF(2) multiply by x^(512 k) mod P:
+// One wave per block: 72-byte windows counted from the block's END, one per lane; each window's
+// raw CRC (slicing-by-8) is shifted into place with a GF(2) multiply by x^(576 k) mod P:
 //   crc_raw(A || B) = multmodp(x^(8|B|), crc_raw(A)) ^ crc_raw(B)
-// through nibble tables of the constants x^(512 k) (crc_dev.h MulTabs: 8 lookups instead of a
+// through nibble tables of the constants x^(576 k) (crc_dev.h MulTabs: 8 lookups instead of a
 // 32-step bitwise multiply, which was ~190 of ~510 vector instructions per 4 KiB block)
 // and the wave XOR-reduces; see k_crc32c_blocks.
 #include <hip/hip_runtime.h>
@@ -24,21 +23,25 @@ struct Slice8 {
   uint32_t t[8][256];
 };
 
-// raw CRC (init 0) of the 64-byte window ending at block position hi: bytes before the block
-// start (positions < 0) count as zeros, which leave a zero-init CRC unchanged; the 0xFFFFFFFF
-// init is folded into block bytes 0..3.  16 words -> 8 slicing-by-8 steps.
+// raw CRC (init 0) of the kCrcWin-byte window ending at block position hi: bytes before the
+// block start (positions < 0) count as zeros, which leave a zero-init CRC unchanged; the
+// 0xFFFFFFFF init is folded into block bytes 0..3.  18 words -> 9 slicing-by-8 steps.
+constexpr int kWords = kCrcWin / 4;
 __device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, const uint32_t (*T)[256], bool safe) {
-  const int64_t lo = hi - kChunk;
-  uint32_t w[16];
+  const int64_t lo = hi - kCrcWin;
+  uint32_t w[kWords];
   if (safe) {   // d + lo is readable (inside the buffer) even where lo < 0
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
       w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
     }
+    typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
+    const v2u y = *reinterpret_cast<const v2u*>(d + lo + 64);
+    w[16] = y.x; w[17] = y.y;
   } else {      // the window starts before the buffer: byte loads of the in-block part only
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
+    for (int m = 0; m < kWords; ++m) {
       uint32_t v = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -50,7 +53,7 @@ __device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, con
   }
   if (lo < 4) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
+    for (int m = 0; m < kWords; ++m) {
       const int64_t pos = lo + 4 * m;   // block position of the word's first byte
       if (pos < 4) {
         const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
@@ -61,7 +64,7 @@ __device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, con
   }
   uint32_t c = 0;
 #pragma unroll
-  for (int m = 0; m < 16; m += 2) {
+  for (int m = 0; m < kWords; m += 2) {
     const uint32_t x = c ^ w[m], y = w[m + 1];
     c = T[7][x & 0xFFu] ^ T[6][(x >> 8) & 0xFFu] ^ T[5][(x >> 16) & 0xFFu] ^ T[4][x >> 24] ^
         T[3][y & 0xFFu] ^ T[2][(y >> 8) & 0xFFu] ^ T[1][(y >> 16) & 0xFFu] ^ T[0][y >> 24];
@@ -69,15 +72,15 @@ __device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, con
   return c;
 }
 
-// One wave per block: lane j takes the 64-byte windows j, j + 64, ... counted from the block's
-// END (window k = block bytes [L - 64 (k + 1), L - 64 k)), each a raw CRC shifted into place
-// by x^(512 k) (a GF(2) multiply; k < 64 from an LDS table), XOR-reduced over the wave.
+// One wave per block: lane j takes the kCrcWin-byte windows j, j + 64, ... counted from the
+// block's END (window k = block bytes [L - W (k + 1), L - W k)), each a raw CRC shifted into
+// place by x^(8 W k) (nibble tables in LDS), XOR-reduced over the wave.
 __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* data, uint64_t data_len,
                                                                const uint64_t* blk_off, const uint32_t* blk_len,
                                                                uint32_t nblk, uint32_t* crc_out, uint8_t* bad,
                                                                int framed) {
   __shared__ Slice8 S;
-  __shared__ MulLds M;   // window shifts x^(512 k) as nibble tables
+  __shared__ MulLds M;   // window shifts x^(576 k) as nibble tables
   for (int i = threadIdx.x; i < 4 * 256; i += kCrcThreads) S.t[i >> 8][i & 255] = kTab.slice[i >> 8][i & 255];
   {
     const uint4* src = reinterpret_cast<const uint4*>(&kMul);
@@ -100,20 +103,20 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
     // a window past the buffer: the reference's slice panics before the checksum (bad = 1)
     const bool oob = off + L > data_len;
     uint32_t acc = 0;
-    if (!oob && L >= (uint64_t)kChunk) {
-      for (uint64_t k = lane; k * kChunk < L; k += kWave) {
-        const int64_t hi = (int64_t)(L - k * kChunk);
-        const bool safe = (int64_t)off + hi - kChunk >= 0;
+    if (!oob && L >= (uint64_t)kCrcWin) {
+      for (uint64_t k = lane; k * kCrcWin < L; k += kWave) {
+        const int64_t hi = (int64_t)(L - k * kCrcWin);
+        const bool safe = (int64_t)off + hi - kCrcWin >= 0;
         const uint32_t c = window_crc(d, hi, S.t, safe);
         if (k < 64) acc ^= mul_nib(c, M.a[k]);
         else if (k < 1024) acc ^= mul_nib(mul_nib(c, M.a[k & 63]), M.b[k >> 6]);
-        else acc ^= dmultmodp(xpow512(k), c);
+        else acc ^= dmultmodp(xpow8(k * kCrcWin), c);
       }
 #pragma unroll
       for (int sh = 32; sh >= 1; sh >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, sh, kWave);
       acc ^= 0xFFFFFFFFu;
     } else if (!oob) {
-      acc = wave_crc32c(d, L, S.t[0], lane);   // < 64 bytes: byte-wise
+      acc = wave_crc32c(d, L, S.t[0], lane);   // < kCrcWin bytes (wave_crc32c: byte-wise under 64)
     }
     if (lane == 0) {
       if (crc_out) crc_out[b] = acc;

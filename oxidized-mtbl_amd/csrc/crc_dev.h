@@ -68,10 +68,16 @@ struct Tables {
 
 static __constant__ Tables kTab = Tables();
 
-// Multiplication by the constants x^(512 k) through nibble tables: multmodp(c, K) is linear in
-// c, so it is the XOR over c's eight nibbles of a[k][j][nibble j] = multmodp(nibble << 4j, K).
-// a: K = x^(512 k), k < 64 (the windows of a 4 KiB block); b: K = x^(32768 m), m < 16 (with a,
-// every window of a block up to 512 KiB).  Built from K·x^i, i < 32 (bit 31 - i of c is x^i).
+// Block CRC windows (crc.hip): 72 bytes, so 64 lanes cover 4608 bytes in one pass -- the
+// Writer's 4 KiB blocks run a little over 4096 bytes, which 64-byte windows would split into a
+// full pass plus one for 1-2 lanes.
+constexpr int kCrcWin = 72;
+
+// Multiplication by the constants x^(8 kCrcWin k) through nibble tables: multmodp(c, K) is
+// linear in c, so it is the XOR over c's eight nibbles of a[k][j][nibble j] =
+// multmodp(nibble << 4j, K).  a: K = x^(576 k), k < 64 (the windows of a block up to 4.5 KiB);
+// b: K = x^(576 * 64 m), m < 16 (with a, every window of a block up to 72 KiB).  Built from
+// K·x^i, i < 32 (bit 31 - i of c is x^i).
 struct MulTabs {
   uint32_t a[64][8][16];
   uint32_t b[16][8][16];
@@ -89,19 +95,19 @@ struct MulTabs {
       }
   }
   constexpr MulTabs() : a(), b() {
-    uint32_t x512 = 0x80000000u;   // x^0 -> x^512: 512 single-bit shifts
-    for (int i = 0; i < 512; ++i) x512 = mulx(x512);
+    uint32_t xw = 0x80000000u;   // x^0 -> x^(8 kCrcWin): single-bit shifts
+    for (int i = 0; i < 8 * kCrcWin; ++i) xw = mulx(xw);
     uint32_t K = 0x80000000u;
     for (int k = 0; k < 64; ++k) {
       fill(a[k], K);
-      K = multmodp(x512, K);
+      K = multmodp(xw, K);
     }
-    // K = x^(512 * 64) = x^32768 now
-    const uint32_t x32768 = K;
+    // K = x^(8 kCrcWin 64) now
+    const uint32_t xw64 = K;
     uint32_t M = 0x80000000u;
     for (int m = 0; m < 16; ++m) {
       fill(b[m], M);
-      M = multmodp(x32768, M);
+      M = multmodp(xw64, M);
     }
   }
 };

@@ -411,6 +411,14 @@ def run_cfg3(args, dist, world, rank):
             out = codec.DecodedBlocks(nb, nr, kb, vb)
             codec.decode_into(batch, out, ws, s)
             dec_ms = _timed(lambda: codec.decode_into(batch, out, ws, s), s, 5)
+        if args.stamps and ci == 0:   # diagnostic build: per-phase cycles per tile of this chunk's decode
+            torch.cuda.synchronize()
+            d = ws.buf[:128].cpu().numpy().view(np.uint64).astype(np.float64)
+            names = ["copy:wait-ready", "w1:lookback+barrier", "w0:walk-loop", "w0:scan-publish",
+                     "loader:dma-issue", "copy:barrier", "loader:dma-wait", "copy:copy", "w0:barrier",
+                     "w0:trailers", "w0:interval-setup", "w1:barrier", "loader:barrier",
+                     "copy:barrier-min-over-waves", "copy:prepare-max-over-waves"]
+            acc["phase_cycles_per_tile"] = {n: round(d[k] / max(d[15], 1), 1) for k, n in enumerate(names)}
         # round trip: every decoded record == the generated record
         r_used = int(blk[-1].item())
         ke_used = int(recs.key_end[r_used - 1].item())
@@ -456,6 +464,7 @@ def run_cfg3(args, dist, world, rank):
                    "blocks_per_gpu": acc["blocks"], "records_per_gpu": acc["records"],
                    "block_bytes_per_gpu": acc["block_bytes"], "chunks": acc["chunks"]},
         "round_trip": "bit-exact (keys, values, key END offsets of every record; all statuses OK)",
+        **({"phase_cycles_per_tile": acc["phase_cycles_per_tile"]} if "phase_cycles_per_tile" in acc else {}),
         "roofline": {"decode": {"kernel": "k_decode_pipe<PipeLarge>", "achieved_GBs":
                                 round(alg_dec / (acc["dec_ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                                 "alg_bytes": alg_dec},
@@ -895,6 +904,7 @@ def main():
             G = 1024
             tl = np.zeros((G, 16), np.uint64)
             if L.mtblx_dbg_timeline(tl.ctypes.data_as(C.POINTER(C.c_uint64)), G) == 0:
+                tl_all = tl.copy()
                 tl = tl[tl[:, 0] > 0].astype(np.int64)
                 t0 = tl[:, 0].min()
                 us = (tl[:, :6] - t0) / 100.0   # s_memrealtime ticks at 100 MHz
@@ -903,6 +913,13 @@ def main():
                         "max": round(float(us[:, k].max()), 2)}
                     for k, n in enumerate(["entry", "preload", "first_walk", "iter0", "loop_end", "exit"])}
                 res["timeline_us"]["tiles_per_wg"] = [int(tl[:, 6].min()), int(tl[:, 6].max())]
+                le = us[:, 4]
+                res["timeline_us"]["loop_end_pct"] = {q: round(float(np.percentile(le, q)), 2) for q in (10, 50, 90, 99)}
+                res["timeline_us"]["loop_end_mean_by_tiles"] = {int(n): round(float(le[tl[:, 6] == n].mean()), 2)
+                                                               for n in np.unique(tl[:, 6])}
+                wg = np.nonzero(tl_all[:, 0] > 0)[0]
+                res["timeline_us"]["loop_end_mean_by_xcd"] = [round(float(le[(wg % 8) == x].mean()), 2) for x in range(8)]
+                res["timeline_us"]["latest_wgs"] = [int(x) for x in wg[np.argsort(-le)[:8]]]
                 res["timeline_us"]["wgs"] = int(tl.shape[0])
                 ux = (tl[:, 7:16] - t0) / 100.0     # penult, last look-back, copy0 done, copyN done, penult look-back, drains
                 res["timeline_raw"] = [[round(float(x), 1) for x in us[i, [1, 3, 4, 5]]] + [int(tl[i, 6])] +

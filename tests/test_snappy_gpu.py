@@ -89,6 +89,78 @@ def test_small_blocks_vs_oracle(oracle):
     assert (o % 16 == 0).all()
 
 
+def _varint(n):
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def _lit4(b):   # a literal with a 4-byte length field (the longest legal header)
+    return bytes([63 << 2]) + (len(b) - 1).to_bytes(4, "little") + b
+
+
+def _copy4(length, off):   # a copy with a 4-byte offset, 1..64 bytes
+    return bytes([((length - 1) << 2) | 3]) + off.to_bytes(4, "little")
+
+
+def _copy2(length, off):
+    return bytes([((length - 1) << 2) | 2]) + off.to_bytes(2, "little")
+
+
+def test_small_blocks_wasteful_encodings_vs_oracle(oracle):
+    """valid streams whose encodings are far longer than their output (<= 4.5 KiB, the
+    four-blocks-per-wave kernel): tag bytes and literal bytes past its 4752-byte LDS window are
+    read from HBM; a literal straddling the window end; long runs of 1-byte copies"""
+    codec = _dev()
+    rng = np.random.default_rng(5)
+    streams = []
+    out = rng.integers(0, 256, 1000, dtype=np.uint8).tobytes()
+    streams.append(_varint(1000) + b"".join(_lit4(out[i: i + 1]) for i in range(1000)))   # 6 B per byte
+    tail = rng.integers(0, 256, 1500, dtype=np.uint8).tobytes()
+    streams.append(_varint(3001 + 1500) + bytes([0]) + b"A" + b"".join(_copy4(1, 1) for _ in range(3000)) + _lit4(tail))
+    # a literal starting inside the window and ending past it
+    pre = b"".join(_copy2(1, 1) for _ in range(1500))   # 3 B per output byte
+    mid = rng.integers(0, 256, 1200, dtype=np.uint8).tobytes()
+    streams.append(_varint(1 + 1500 + 1200) + bytes([0]) + b"z" + pre + _lit4(mid))
+    # random element mix, some copies reaching back the whole block
+    for seed in range(6):
+        r = np.random.default_rng(100 + seed)
+        body, produced, parts = bytearray(), 0, []
+        first = r.integers(0, 256, 8, dtype=np.uint8).tobytes()
+        body += _lit4(first)
+        parts.append(first)
+        produced = 8
+        while produced < 4000:
+            k = int(r.integers(0, 3))
+            if k == 0:
+                b = r.integers(0, 256, int(r.integers(1, 90)), dtype=np.uint8).tobytes()
+                body += _lit4(b)
+                parts.append(b)
+                produced += len(b)
+            else:
+                ln = int(r.integers(1, 65))
+                off = int(r.integers(1, produced + 1))
+                body += _copy4(ln, off) if k == 1 else _copy2(ln, min(off, 65535))
+                o = min(off, 65535) if k == 2 else off
+                cur = b"".join(parts)
+                piece = bytearray()
+                for i in range(ln):
+                    piece.append((cur + bytes(piece))[len(cur) - o + i])
+                parts.append(bytes(piece))
+                produced += ln
+        streams.append(_varint(produced) + bytes(body))
+    assert all(len(z) > 4752 for z in streams[:3])
+    from mtblx import pipe
+    streams += [pipe.snappy_compress(bytes(rng.integers(0, 256, 3000, dtype=np.uint8)))] * 5
+    got, st, _ = _device(codec, streams, rng, lead=5)
+    _check(oracle, streams, got, st)
+    assert (st == 0).all()
+
+
 def test_mixed_and_large_blocks_vs_oracle(oracle):
     """outputs up to 200 KB: the Large variant, in-HBM assembly above 65 KiB, long literals
     crossing staging windows, overlapping copies"""

@@ -400,30 +400,36 @@ __global__ void __launch_bounds__(C::WAVES * kWave) k_snappy_blocks(const uint8_
   }
 }
 
-// ---- Small outputs (<= 4.5 KiB): four blocks per wave ----
+// ---- Small outputs (<= 4.5 KiB): four blocks per wave, one LDS buffer per block ----
 //
 // One wave per block leaves the tag chain to the CU's one scalar unit, shared by all 16 waves
 // (~70 scalar instructions per element: profiles/r02/snappy).  Here a wave decodes FOUR blocks
 // at once, one per 16-lane group: the parse state is group-uniform and lives in VGPRs, so one
 // vector instruction advances four chains, and the 16 lanes of a group then write the element
-// (4 bytes per lane, 64 per step) straight into the group's LDS output -- element by element,
-// so an overlapping copy reads only bytes written before it (its period pattern), and no
-// parking or run flushes are needed.  The four blocks of a wave start and end together (a
-// "quad"); the next quad's stored bytes and the one after's offsets are loaded into VGPRs
-// while the current quad decodes, so a quad switch waits on nothing recent.
+// (4 bytes per lane, 64 per step) -- element by element, so an overlapping copy reads only
+// bytes written before it (its period pattern), and no parking or run flushes are needed.
+// The four blocks of a wave start and end together (a "quad").
+//
+// The loop is latency-bound, so throughput is blocks in flight per CU, and LDS sets that: each
+// block has ONE buffer, its output growing from offset 0 and its stored bytes staged
+// right-aligned at the end.  An element is written only if its bytes end before the first
+// stored byte not yet consumed (checked per element; a stream ordinary compressors write never
+// trips it, the output only catches up with the input at the end); a block that would is left
+// to the one-wave-per-block kernel (status kDefer, k_snappy_deferred), as is a block whose
+// stored bytes or output do not fit.  4.6 KiB per block: 8 waves per CU, twice the blocks of
+// separate window + output buffers.
 namespace quad {
 constexpr int G = 16, NG = kWave / G;
-constexpr int WIN = 4752;               // stored bytes staged per block (>= 4736 from position 0)
 constexpr int OUT = 4608;
-constexpr int NCH = WIN / 16;           // 16-byte chunks per window
-constexpr int NPF = (NCH + G - 1) / G;  // chunks per lane
-constexpr int WG_PER_CU = 4;
+constexpr int BUF = 4672;               // output [0, W) and the stored bytes right-aligned below BUF
+constexpr int NCH = BUF / 16;           // 16-byte chunks of a buffer
+constexpr int NPL = (NCH + G - 1) / G;  // chunks per lane
+constexpr int WG_PER_CU = 8;
+constexpr int32_t kDefer = 0x7fffffff;  // internal status: the block goes to k_snappy_deferred
 
 struct alignas(16) Blk {
-  uint8_t win[WIN + 16];   // stored bytes at block positions [wbase, wbase + WIN); 16 B slack
-  uint8_t out[OUT + 16];
+  uint8_t b[BUF + 16];   // 16 B slack: 8-byte header reads and 4-byte writes past the end
 };
-constexpr uint32_t kOutOff = WIN + 16;   // Blk::out - Blk::win
 
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
@@ -447,37 +453,6 @@ __device__ __forceinline__ Meta load_meta(uint32_t b, uint32_t nblk, const uint8
   return m;
 }
 
-// the window of a block: its stored bytes from the 16-byte address at or below position 0
-// (wbase = -misalignment), chunk c = lane l + 16 k; bytes past the stream read as 0.  Whole
-// chunks are 16-byte loads; the two partial ones (head, tail) one byte per lane.
-struct Win {
-  uint4 v[NPF];
-  uint32_t hb, tb, ct;   // head chunk byte l, tail chunk ct's byte l
-  __device__ __forceinline__ void load(const Meta& m, bool on, int l) {
-    const int32_t wb = -(int32_t)((uintptr_t)m.s & 15u), n = on ? (int32_t)m.n : 0;
-#pragma unroll
-    for (int k = 0; k < NPF; ++k) {
-      const int32_t c = l + G * k, bp = wb + 16 * c;
-      v[k] = make_uint4(0, 0, 0, 0);
-      if (c < NCH && bp >= 0 && bp + 16 <= n) v[k] = *reinterpret_cast<const uint4*>(m.s + bp);
-    }
-    const int32_t ph = wb + l;
-    hb = (ph >= 0 && ph < n) ? m.s[ph] : 0u;
-    ct = n > 0 ? (uint32_t)(n - 1 - wb) / 16u : 0u;
-    const int32_t pt = wb + 16 * (int32_t)ct + l;
-    tb = (ct < (uint32_t)NCH && pt >= 0 && pt < n) ? m.s[pt] : 0u;
-  }
-  __device__ __forceinline__ void store(uint8_t* win, int l) const {
-#pragma unroll
-    for (int k = 0; k < NPF; ++k) {
-      const int c = l + G * k;
-      if (c < NCH) *reinterpret_cast<uint4*>(win + 16 * c) = v[k];
-    }
-    win[l] = (uint8_t)hb;
-    if (ct < (uint32_t)NCH) win[16 * ct + l] = (uint8_t)tb;
-  }
-};
-
 // j mod off for j < 2^20, off >= 1: float quotient (rcp within an ulp), one correction each way
 __device__ __forceinline__ uint32_t umod(uint32_t j, uint32_t off, float rcp) {
   const int32_t q = (int32_t)((float)j * rcp);
@@ -493,52 +468,65 @@ __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, cons
                                                         uint32_t max_out, int32_t* status, uint32_t* dec_len) {
   __shared__ Blk S[NG];
   const int lane = threadIdx.x, g = lane >> 4, l = lane & 15;
-  Blk& B = S[g];
-  uint8_t* base = B.win;   // LDS offsets below are relative to B.win (B.out = base + kOutOff)
+  uint8_t* base = S[g].b;
   const uint32_t nquad = (nblk + NG - 1) / NG, qstride = gridDim.x;
   uint32_t q = blockIdx.x;
   if (q >= nquad) return;
-  const uint32_t cap_lds = min(max_out, (uint32_t)OUT);
   auto blk_of = [&](uint32_t qq) { return qq * NG + (uint32_t)g; };
   auto meta = [&](uint32_t qq) {
     return load_meta(qq < nquad ? blk_of(qq) : nblk, nblk, src, src_off, src_len, dst, dst_off, dst_len);
   };
-  // prologue: quad q's window into LDS, q+1's window and q+2's offsets in flight
-  Meta cur = meta(q), m1 = meta(q + qstride);
-  Win pf;
-  pf.load(cur, blk_of(q) < nblk, l);
-  pf.store(base, l);
-  pf.load(m1, q + qstride < nquad && blk_of(q + qstride) < nblk, l);
-  Meta m2 = meta(q + 2 * qstride);
+  Meta cur = meta(q), m1 = meta(q + qstride);   // offsets of the next quad are loaded a quad ahead
 
   for (;;) {
     const uint32_t b = blk_of(q);
     const bool on = b < nblk;
     const uint8_t* s = cur.s;
     const uint32_t n = cur.n;
+    // stored bytes: stream position p <-> buffer offset p + sh (16-byte chunks from the aligned
+    // address at or below position 0, placed so the last one ends at or below BUF)
     const int32_t wb = -(int32_t)((uintptr_t)s & 15u);
-    const uint32_t wend = (uint32_t)(wb + WIN);   // block positions [.., wend) are in the window
-    // 8 stored bytes at position p (p < n): LDS when they are staged (or the stream ends inside
-    // the window: bytes past n are never used), else from HBM byte by byte
-    auto hdr8 = [&](uint32_t p, uint32_t& lo, uint32_t& hi) {
-      if (p + 8u <= wend || n <= wend) {
-        const v2u x = *reinterpret_cast<const v2u*>(base + (p - (uint32_t)wb));
-        lo = x.x;
-        hi = x.y;
-      } else {
-        uint64_t x = 0;
+    const uint32_t span = n + (uint32_t)(-wb);            // bytes from the aligned start
+    const bool fits = on && span <= (uint32_t)BUF;
+    const uint32_t nch = fits ? (span + 15u) / 16u : 0u;
+    const uint32_t ib = (uint32_t)BUF - 16u * nch;        // buffer offset of chunk 0
+    const uint32_t sh = ib - (uint32_t)wb;                // stream position p at buffer offset p + sh
+    {
+      uint4 v[NPL];
 #pragma unroll
-        for (uint32_t t = 0; t < 8; ++t)
-          if (p + t < n) x |= (uint64_t)s[p + t] << (8 * t);
-        lo = (uint32_t)x;
-        hi = (uint32_t)(x >> 32);
+      for (int k = 0; k < NPL; ++k) {
+        const int32_t c = l + G * k, bp = wb + 16 * c;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if ((uint32_t)c < nch && bp >= 0 && bp + 16 <= (int32_t)n) v[k] = *reinterpret_cast<const uint4*>(s + bp);
       }
+      // the partial head / tail chunks, one byte per lane
+      const int32_t ph = wb + l;
+      const uint32_t hb = (fits && ph >= 0 && ph < (int32_t)n) ? s[ph] : 0u;
+      const uint32_t ct = nch ? nch - 1u : 0u;
+      const int32_t pt = wb + 16 * (int32_t)ct + l;
+      const uint32_t tb = (fits && pt >= 0 && pt < (int32_t)n) ? s[pt] : 0u;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        const uint32_t c = (uint32_t)(l + G * k);
+        if (c < nch) *reinterpret_cast<uint4*>(base + ib + 16 * c) = v[k];
+      }
+      if (nch) {
+        base[ib + l] = (uint8_t)hb;
+        base[ib + 16 * ct + l] = (uint8_t)tb;
+      }
+    }
+    const uint32_t qn = q + qstride;
+    Meta m2 = meta(qn + qstride);
+    auto hdr8 = [&](uint32_t p, uint32_t& lo, uint32_t& hi) {   // stream bytes [p, p + 8), p < n
+      const v2u x = *reinterpret_cast<const v2u*>(base + p + sh);
+      lo = x.x;
+      hi = x.y;
     };
     // ---- preamble ----
     uint32_t lo = 0, hi = 0, pos = 0, W = 0, d = 0;
     int32_t st = MTBLX_SNAPPY_OK;
     if (on) {
-      if (n) hdr8(0, lo, hi);
+      if (fits && n) hdr8(0, lo, hi);
       uint64_t want = 0;
       bool term = false;
       for (uint32_t i = 0; i < 5 && i < n; ++i) {
@@ -550,8 +538,10 @@ __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, cons
           break;
         }
       }
-      if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
-      else if (want > cur.cap || want > cap_lds) st = MTBLX_SNAPPY_TOO_SMALL;
+      if (!fits) st = kDefer;
+      else if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
+      else if (want > cur.cap) st = MTBLX_SNAPPY_TOO_SMALL;
+      else if (want > min(max_out, (uint32_t)OUT)) st = kDefer;
       W = (uint32_t)want;
     }
     // ---- elements: decode one per group, then the groups write them together ----
@@ -577,20 +567,23 @@ __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, cons
       const uint32_t L0 = lit ? llit : lc, hl = lit ? hlit : need + 1u, sp = pos + hl;
       bool bad = lit ? (lbad || n - sp < L0) : (avail < need || off == 0u || off > d);
       bad = bad || W - d < L0;
-      const bool hbm = lit && sp + L0 > wend;   // literal bytes not staged: read from HBM
-      const uint32_t so = lit ? (hbm ? sp : sp - (uint32_t)wb) : kOutOff + d - off;
-      const uint32_t P = (!lit && off < L0) ? off : 0xFFFFFFFFu;   // overlapping copy: period off
+      const uint32_t np = lit ? sp + L0 : sp;                   // the next unread stream byte
+      const bool over = !bad && d + L0 + 3u > np + sh;          // the writes would reach it
+      const uint32_t so = lit ? sp + sh : d - off;               // buffer offset of the source
+      const uint32_t P = (!lit && off < L0) ? off : 0xFFFFFFFFu; // overlapping copy: period off
       const float rcp = __builtin_amdgcn_rcpf((float)(P & 0xffffu));
       uint32_t L = 0;
       if (work) {
         if (bad) {
           st = MTBLX_SNAPPY_CORRUPT;
+        } else if (over) {
+          st = kDefer;
         } else {
           L = L0;
-          pos = lit ? sp + L0 : sp;
+          pos = np;
         }
       }
-      const bool go = work && !bad;
+      const bool go = work && !bad && !over;
       work = go && pos < n;
       if (work) hdr8(pos, lo, hi);   // next element's header, in flight during the writes below
       // write the element: lane l covers bytes [4 l, 4 l + 4) of each 64-byte step (bytes past
@@ -602,59 +595,70 @@ __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, cons
         const uint32_t j = s0 + 4u * (uint32_t)l;
         if (j < L) {
           uint32_t v;
-          if (!hbm) {
-            uint32_t r = P == 0xFFFFFFFFu ? j : umod(j, P, rcp);
-            if (r + 4u <= P) {
-              v = *reinterpret_cast<const u32u*>(base + so + r);
-            } else {
-              v = 0;
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                v |= (uint32_t)base[so + r] << (8 * t);
-                r = r + 1u == P ? 0u : r + 1u;
-              }
-            }
+          uint32_t r = P == 0xFFFFFFFFu ? j : umod(j, P, rcp);
+          if (r + 4u <= P) {
+            v = *reinterpret_cast<const u32u*>(base + so + r);
           } else {
             v = 0;
 #pragma unroll
-            for (uint32_t t = 0; t < 4; ++t)
-              if (j + t < L) v |= (uint32_t)s[so + j + t] << (8 * t);
+            for (int t = 0; t < 4; ++t) {
+              v |= (uint32_t)base[so + r] << (8 * t);
+              r = r + 1u == P ? 0u : r + 1u;
+            }
           }
-          *reinterpret_cast<u32u*>(base + kOutOff + d + j) = v;
+          *reinterpret_cast<u32u*>(base + d + j) = v;
         }
       }
       d += L;
     }
     if (on && st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
 
-    // ---- quad switch: next window into LDS, this quad's output to HBM, loads for later quads ----
-    const uint32_t qn = q + qstride;
-    const bool more = qn < nquad;   // wave-uniform
-    const bool emit = on && st == MTBLX_SNAPPY_OK;
-    if (emit) {
+    // ---- output to HBM, statuses ----
+    if (on && st == MTBLX_SNAPPY_OK) {
       if (((uintptr_t)cur.dg & 15u) == 0) {
         const uint32_t n16 = W / 16u;
         for (uint32_t c = (uint32_t)l; c < n16; c += G)
-          reinterpret_cast<uint4*>(cur.dg)[c] = *reinterpret_cast<const uint4*>(B.out + 16 * c);
+          reinterpret_cast<uint4*>(cur.dg)[c] = *reinterpret_cast<const uint4*>(base + 16 * c);
         const uint32_t tb = 16u * n16 + (uint32_t)l;
-        if (tb < W) cur.dg[tb] = B.out[tb];
+        if (tb < W) cur.dg[tb] = base[tb];
       } else {
 #pragma unroll 1
-        for (uint32_t j = (uint32_t)l; j < W; j += G) cur.dg[j] = B.out[j];
+        for (uint32_t j = (uint32_t)l; j < W; j += G) cur.dg[j] = base[j];
       }
     }
-    if (more) pf.store(base, l);
     if (on && l == 0) {
       status[b] = st;
-      if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
+      if (dec_len && st != kDefer) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
     }
-    if (!more) break;
+    if (qn >= nquad) break;   // wave-uniform
     q = qn;
     cur = m1;
     m1 = m2;
-    const uint32_t q1 = q + qstride;
-    pf.load(m1, q1 < nquad && blk_of(q1) < nblk, l);
-    m2 = meta(q + 2 * qstride);
+  }
+}
+
+// The blocks k_snappy_quads left (status kDefer): one wave per block, the one-wave kernel's
+// code (Large config: outputs up to 65 KiB in LDS, larger in place in HBM).  A wave checks 64
+// statuses per load and decodes the deferred ones among them.
+__global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, const uint64_t* src_off,
+                                                           const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                           const uint64_t* dst_off, const uint32_t* dst_len,
+                                                           int32_t* status, uint32_t* dec_len) {
+  __shared__ WaveLds<Large> SL;
+  const int lane = threadIdx.x;
+  for (uint32_t b0 = blockIdx.x * kWave; b0 < nblk; b0 += gridDim.x * kWave) {
+    const uint32_t bl = b0 + (uint32_t)lane;
+    uint64_t m = __ballot(bl < nblk && status[bl] == kDefer);
+    while (m) {
+      const uint32_t b = b0 + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1ull;
+      const uint8_t* s = src + src_off[b];
+      const uint32_t n = src_len[b];
+      Window<Large> pf;
+      pf.load(s, n, 0, lane);
+      snap_block<Large>(SL, pf, s, n, s, 0u, dst + dst_off[b], dst_len[b], lane, status + b,
+                        dec_len ? dec_len + b : nullptr);
+    }
   }
 }
 }  // namespace quad
@@ -802,6 +806,8 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
     hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len);
+    hipLaunchKernelGGL(quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
+                       src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   } else {
     hipLaunchKernelGGL(k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,
                        src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);

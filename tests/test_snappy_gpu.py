@@ -153,6 +153,12 @@ def test_small_blocks_wasteful_encodings_vs_oracle(oracle):
                 parts.append(bytes(piece))
                 produced += ln
         streams.append(_varint(produced) + bytes(body))
+    # output that catches up with its unread stored bytes: a copy-heavy head (3009 bytes from
+    # ~144 stored bytes) then 1500 one-byte literals with 1-byte tags (2 stored bytes each) --
+    # the shared-buffer kernel must hand this block to the deferred pass
+    lits = rng.integers(0, 256, 1500, dtype=np.uint8).tobytes()
+    streams.append(_varint(1 + 47 * 64 + 1500) + bytes([0]) + b"A" + _copy2(64, 1) * 47 +
+                   b"".join(bytes([0]) + lits[i: i + 1] for i in range(1500)))
     assert all(len(z) > 4752 for z in streams[:3])
     from mtblx import pipe
     streams += [pipe.snappy_compress(bytes(rng.integers(0, 256, 3000, dtype=np.uint8)))] * 5

@@ -1176,6 +1176,7 @@ struct alignas(16) PipeLds {
   uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
   uint32_t pub;      // wave 0 sets after publishing the aggregate of the tile it walked
   uint32_t cdone;    // copy waves that finished their copy (monotonic)
+  uint8_t cmk[kPipeThreads / kWave][kWave];   // per copy wave: first-chunk marks of the dense key-tail copy
   // VERIFY: slicing-by-4 CRC-32C tables, per-block XOR accumulators (by tile parity), and
   // the count of CRC waves done (monotonic; the last of a tile finalises it)
   uint32_t crcT[P::VERIFY ? 4 : 1][P::VERIFY ? 256 : 1];
@@ -1724,8 +1725,54 @@ __device__ __forceinline__ CopyRow copy_prepare(const PipeBuf<P>& B, uint32_t fb
   return r;
 }
 
+// Key bytes at positions >= 16 when no live entry of the wave inherits one there: each such
+// byte is the entry's own suffix (key.truncate(shared) + key.extend(suffix), src/block.rs:134-135),
+// so the wave's key tails form one dense list of 16-byte chunks and pass c0 gives chunk c0 + l
+// to lane l.  The chunk's entry is the last one whose first chunk is <= it: entries mark their
+// first chunk in the wave's LDS row (by lane id; 0 = no mark, lane 0 never starts past chunk 0)
+// and a prefix max over the row, seeded with the entry holding chunk c0 (a ballot), fills the rest.  That is
+// ceil(sum of chunks / 64) passes instead of one per 16-byte plane of the wave's longest key
+// (cfg3's Zipf keys: ~2 instead of ~15).  src / dst = stage offset / key-region offset of the
+// entry's byte 16.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  uint32_t y;
+  y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false); x = x > y ? x : y;  // row_shr:1
+  y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false); x = x > y ? x : y;  // row_shr:2
+  y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false); x = x > y ? x : y;  // row_shr:4
+  y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false); x = x > y ? x : y;  // row_shr:8
+  y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false); x = x > y ? x : y;  // row_bcast:15
+  y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false); x = x > y ? x : y;  // row_bcast:31
+  return x;
+}
+
+__device__ __forceinline__ void key_tails_dense(uint8_t* kb, const uint8_t* stage, uint8_t* mk, bool tl, uint32_t klen,
+                                                uint32_t src, uint32_t dst, int lane) {
+  const uint32_t nc = tl ? (klen - 1u) >> 4 : 0u;   // ceil((klen - 16) / 16)
+  const uint32_t ci = wave_incl_scan(nc);
+  const uint32_t cx = ci - nc;
+  const uint32_t C = (uint32_t)__builtin_amdgcn_readlane((int)ci, 63);
+  const uint32_t tail = klen - 16u;
+  for (uint32_t c0 = 0; c0 < C; c0 += kWave) {   // wave-uniform
+    const uint32_t seed = (uint32_t)__builtin_popcountll(__ballot(ci <= c0));   // entry holding chunk c0
+    mk[lane] = 0;
+    if (nc != 0u && cx > c0 && cx < c0 + kWave) mk[cx - c0] = (uint8_t)lane;   // lane > 0 here
+    wave_sync();   // DS instructions of one wave run in order: the read sees both writes
+    uint32_t own = mk[lane];
+    own = wave_incl_max(own > seed ? own : seed);
+    wave_sync();   // the row is rewritten next pass after every lane has read it
+    const int o = (int)own;
+    const uint32_t ocx = (uint32_t)__shfl((int)cx, o, kWave), osrc = (uint32_t)__shfl((int)src, o, kWave);
+    const uint32_t odst = (uint32_t)__shfl((int)dst, o, kWave), otl = (uint32_t)__shfl((int)tail, o, kWave);
+    const uint32_t c = c0 + (uint32_t)lane;
+    if (c < C) {
+      const uint32_t q = 16u * (c - ocx), n = otl - q;
+      store_bytes(kb + odst + q, lds_win16(stage, osrc + q), n < 16u ? n : 16u);
+    }
+  }
+}
+
 template <class P>
-__device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a, const CopyRow& r, int lane) {
+__device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a, const CopyRow& r, int lane, uint8_t* mk) {
   const uint64_t pr = B.tpre[0], pk = B.tpre[1], pv = B.tpre[2];
   const bool live = r.live && B.bwr[r.j];   // bwr may have been cleared by the look-back (overflow)
   if (live) {
@@ -1785,6 +1832,13 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
 #ifndef MTBLX_ABL_NOKEY
   uint8_t* kd = a.keys + pk + r.ks;
   if (live && r.klen > 0u) store_bytes(kd, r.W0, r.klen < 16u ? r.klen : 16u);
+  const bool tl = live && r.klen > 16u;
+  if (__ballot(tl) == 0ull) return;
+  // (not in the fused-verify kernels: at their 128-VGPR cap it pushes PipeLargeV into scratch)
+  if (!P::VERIFY && __ballot(tl && r.sh > 16u) == 0ull) {
+    key_tails_dense(a.keys + pk, B.stage, mk, tl, r.klen, r.sp - r.sh + 16u, r.ks + 16u, lane);
+    return;
+  }
   for (uint32_t q0 = 16; __ballot(live && r.klen > q0) != 0ull; q0 += 16) {   // further planes (keys > 16 B)
     if (__ballot(live && r.sh > q0 && q0 < r.klen) == 0ull) {
       // no live entry inherits a byte of this plane from an earlier key: every byte is the
@@ -1823,7 +1877,7 @@ __device__ __forceinline__ void wait_flag(const TileArgs& a, const uint32_t* fla
 
 template <class P>
 __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a, int cw, int lane, const uint32_t* ready,
-                                          uint32_t want, Stamps& ST, uint32_t rows = P::ROWS) {
+                                          uint32_t want, Stamps& ST, uint8_t* mk, uint32_t rows = P::ROWS) {
   const uint32_t nint = B.nint, nb = B.nb;
   uint32_t fb = (uint32_t)cw * (kWave / 16);
   if (fb < nint) {
@@ -1831,10 +1885,10 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
     ST.hit(14);
     wait_flag(a, ready, want);
     ST.hit(0);
-    if (a.write) copy_emit(B, a, r, lane);
+    if (a.write) copy_emit(B, a, r, lane, mk);
     for (fb += rows; fb < nint; fb += rows) {   // wave-uniform
       const CopyRow r2 = copy_prepare(B, fb, lane);
-      if (a.write) copy_emit(B, a, r2, lane);
+      if (a.write) copy_emit(B, a, r2, lane, mk);
     }
   } else {
     wait_flag(a, ready, want);
@@ -2078,7 +2132,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
         wait_flag(a, &S.pub, it + 1);
-        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, it + 1, ST);
+        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, it + 1, ST, S.cmk[wv]);
         ST.hit(7);
       }
       raw_barrier();
@@ -2100,7 +2154,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     } else if (loader) {
       if constexpr (kLoadCopy) {
         if (it >= 0) {
-          pipe_copy(S.buf[(uint32_t)it % P::NBUF], a, P::NCOPY + (int)part, lane, &S.ready, (uint32_t)it + 1, ST, kRows);
+          pipe_copy(S.buf[(uint32_t)it % P::NBUF], a, P::NCOPY + (int)part, lane, &S.ready, (uint32_t)it + 1, ST, S.cmk[wv], kRows);
           if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
@@ -2141,7 +2195,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         }
         ST.hit(1);
       } else {
-        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST, kRows);
+        pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST, S.cmk[wv], kRows);
         if (wv == P::COPY0 && it + 1 == (int)nloc) TLW(9);   // first copy wave: last tile's stores issued
         if (wv == P::COPY0 + P::NCOPY - 1 && it + 1 == (int)nloc) TLW(10);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

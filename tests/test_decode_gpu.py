@@ -273,3 +273,52 @@ def test_fused_verify_decode(oracle):
         exp = np.array([oracle.crc32c(bytes(d_[int(a): int(a) + int(n)])) for a, n in zip(o_, l_)], np.uint32)
         assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
         assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == (bad_exp if framed else [])
+
+
+
+def _tail_records(rng, n, mode):
+    """n strictly increasing keys for the copy waves' key-tail paths, random 0..64 B values.
+    "counter": be64 counter with random gaps (shared ~5 B) + a random tail of 0..292 B, so every
+    key byte past 16 is the entry's own suffix (the dense chunk list); "p16": a common 16-byte
+    prefix, one distinct byte, a tail (shared == 16 exactly: the dense path's boundary; n <= 256);
+    "mixed": counter keys, every third one repeating the previous key's first 20..60 bytes
+    (shared > 16 in some rows of a wave: the per-plane path)."""
+    lens = [0, 1, 8, 9, 16, 17, 24, 31, 32, 33, 48, 100, 160, 240, 292]
+    keys, c, prev = [], 0, b""
+    p16 = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    for i in range(n):
+        tail = bytes(rng.integers(0, 256, int(rng.choice(lens)), dtype=np.uint8))
+        if mode == "p16":
+            k = p16 + bytes([i]) + tail
+        elif mode == "mixed" and len(prev) > 24 and rng.random() < 0.35:
+            cut = int(rng.integers(20, min(60, len(prev)) + 1))
+            k = prev[:cut] + b"\xff" + tail   # > prev: byte `cut` of prev is < 0xff or prev ends there
+            if k <= prev:
+                k = prev + b"\x01"
+        else:
+            c += int(rng.integers(1, 1 << 20))
+            k = c.to_bytes(8, "big") + tail
+            if k <= prev:
+                k = prev + b"\x02"
+        keys.append(k)
+        prev = k
+    assert all(a < b for a, b in zip(keys, keys[1:]))
+    return [(k, bytes(rng.integers(0, 256, int(rng.integers(0, 65)), dtype=np.uint8))) for k in keys]
+
+
+def test_key_tails_dense_and_planes(oracle):
+    """Keys longer than 16 B through both copy paths: the wave-wide dense chunk list (no live
+    entry of the wave inherits a byte past 16) and the per-plane scan (some entry does), in
+    ~4 KiB blocks (PipeSmall) and ~40-64 KiB blocks (PipeLarge), restart intervals 16, 1, 7, 13."""
+    rng = np.random.default_rng(0x7a11)
+    for nrec in (36, 560):
+        blocks = []
+        for mode in ("counter", "p16", "mixed"):
+            for iv in (16, 16, 1, 7, 13):
+                recs = _tail_records(rng, min(nrec, 256) if mode == "p16" else nrec, mode)
+                blocks.append(oracle.build_block(recs, restart_interval=iv))
+        blocks = [b for b in blocks if len(b) <= 65000] * 4
+        assert nrec < 100 or max(len(b) for b in blocks) > 49200   # PipeLarge
+        orc = run_both(oracle, blocks, rng=np.random.default_rng(5))
+        assert (orc.status == 0).all()
+        assert int(np.diff(orc.key_end.astype(np.int64)).max()) > 200

@@ -1176,6 +1176,7 @@ struct alignas(16) PipeLds {
   uint32_t ready;    // wave 1 sets after the prefix + per-block outputs of the tile to copy
   uint32_t pub;      // wave 0 sets after publishing the aggregate of the tile it walked
   uint32_t cdone;    // copy waves that finished their copy (monotonic)
+  uint32_t staged;   // late-walk schedule: loader waves whose DMA of a tile has landed (monotonic)
   uint8_t cmk[kPipeThreads / kWave][kWave];   // per copy wave: first-chunk marks of the dense key-tail copy
   // VERIFY: slicing-by-4 CRC-32C tables, per-block XOR accumulators (by tile parity), and
   // the count of CRC waves done (monotonic; the last of a tile finalises it)
@@ -2037,6 +2038,15 @@ constexpr bool kLargeSerial = true;   // A/B: the round-2 two-buffer schedule fo
 #else
 constexpr bool kLargeSerial = false;
 #endif
+// Two-buffer schedule (PipeLarge): 1 = late walk (the DMA of tile it+1 into the free buffer at
+// the start of iteration it, beside the prepare + copy of tile it; the walker walks tile it+1 once
+// it has landed); 0 = walk of tile it+1 beside the copy of tile it, DMA of tile it+2 after it.
+#ifndef MTBLX_LARGE_LATE
+#define MTBLX_LARGE_LATE 1
+#endif
+#ifndef MTBLX_LATE_LOADCOPY   // late walk: the loaders copy rows of tile it after their DMA
+#define MTBLX_LATE_LOADCOPY 0
+#endif
 
 template <class P>
 __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
@@ -2049,7 +2059,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   // Two buffers, three stages: the loaders have nothing to do until the copy waves leave tile
   // it's buffer, so they copy too (as copy waves NCOPY ..): 56 rows per pass, so a 64 KiB block
   // (~53 restart intervals) takes one pass instead of 48 + 5.
-  constexpr bool kLoadCopy = P::NBUF == 2 && !serial2;
+  constexpr bool kLate = P::NBUF == 2 && !serial2 && MTBLX_LARGE_LATE;
+  constexpr bool kLoadCopy = P::NBUF == 2 && !serial2 && (!kLate || MTBLX_LATE_LOADCOPY);
   constexpr uint32_t kCopyW = P::NCOPY + (kLoadCopy ? P::LOADW : 0);   // waves that copy a tile
   constexpr uint32_t kRows = kCopyW * (kWave / 16);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2060,7 +2071,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   TL(0);
   ws_begin(a);
   a.flags_direct = 1;
-  if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; }
+  if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; S.staged = 0; }
   if constexpr (P::VERIFY) {
     for (int i = tid; i < 4 * 256; i += kPipeThreads) S.crcT[i >> 8][i & 255] = mtblx_crc::kTab.slice[i >> 8][i & 255];
     for (int i = tid; i < 2 * P::MAXBLK; i += kPipeThreads) S.cacc[i / P::MAXBLK][i % P::MAXBLK] = 0;
@@ -2083,8 +2094,10 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   const uint32_t part = (uint32_t)(wv - kPipeLoadWave);
   if (loader) {
     load_info(0);
-    if (nloc > 0) pipe_dma(S.buf[0], a, g, ioff, ilen, lane, part);
-    load_info(1);
+    if constexpr (!kLate) {
+      if (nloc > 0) pipe_dma(S.buf[0], a, g, ioff, ilen, lane, part);
+      load_info(1);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (wv == 1) {
     if (!serial2 && nloc > 0) pipe_lookback_issue(a, g, G, lbv, lane);
@@ -2140,6 +2153,71 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       else if (wv == P::COPY0) ST.hit(5);
       else if (loader) ST.hit(12);
       else ST.hit(1);
+    }
+  } else if constexpr (kLate) {
+    // iteration it: the loaders stage tile it+1 into the buffer tile it-1 left, then (optionally)
+    // copy rows of tile it; the walker walks tile it+1 once both loaders' DMA has landed; the
+    // look-back and copy waves finish tile it meanwhile.  The DMA (HBM reads) now overlaps the
+    // copy's prepare and stores instead of following them.
+    for (int it = -1; it < (int)nloc; ++it) {
+      const uint32_t k1 = (uint32_t)(it + 1);
+      if (wv == 0) {
+        if (k1 < nloc) {
+          wait_flag(a, &S.staged, (k1 + 1) * (uint32_t)P::LOADW);
+          pipe_walk(S.buf[k1 & 1u], a, g + k1 * G, lane, ST);
+          if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        ST.hit(3);
+      } else if (loader) {
+        if (k1 < nloc) {
+          pipe_dma(S.buf[k1 & 1u], a, g + k1 * G, ioff, ilen, lane, part);
+          load_info(k1 + 1);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of tile it+1 has landed
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_fetch_add(&S.staged, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        ST.hit(4);
+        if constexpr (kLoadCopy) {
+          if (it >= 0) {
+            pipe_copy(S.buf[(uint32_t)it & 1u], a, P::NCOPY + (int)part, lane, &S.ready, (uint32_t)it + 1, ST, S.cmk[wv], kRows);
+            if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        ST.hit(6);
+      } else if (it >= 0) {
+        PipeBuf<P>& C = S.buf[(uint32_t)it & 1u];
+        const uint32_t tc = g + (uint32_t)it * G;
+        if (wv == 1) {
+          pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, (uint32_t)it + 1);
+          if (it + 1 == (int)nloc) TLW(8);
+          else if (it + 2 == (int)nloc) TLW(11);
+          ST.hit(1);
+          if (k1 < nloc) {
+            WaitBound wb;
+            while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
+              __builtin_amdgcn_s_sleep(1);
+              if (wb.expired()) { ws_flag(a, 2ull); break; }
+            }
+            pipe_lookback_issue(a, tc + G, G, lbv, lane);
+            pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kCopyW);
+          }
+          ST.hit(1);
+        } else {
+          pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST, S.cmk[wv], kRows);
+          if (wv == P::COPY0 && it + 1 == (int)nloc) TLW(9);
+          if (wv == P::COPY0 + P::NCOPY - 1 && it + 1 == (int)nloc) TLW(10);
+          if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          ST.hit(7);
+        }
+      }
+      raw_barrier();
+      if (it == -1) TL(2);
+      else if (it == 0) TL(3);
+      else if (it + 2 == (int)nloc) TL(7);
+      if (wv == 0) { ST.hit(8); ++ntl; }
+      else if (wv >= P::COPY0) ST.hit(5);
+      else if (loader) ST.hit(12);
+      else ST.hit(11);
     }
   } else
   for (int it = -1; it < (int)nloc; ++it) {

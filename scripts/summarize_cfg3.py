@@ -11,7 +11,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out", "prof_cfg3")
-DST = os.path.join(ROOT, "profiles", "r02", "cfg3")
+DST = os.environ.get("CFG3_DST") or os.path.join(ROOT, "profiles", "r02", "cfg3")
 
 
 def rows(pattern):

@@ -397,6 +397,12 @@ def run_cfg3(args, dist, world, rank):
         with torch.cuda.stream(s):
             encode.encode_into(recs, blk, bufs, 16, True, s)      # warm-up
             enc_ms = _timed(lambda: encode.encode_into(recs, blk, bufs, 16, True, s), s, 3)
+        if os.environ.get("MTBLX_ENC_STAMPS_PRINT") and ci == 0:   # diagnostic build (make variant_enc, -DMTBLX_ENC_STAMPS)
+            torch.cuda.synchronize()
+            d = bufs.ws[:128].cpu().numpy().view(np.uint64).astype(np.float64)
+            names = ["tables+ticket", "phaseA", "assemble", "lookback", "crc", "stream"]
+            log("[enc stamps] cycles per block (thread 0, after a barrier): " + json.dumps(
+                {n: round(d[2 + k] / max(d[15], 1), 1) for k, n in enumerate(names)}))
         e = encode.Encoded(bufs.out, bufs.blk_off[:nb], bufs.blk_len[:nb], bufs.status[:nb], bufs.totals)
         if int(e.totals[1].item()) != 0:
             raise RuntimeError("cfg3: encode reported a failed block")

@@ -30,9 +30,18 @@
 namespace mtblx_enc {
 
 constexpr int kWave = 64;
-constexpr int kThreads = 512;
+#ifndef MTBLX_ENC_THREADS
+#define MTBLX_ENC_THREADS 512
+#endif
+constexpr int kThreads = MTBLX_ENC_THREADS;   // one workgroup per block, 2 per CU (LDS)
 constexpr int kWaves = kThreads / kWave;
-constexpr uint32_t kLdsBlock = 65536 + 1024;   // contents up to this many bytes are assembled in LDS
+#ifndef MTBLX_ENC_LDS_BLOCK
+#define MTBLX_ENC_LDS_BLOCK (65536 + 1024)
+#endif
+#ifndef MTBLX_ENC_WPE   // waves per SIMD the register budget is sized for
+#define MTBLX_ENC_WPE (kThreads / 128)
+#endif
+constexpr uint32_t kLdsBlock = MTBLX_ENC_LDS_BLOCK;   // contents up to this many bytes are assembled in LDS
 constexpr uint32_t kShCache = 2048;            // entries whose `shared` phase A keeps for phase B
 constexpr uint64_t kIncl = 1ull << 63, kAgg = 1ull << 62, kVal = kAgg - 1;
 
@@ -408,8 +417,20 @@ __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeo
   return excl;
 }
 
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) k_encode(EncArgs a) {   // 2 per CU
+// diagnostic per-phase cycle stamps (MTBLX_ENC_STAMPS builds only): thread 0 of each workgroup
+// adds s_memtime deltas into u64 slots 2.. of the workspace header, slot 15 counts blocks
+#ifdef MTBLX_ENC_STAMPS
+#define ESTAMP(k) do { __syncthreads(); if (threadIdx.x == 0) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket) + (k), (unsigned long long)(t_ - tprev)); tprev = t_; } } while (0)
+#else
+#define ESTAMP(k) do { } while (0)
+#endif
+
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MTBLX_ENC_WPE))) k_encode(EncArgs a) {   // 2 per CU
   __shared__ EncLds S;
+#ifdef MTBLX_ENC_STAMPS
+  uint64_t tprev = __builtin_amdgcn_s_memtime();
+#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int i = tid; i < 256; i += kThreads) {   // slicing-by-4 tables from the byte table
     uint32_t t = mtblx_crc::kTab.byte[i];
@@ -426,6 +447,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   if (b >= a.nblk) return;
   const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
   const uint32_t iv = a.interval;
+  ESTAMP(2);   // tables + ticket
 
   // ---- phase A: the content length (entries + restart array + count) ----
   uint64_t part = 0;
@@ -447,6 +469,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     __hip_atomic_store(a.lbw + b, (b == 0 ? kIncl : kAgg) | F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const bool in_lds = L <= kLdsBlock && st == MTBLX_ST_OK;
+  ESTAMP(3);   // phase A: sizes, scan, publish
 
   // ---- phase B (LDS path): assemble the block ----
   const uint64_t R = entries;   // restart array offset
@@ -475,6 +498,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     }
   };
   if (in_lds) assemble(S.ob);
+  ESTAMP(4);   // assembly in LDS
 
   // ---- look-back: this block's offset in the output ----
   if (w == 0) {
@@ -487,6 +511,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     }
   }
   __syncthreads();
+  ESTAMP(5);   // look-back
   const uint64_t pre = S.sh_u64[0];
   const uint64_t coff = pre + (a.framed ? vlen64(L) + 4 : 0);
   if (st == MTBLX_ST_OK && pre + F > a.out_cap) st = MTBLX_ST_OVERFLOW;
@@ -501,6 +526,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
     }
     if (a.framed) {
       const uint32_t crc = wg_crc32c(S, src, L);
+      ESTAMP(6);   // CRC-32C
       if (tid == 0) {
         uint8_t h[10];
         const uint32_t hl = venc(h, L);
@@ -521,6 +547,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       for (uint64_t o = 16 * nch + tid; o < L; o += kThreads) dst[o] = S.ob[o];
     }
   }
+  ESTAMP(7);   // stream out
+#ifdef MTBLX_ENC_STAMPS
+  if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket) + 15, 1ull);
+#endif
   if (tid == 0) {
     a.blk_off[b] = st == MTBLX_ST_OK ? coff : 0;
     a.blk_len[b] = st == MTBLX_ST_OK ? (uint32_t)L : 0u;

@@ -270,67 +270,8 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
 #ifndef MTBLX_ENC_NT_STORES
 #define MTBLX_ENC_NT_STORES 1
 #endif
-#ifndef MTBLX_ENC_ALIGNED_COPY
-#define MTBLX_ENC_ALIGNED_COPY 1
-#endif
 
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n, const uint8_t* base) {
-#if MTBLX_ENC_ALIGNED_COPY
-  // destination-aligned: the bytes before dst's first 4-aligned address one by one, then whole
-  // dwords written aligned (16-byte loads from the matching, unaligned source offset; misaligned
-  // multi-byte LDS writes issue far below the aligned rate), then the last < 16 bytes from the
-  // window ending at n
-  const uint32_t lead = (uint32_t)((4u - ((uint32_t)reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u);
-  const uint64_t h = lead < n ? lead : n;
-  for (uint64_t k = 0; k < h; ++k) dst[k] = src[k];
-  if (n <= lead) return;
-  const uint64_t m = n - lead;
-  const uint8_t* s = src + lead;
-  uint32_t* d = reinterpret_cast<uint32_t*>(dst + lead);
-  const uint64_t ng = m / 16;   // whole 16-byte groups
-  for (uint64_t g0 = 0; g0 < ng; g0 += 4) {
-    v4u w[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (g0 + u < ng) w[u] = *reinterpret_cast<const v4u*>(s + 16 * (g0 + u));
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (g0 + u < ng) {
-        uint32_t* q = d + 4 * (g0 + u);
-        q[0] = w[u].x; q[1] = w[u].y; q[2] = w[u].z; q[3] = w[u].w;
-      }
-  }
-  const uint32_t t = (uint32_t)(m % 16);
-  if (t == 0) return;
-  v4u w;
-  if (s + m >= base + 16) {   // the 16-byte window ending at m, shifted down by 16 - t bytes
-    const v4u x = *reinterpret_cast<const v4u*>(s + m - 16);
-    const unsigned __int128 y = ((((unsigned __int128)(((uint64_t)x.w << 32) | x.z)) << 64) |
-                                 (((uint64_t)x.y << 32) | x.x)) >> (8u * (16u - t));
-    w = v4u{(uint32_t)y, (uint32_t)(y >> 32), (uint32_t)(y >> 64), (uint32_t)(y >> 96)};
-  } else {
-    uint64_t lo = 0, hi = 0;
-    for (uint32_t k = 0; k < t; ++k) {
-      const uint64_t b = s[16 * ng + k];
-      if (k < 8) lo |= b << (8 * k);
-      else hi |= b << (8 * (k - 8));
-    }
-    w = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-  }
-  uint32_t* q = d + 4 * ng;
-  const uint32_t td = t / 4;
-  if (td > 0) q[0] = w.x;
-  if (td > 1) q[1] = w.y;
-  if (td > 2) q[2] = w.z;
-  const uint32_t rb = t % 4;
-  if (rb) {
-    const uint32_t x = td == 0 ? w.x : td == 1 ? w.y : td == 2 ? w.z : w.w;
-    uint8_t* e = reinterpret_cast<uint8_t*>(q + td);
-    e[0] = (uint8_t)x;
-    if (rb > 1) e[1] = (uint8_t)(x >> 8);
-    if (rb > 2) e[2] = (uint8_t)(x >> 16);
-  }
-#else
   // chunks of 16 bytes: [0, nfull); tail bytes [16 nfull, n)
   const uint64_t nfull = n / 16;
   for (uint64_t c = 0; c < nfull; c += 4) {
@@ -355,7 +296,6 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   } else {
     for (uint64_t k = to; k < n; ++k) dst[k] = src[k];
   }
-#endif
 }
 
 __device__ __forceinline__ void put32(uint8_t* p, uint32_t v) {

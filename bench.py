@@ -636,8 +636,8 @@ def main():
                          "from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)")
     args = ap.parse_args()
 
-    if args.stamps or args.lib:
-        args.no_crc = True    # diagnostic builds: decode timing only
+    if args.stamps or (args.lib and not os.environ.get("MTBLX_AB_CRC")):
+        args.no_crc = True    # diagnostic builds: decode timing only (MTBLX_AB_CRC=1: keep the CRC legs)
     if args.stamps:
         os.environ["MTBLX_LIB"] = args.lib or os.path.join(ROOT, "oxidized-mtbl_amd", "mtblx", "libmtblx_stamps.so")
     elif args.lib:

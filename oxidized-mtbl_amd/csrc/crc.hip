@@ -27,17 +27,35 @@ struct Slice8 {
 // block start (positions < 0) count as zeros, which leave a zero-init CRC unchanged; the
 // 0xFFFFFFFF init is folded into block bytes 0..3.  18 words -> 9 slicing-by-8 steps.
 constexpr int kWords = kCrcWin / 4;
+// block bytes are read once: non-temporal loads (MTBLX_CRC_NT_LOADS) keep them out of the L2s
+#ifndef MTBLX_CRC_NT_LOADS
+#define MTBLX_CRC_NT_LOADS 0
+#endif
+typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
+__device__ __forceinline__ v4u crc_ld16(const uint8_t* p) {
+#if MTBLX_CRC_NT_LOADS
+  return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+#else
+  return *reinterpret_cast<const v4u*>(p);
+#endif
+}
+__device__ __forceinline__ v2u crc_ld8(const uint8_t* p) {
+#if MTBLX_CRC_NT_LOADS
+  return __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+#else
+  return *reinterpret_cast<const v2u*>(p);
+#endif
+}
 __device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, const uint32_t (*T)[256], bool safe) {
   const int64_t lo = hi - kCrcWin;
   uint32_t w[kWords];
   if (safe) {   // d + lo is readable (inside the buffer) even where lo < 0
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
+      const v4u x = crc_ld16(d + lo + 16 * q);
       w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
     }
-    typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
-    const v2u y = *reinterpret_cast<const v2u*>(d + lo + 64);
+    const v2u y = crc_ld8(d + lo + 64);
     w[16] = y.x; w[17] = y.y;
   } else {      // the window starts before the buffer: byte loads of the in-block part only
 #pragma unroll

@@ -268,11 +268,19 @@ def compressible_snappy(s, nrec=2_000_000):
     from mtblx import codec, synth
     from mtblx.writer import Writer
     w = Writer(4096, 16, 1)
-    n = nrec   # ~25 000 blocks of ~80 records
-    for k, v in synth.cfg1_records(n):
+    n1 = nrec   # ~25 000 blocks of ~80 records
+    for k, v in synth.cfg1_records(n1):
         w.insert(k, v)
-    z = np.frombuffer(w.into_inner(), np.uint8).copy()
-    zoff, zln = w.block_dir
+    z1 = np.frombuffer(w.into_inner(), np.uint8).copy()
+    zoff1, zln1 = w.block_dir
+    # the file's blocks 4x over (100 000 blocks, the cfg2 / cfg5 batch size; generating 8 M records
+    # in Python would take ~40 s): the quad kernel takes 4 blocks per wave, 2048 waves, so 25 000
+    # blocks end on a round of 106 busy waves (3.05 rounds -> 4) and read ~13 % low
+    rep = 4
+    n = n1 * rep
+    z = np.tile(z1, rep)
+    zoff = np.concatenate([zoff1.astype(np.uint64) + np.uint64(i * z1.size) for i in range(rep)])
+    zln = np.tile(zln1, rep)
     zb = codec.SnappyBatch.from_host(z, zoff, zln)
     lay = codec.SnappyLayout(zb.nblk)
     codec.snappy_dir(zb, lay)
@@ -309,7 +317,7 @@ def compressible_snappy(s, nrec=2_000_000):
     if out.totals_host() != (nr, kb, vb, 0):
         raise RuntimeError("compressible cfg5: decode after device decompression failed")
     stored = int(zln.sum(dtype=np.uint64))
-    return {"records": n, "blocks": int(zb.nblk), "stored_bytes": stored, "decompressed_bytes": out_bytes,
+    return {"records": n, "blocks": int(zb.nblk), "file_repeats": rep, "stored_bytes": stored, "decompressed_bytes": out_bytes,
             "ratio": round(out_bytes / stored, 2), "kernel": "k_snappy_quads",
             "device_decompress_ms": round(dz_ms, 4),
             "device_decompress_GB_per_s_out": round(out_bytes / (dz_ms * 1e-3) / 1e9, 1),

@@ -11,7 +11,8 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out", "prof_r02")
-DST = os.path.join(ROOT, "profiles", "r02", "decode")
+DST = os.environ.get("PROF_DST") or os.path.join(ROOT, "profiles", "r02", "decode")
+TRAFFIC = os.environ.get("PROF_TRAFFIC")   # write profiles/traffic.json (the bench's `traffic`) from cur_small
 
 
 def rows(path):
@@ -30,6 +31,8 @@ out = {}
 os.makedirs(DST, exist_ok=True)
 for tag in ("cur_small", "r01_small", "cur_large", "r01_large"):
     d = os.path.join(SRC, tag)
+    if not os.path.isdir(d):
+        continue
     st = [r for r in rows(os.path.join(d, "stats", "run_kernel_stats.csv")) if "k_decode_pipe" in r["Name"]]
     st.sort(key=lambda r: -float(r["TotalDurationNs"]))
     k = st[0]
@@ -64,6 +67,13 @@ for tag in ("cur_small", "r01_small", "cur_large", "r01_large"):
         rec["active_inst_any_frac"] = rec.get("SQ_ACTIVE_INST_ANY", 0) / wc
     out[tag] = rec
 json.dump(out, open(os.path.join(DST, "summary.json"), "w"), indent=1)
+if TRAFFIC and "cur_small" in out and out["cur_small"].get("hbm_bytes"):
+    c = out["cur_small"]
+    json.dump({"kernel": "k_decode_pipe<PipeSmall>", "blocks": 100000, "hbm_bytes_per_launch": c["hbm_bytes"],
+               "alg_bytes_per_launch": c["alg_bytes"], "ratio": round(c["traffic_ratio"], 3),
+               "source": os.path.relpath(DST, ROOT) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate passes, "
+                         "full-batch dispatches of the current kernel)"},
+              open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
 keys = ["kernel", "avg_us", "achieved_GBs", "frac_of_8TBs", "traffic_ratio", "SQ_BUSY_CYCLES", "wait_any_frac",
         "wait_inst_any_frac", "active_inst_any_frac", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
         "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"]

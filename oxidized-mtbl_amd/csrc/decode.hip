@@ -1286,8 +1286,9 @@ __device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, ui
 // or more than 16 entries.  Reads past R land inside the LDS allocation or return 0 and are
 // never used when the walk is rejected (p is monotonic; the result requires p == e <= R).
 __device__ __forceinline__ bool walk_pos2(const uint8_t* stage, uint16_t* pos, uint32_t bo, uint32_t s, uint32_t e,
-                                          uint32_t slot0, uint32_t& cnt, uint32_t& kb, uint32_t& vb) {
+                                          uint32_t slot0, uint32_t& cnt, uint32_t& kb, uint32_t& vb, bool& all1) {
   cnt = kb = vb = 0;
+  all1 = false;
   if (!(s < e)) return false;
   uint32_t p = s, prevlen = 0, bad = 0, ssh = 0, svl = 0, shl = 0, c = 0;
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
@@ -1317,6 +1318,7 @@ __device__ __forceinline__ bool walk_pos2(const uint8_t* stage, uint16_t* pos, u
   cnt = c;
   vb = svl;
   kb = ssh + (p - s) - shl - svl;   // sum(shared + non_shared): p - s = sum(header + ns + vl)
+  all1 = shl == 3u * c;             // every header 1-byte varints: walk_pos would have accepted it
   return p == e && bad == 0u;
 }
 
@@ -1443,7 +1445,12 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
 // publish A(t), then the block / interval bases the copy and the look-back read.
 // Cross-lane traffic uses readlane / DPP / bpermute (no LDS round trips before the walk).
 template <class P>
-__device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint32_t t, int lane, Stamps& ST) {
+// wmode (wave 0's, carried across its tiles): 1 = walk with walk_pos2 first.  A wave walks its
+// intervals in lockstep, so one interval with a 2-byte varint (cfg3: 8 % of keys have a suffix
+// of >= 128 bytes, ~3/4 of intervals one such entry) made every lane walk twice (walk_pos, then
+// walk_pos2); the previous tile decides which walk goes first.
+__device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint32_t t, int lane, Stamps& ST,
+                                          uint32_t& wmode) {
   uint32_t b0, nb;
   tile_span(a, t, b0, nb);
   // trailers (Block::init, src/block.rs:16-49): lane = block
@@ -1472,20 +1479,34 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   ST.hit(9);
   const bool fl = (uint32_t)lane < nint;
   uint32_t cnt = 0, kb = 0, vb = 0;
-  bool wok = false;
+  bool wok = false, need2 = false;
   if (fl) {
     const uint32_t i = (uint32_t)lane - jb0;
     const uint32_t s = lds_rd32(B.stage, jbo + jR + 4u * i);
     const uint32_t e = (i + 1 < jn) ? lds_rd32(B.stage, jbo + jR + 4u * (i + 1)) : jR;
     ST.hit(10);
     const uint32_t slot0 = (uint32_t)lane * kP2Spi;
-    wok = e <= jR && walk_pos(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb);
-    if (!wok) wok = e <= jR && walk_pos2(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb);
+    bool all1 = true;
+    // (PipeLarge only: the fused-verify kernels are at their VGPR cap, and PipeSmall's cfg2
+    // headers are all 1-byte varints -- the extra code cost its launch 1 %)
+    constexpr bool kAdaptive = P::NBUF == 2 && !P::VERIFY;
+    if (!kAdaptive || wmode == 0u) {
+      wok = e <= jR && walk_pos(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb);
+      if (!wok) {
+        wok = e <= jR && walk_pos2(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb, all1);
+        all1 = false;   // walk_pos failed here
+      }
+    } else {
+      wok = e <= jR && walk_pos2(B.stage, B.pos, jbo, s, e, slot0, cnt, kb, vb, all1);
+      all1 = all1 || !wok;   // a rejected interval goes to the careful walk either way
+    }
+    need2 = !all1;
     if (!wok) wok = walk_careful_pos(B.stage, B.pos, jbo, jL, jR, s, e, slot0, cnt, kb, vb);
     B.iraw[lane] = (uint8_t)(cnt < 255u ? cnt : 255u);
     B.iblk[lane] = (uint8_t)j;
   }
   ST.hit(2);
+  if constexpr (P::NBUF == 2 && !P::VERIFY) wmode = __ballot(need2) != 0ull ? 1u : 0u;
   // a block with a rejected interval is irregular
   const uint64_t failm = __ballot(fl && !wok);
   {
@@ -2108,13 +2129,14 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   TL(1);
   if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
   uint64_t ntl = 0;
+  uint32_t wmode = 0;   // wave 0: which interval walk goes first (pipe_walk)
 
   if constexpr (serial2) {
     for (uint32_t it = 0; it < nloc; ++it) {
       PipeBuf<P>& C = S.buf[it & 1u];
       const uint32_t tc = g + it * G;
       if (wv == 0) {
-        pipe_walk(C, a, tc, lane, ST);
+        pipe_walk(C, a, tc, lane, ST, wmode);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&S.pub, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         ST.hit(3);
@@ -2166,7 +2188,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       if (wv == 0) {
         if (k1 < nloc) {
           wait_flag(a, &S.staged, (k1 + 1) * (uint32_t)P::LOADW);
-          pipe_walk(S.buf[k1 & 1u], a, g + k1 * G, lane, ST);
+          pipe_walk(S.buf[k1 & 1u], a, g + k1 * G, lane, ST, wmode);
           if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         ST.hit(3);
@@ -2227,7 +2249,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     if (wv == 0) {
       // walk first: the aggregate A(tile it+1) is published as early as possible
       if (k1 < nloc) {
-        pipe_walk(S.buf[k1 % P::NBUF], a, g + k1 * G, lane, ST);
+        pipe_walk(S.buf[k1 % P::NBUF], a, g + k1 * G, lane, ST, wmode);
         if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       ST.hit(3);

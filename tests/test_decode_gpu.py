@@ -322,3 +322,37 @@ def test_key_tails_dense_and_planes(oracle):
         orc = run_both(oracle, blocks, rng=np.random.default_rng(5))
         assert (orc.status == 0).all()
         assert int(np.diff(orc.key_end.astype(np.int64)).max()) > 200
+
+
+def test_pipelarge_walk_modes_alternate(oracle):
+    """PipeLarge's walker picks its first interval walk from the previous tile (1-byte headers ->
+    walk_pos, 2-byte -> walk_pos2).  One batch alternates 64 KiB-class blocks of 16 B keys
+    (1-byte headers), long-key blocks (2-byte non_shared varints), blocks with 20 KB values
+    (3-byte varints: the careful walk) and corrupted copies, so the mode flips both ways."""
+    from mtblx import synth
+    rng = np.random.default_rng(0x3a1c)
+    d2, o2, l2 = synth.cfg2_file(12, block_size=65536)
+    short = [bytes(d2[int(o): int(o) + int(n)]) for o, n in zip(o2, l2)]
+    longk = []
+    while len(longk) < 8:
+        b = oracle.build_block(_tail_records(rng, 520, "counter"), restart_interval=16)
+        if 49200 < len(b) <= 65000:
+            longk.append(b)
+    big = []
+    for _ in range(3):
+        recs = corpus.random_records(rng, 40, 8, 24, 16, 64)
+        k, _ = recs[17]
+        recs[17] = (k, bytes(rng.integers(0, 256, 20000, dtype=np.uint8)))
+        big.append(oracle.build_block(recs, restart_interval=16))
+    blocks = []
+    for i in range(12):
+        blocks.append(short[i])
+        if i < 8:
+            blocks.append(longk[i])
+        if i % 4 == 1:
+            blocks.append(big[i // 4])
+        if i % 3 == 2:
+            blocks.append(corpus.mutate(rng, longk[i % 8]))
+    assert max(len(b) for b in blocks) > 49200 and max(len(b) for b in blocks) <= 65600
+    orc = run_both(oracle, blocks, rng=np.random.default_rng(9))
+    assert int((orc.status == 0).sum()) >= 23

@@ -89,6 +89,9 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 #endif
 // LDS-DMA of the block bytes with the non-temporal policy (aux = 2): the blocks are read once, so
 // they stay out of the L2s the byte-granular key stores merge in (cfg2 +5 %, 64 KiB +4 %)
+#ifndef MTBLX_DMA_AUX   // cache-policy bits of the LDS-DMA loads (2 = non-temporal)
+#define MTBLX_DMA_AUX 2
+#endif
 #ifndef MTBLX_NT_LOADS
 #define MTBLX_NT_LOADS 1
 #endif
@@ -1394,12 +1397,12 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
     if (mlo <= part) m = part;
     const uint8_t* gp = a.data + r0 + 16ull * ((uint64_t)m * kWave + (uint32_t)lane);
     for (; m < mfull; m += P::LOADW, gp += 16 * kWave * P::LOADW)
-      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? 2 : 0);
+      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
     for (; m * kWave < nch && m < mhi; m += P::LOADW) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
       if (c < nfull)
-        __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? 2 : 0);
+        __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
       else if (c < nch)
         *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
     }
@@ -1428,7 +1431,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
           if (c < nch) {
             if (go + 16 <= a.data_len && ((base + go) & 15ull) == 0)
               __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + so + 1024 * m), 16, 0,
-                                               MTBLX_NT_LOADS ? 2 : 0);
+                                               MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
             else
               *reinterpret_cast<uint4*>(B.stage + so + 16 * c) = load_chunk(a, go);
           }

@@ -356,3 +356,37 @@ def test_pipelarge_walk_modes_alternate(oracle):
     assert max(len(b) for b in blocks) > 49200 and max(len(b) for b in blocks) <= 65600
     orc = run_both(oracle, blocks, rng=np.random.default_rng(9))
     assert int((orc.status == 0).sum()) >= 23
+
+
+def test_pipelarge_tile_counts_one_workspace(oracle):
+    """PipeLarge's late-walk pipeline with 1, 2, 3, 257 and 513 tiles (workgroups with 1..3 tiles:
+    the fill and drain of the two-buffer schedule), one workspace reused across the batches, and
+    long-key blocks mixed in so the walk order switches mid-launch."""
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(513, block_size=65536)
+    rng = np.random.default_rng(0x1a7e)
+    longk = []
+    while len(longk) < 4:
+        b = oracle.build_block(_tail_records(rng, 520, "counter"), restart_interval=16)
+        if 49200 < len(b) <= 65000:
+            longk.append(b)
+    blocks = [bytes(data[int(o): int(o) + int(n)]) for o, n in zip(off, ln)]
+    for i, b in enumerate(longk):
+        blocks[100 * i + 7] = b
+    d, o, l = corpus.pack(blocks)
+    ws = codec.Workspace(len(blocks))
+    exp_all = oracle.decode_blocks(d, o, l)
+    assert (exp_all.status == 0).all()
+    for n in (1, 2, 3, 257, 513, 2):
+        batch = codec.DeviceBatch.from_host(d, o[:n], l[:n])
+        probe = codec.DecodedBlocks(batch.nblk, 0, 0, 0)
+        codec.count_blocks(batch, probe, ws)
+        torch.cuda.synchronize()
+        nr, kb, vb, fl = probe.totals_host()
+        assert fl == 0 and nr == int(exp_all.nrec[:n].sum())
+        out = codec.DecodedBlocks(batch.nblk, nr, kb, vb)
+        codec.decode_into(batch, out, ws)
+        torch.cuda.synchronize()
+        assert_same(out.to_host(), oracle.decode_blocks(d, o[:n], l[:n]), n)

@@ -257,11 +257,14 @@ class Reader;
 // iteration reaches, in growing chunks); the host keeps the reference's state: first, valid,
 // the index position and block_offset (0 from the constructors, never updated by next(), so a
 // seek landing on a block at that offset re-seeks the block the iterator holds, with that
-// iterator's key capacity).  next() returns a view valid until the next next()/seek(); it
-// throws Error where the reference returns Some(Err) (the iterator is then exhausted), Panic
-// where it panics or never returns.  Approximation: the index seek runs on a fresh index
-// iterator (differs from the reference only when the index block's restart entries are
-// corrupt, which the index checksum catches unless verification is off).
+// iterator's key capacity).  seek() re-seeks the LIVE index iterator (:303) and seeks the data
+// block to the landed index entry's key (`key` is shadowed at :305).  On a regular index block
+// (mtblx_entry_offsets) the index position is a directory entry; on a corrupt one (read with
+// verification off) the live index iterator is driven on the device with
+// mtblx_block_seek_batch (seek with its key capacity, early return kept, resume), on the scan
+// chain or off it.  next() returns a view valid until the next next()/seek(); it throws Error
+// where the reference returns Some(Err) (the iterator is then exhausted), Panic where it
+// panics or never returns.
 class ReaderIntoIter {
  public:
   std::optional<Record> next();
@@ -302,12 +305,31 @@ class ReaderIntoIter {
     int code = 0;    // 0 ok, 1 panic (framing / checksum), 2 Err(Io), 3 Err(InvalidBlock), 4 >= 4 GiB
     Bi bi;
   };
+  struct IxList {    // the live index iterator of an irregular index: the records next() visits
+    Bi b;            // from its position on (b.pos), emitted by mtblx_block_seek_batch
+    uint64_t stop_off = 0;
+    int64_t ord0 = -1;   // directory entry of record 0 when on the scan chain, else -1
+    bool valid() const { return b.pos < b.n(); }
+    uint64_t kcap() const { return valid() ? b.kcaps[b.pos] : b.kcap_end; }
+  };
+  static constexpr uint64_t kIxEmit = 256;   // index records per emission
+  struct EmitResult {
+    mtblx_block_seek res;
+    Bi b;
+  };
   ReaderIntoIter(const Reader* r, Kind t, Bytes k) : r_(r), type_(t), k_(std::move(k)) {}
   void init_iter();
   void init_from(const Bytes& key);
   Bi load(size_t i);
+  // BlockIter::seek / seek_to_first / resume on one block content, no status checks
+  static EmitResult emit(const Content& c, const Bytes* key, int first, uint64_t kcap, uint64_t max_records,
+                         uint64_t resume_off = 0);
   static Bi seek_block(const Content& c, const Bytes* key, uint64_t kcap);   // key null: seek_to_first
   uint64_t kcap_now(Bi& b);
+  void ix_seek(const Bytes& key);
+  bool ix_next();
+  Bi ix_load();
+  IxList ix_list(EmitResult&& e, int64_t ord0) const;
   const Reader* r_;
   Kind type_;
   Bytes k_;
@@ -315,8 +337,11 @@ class ReaderIntoIter {
   bool first_ = true, valid_ = true;
   std::optional<Bi> bi_;
   int64_t e_ = -1;                  // index position, -1: the index iterator is invalid
+  std::optional<IxList> ix_;        // irregular index: the live index iterator
   size_t chunk0_ = 0, grow_ = 1;
   std::vector<Loaded> chunk_;
+  size_t vchunk0_ = 0;              // irregular index: prefetched blocks of ix_ (by record)
+  std::vector<Loaded> vchunk_;
 };
 
 class Reader {
@@ -354,10 +379,29 @@ class Reader {
     return it;
   }
   mtblx_index_seek index_seek(const Bytes& key) const;
+  Bytes index_key(size_t i) const {   // separator key of directory entry i
+    const uint32_t a = i ? ikend_[i - 1] : 0;
+    return Bytes(ikeys_.begin() + a, ikeys_.begin() + ikend_[i]);
+  }
+  void index_chain() const;
+  bool regular() const { index_chain(); return regular_; }
+  std::optional<size_t> chain_ordinal(uint64_t entry) const;
   size_t ordinal(uint64_t entry) const;
+  ReaderIntoIter::Content index_content() const {
+    return ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), index_off_, index_len_};
+  }
   ReaderIntoIter::Content seek_content(const mtblx_index_seek& s) const;
+  ReaderIntoIter::Content value_content(const Bytes& value) const;
+  struct Framing {   // block_at_index + Reader::block framing of some index entries
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    std::vector<int32_t> st;
+    std::vector<uint64_t> block_off;   // the block offset (for contents >= 4 GiB)
+  };
+  Framing frame_values(const std::vector<Bytes>& values) const;
   std::vector<ReaderIntoIter::Loaded> load_range(size_t i0, size_t i1) const;
-  void load_big(size_t i, ReaderIntoIter::Loaded& L) const;
+  std::vector<ReaderIntoIter::Loaded> load_framed(const Framing& f) const;
+  void load_big(uint64_t block_off, ReaderIntoIter::Loaded& L) const;
   Bytes file_;
   detail::DevBuf dfile_;
   bool verify_;
@@ -369,10 +413,12 @@ class Reader {
   std::vector<uint64_t> boff_;
   std::vector<uint32_t> blen_;
   std::vector<int32_t> dst_;
+  Bytes ikeys_;                  // the index block's keys (separators) and END offsets
+  std::vector<uint32_t> ikend_;
   detail::DevBuf d_off_, d_len_;
   std::vector<std::pair<uint32_t, uint64_t>> big_;   // entries whose content is >= 4 GiB: block offset
   mutable std::vector<uint64_t> eoffs_;
-  mutable bool eoffs_known_ = false;
+  mutable bool eoffs_known_ = false, regular_ = false;
   mutable std::optional<size_t> len_;
 };
 
@@ -414,6 +460,8 @@ inline Reader::Reader(const uint8_t* data, size_t len, bool verify) : file_(data
   if (idx.status[0] == MTBLX_ST_INVALID_BLOCK) throw Error(MtblError::InvalidBlock);   // src/reader.rs:76
   nent_ = idx.nrec[0];
   index_status_ = idx.status[0];
+  ikeys_ = idx.keys;
+  ikend_.assign(idx.key_end.begin(), idx.key_end.begin() + nent_);
   // block_at_index + Reader::block framing for every index entry (device); checksums are
   // checked per block when the iteration loads it
   boff_.assign(nent_, 0);
@@ -445,15 +493,53 @@ inline Reader::Reader(const uint8_t* data, size_t len, bool verify) : file_(data
 // blocks [i0, i1) as next() loads them: Reader::block (framing, checksum, host decompression
 // -- compression stays on the host per the north star) + one device decode of the range
 inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t i1) const {
+  Framing f;
+  f.off.assign(boff_.begin() + i0, boff_.begin() + i1);
+  f.len.assign(blen_.begin() + i0, blen_.begin() + i1);
+  f.st.assign(dst_.begin() + i0, dst_.begin() + i1);
+  f.block_off.assign(i1 - i0, 0);
+  for (const auto& e : big_)
+    if (e.first >= i0 && e.first < i1) f.block_off[e.first - i0] = e.second;
+  return load_framed(f);
+}
+
+// block_at_index + Reader::block framing of arbitrary index values on the device (mtblx_block_dir)
+inline Reader::Framing Reader::frame_values(const std::vector<Bytes>& values) const {
   using namespace detail;
-  const uint32_t n = (uint32_t)(i1 - i0);
+  const uint32_t n = (uint32_t)values.size();
+  Framing f;
+  Bytes blob;
+  std::vector<uint32_t> vend(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    blob.insert(blob.end(), values[i].begin(), values[i].end());
+    vend[i] = (uint32_t)blob.size();
+  }
+  if (blob.empty()) blob.push_back(0);
+  DevBuf d_v = upload(blob.data(), blob.size()), d_ve = upload(vend.data(), n);
+  DevBuf d_o(8ull * n), d_l(4ull * n), d_s(4ull * n);
+  abi_check(mtblx_block_dir(dfile_.as<uint8_t>(), file_.size(), version_, d_v.as<uint8_t>(), d_ve.as<uint32_t>(), 0, n,
+                            d_o.as<uint64_t>(), d_l.as<uint32_t>(), d_s.as<int32_t>(), nullptr),
+            "mtblx_block_dir");
+  hip_check(hipDeviceSynchronize(), "sync");
+  f.off = download<uint64_t>(d_o.p, n);
+  f.len = download<uint32_t>(d_l.p, n);
+  f.st = download<int32_t>(d_s.p, n);
+  f.block_off.assign(n, 0);
+  for (uint32_t i = 0; i < n; ++i)
+    if (f.st[i] == MTBLX_DIR_UNSUPPORTED) mtblx_varint_decode64(values[i].data(), values[i].size(), &f.block_off[i]);
+  return f;
+}
+
+inline std::vector<ReaderIntoIter::Loaded> Reader::load_framed(const Framing& f) const {
+  using namespace detail;
+  const uint32_t n = (uint32_t)f.off.size();
   std::vector<ReaderIntoIter::Loaded> out(n);
   std::vector<uint8_t> bad(n, 0);
-  std::vector<uint32_t> l2(blen_.begin() + i0, blen_.begin() + i1);
+  std::vector<uint32_t> l2(f.len);
   for (uint32_t i = 0; i < n; ++i)
-    if (dst_[i0 + i] != MTBLX_DIR_OK) l2[i] = 0;   // never decoded: the iteration stops before it
-  DevBuf d_l2 = upload(l2.data(), n);
-  const uint64_t* d_o = d_off_.as<uint64_t>() + i0;
+    if (f.st[i] != MTBLX_DIR_OK) l2[i] = 0;   // never decoded: the iteration stops before it
+  DevBuf d_l2 = upload(l2.data(), n), d_off = upload(f.off.data(), n);
+  const uint64_t* d_o = d_off.as<uint64_t>();
   const uint32_t mx = n ? *std::max_element(l2.begin(), l2.end()) : 0;
   if (verify_ && n) {
     DevBuf d_bad(n);
@@ -472,7 +558,7 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t 
     std::vector<uint32_t> sn(n, 0);
     std::vector<int32_t> zst(n, 0);
     for (uint32_t i = 0; i < n; ++i)
-      if (dst_[i0 + i] == MTBLX_DIR_OK && !bad[i]) { so[i] = boff_[i0 + i]; sn[i] = blen_[i0 + i]; }
+      if (f.st[i] == MTBLX_DIR_OK && !bad[i]) { so[i] = f.off[i]; sn[i] = f.len[i]; }
     uint8_t* hb = nullptr;
     mtblx_decompress_blocks(static_cast<uint32_t>(meta_.compression_algorithm), file_.data(), so.data(), sn.data(), n,
                             16, &hb, uoff.data(), ulen.data(), zst.data());
@@ -495,18 +581,18 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t 
   }
   for (uint32_t i = 0; i < n; ++i) {
     auto& L = out[i];
-    if (dst_[i0 + i] == MTBLX_DIR_UNSUPPORTED) {   // content >= 4 GiB (u64 restart array)
-      load_big(i0 + i, L);
+    if (f.st[i] == MTBLX_DIR_UNSUPPORTED) {   // content >= 4 GiB (u64 restart array)
+      load_big(f.block_off[i], L);
       continue;
     }
-    if (dst_[i0 + i] != MTBLX_DIR_OK || bad[i]) { L.code = 1; continue; }
+    if (f.st[i] != MTBLX_DIR_OK || bad[i]) { L.code = 1; continue; }
     if (zerr[i]) { L.code = 2; continue; }
     const int32_t s = dec.status[i];
     if (s == MTBLX_ST_INVALID_BLOCK) { L.code = 3; continue; }
     if (s == MTBLX_ST_UNSUPPORTED) { L.code = 4; continue; }
     auto& b = L.bi;
     if (ubuf) b.c = ReaderIntoIter::Content{ubuf, ubuf->as<uint8_t>(), uoff[i], ul[i]};
-    else b.c = ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), boff_[i0 + i], blen_[i0 + i]};
+    else b.c = ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), f.off[i], f.len[i]};
     b.end = s == MTBLX_ST_CORRUPT ? MTBLX_EMIT_PANIC : s == MTBLX_ST_LOOP ? MTBLX_EMIT_LOOP : MTBLX_EMIT_END;
     const uint64_t r0 = dec.rec_base[i], kb = dec.key_base[i], vb = dec.val_base[i];
     uint64_t kend = 0, vend = 0;
@@ -524,11 +610,8 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_range(size_t i0, size_t 
 
 // Reader::block + Block::init + the scan of a block >= 4 GiB: framing and checksum on the host
 // (mtblx_frame_block), the scan on the device (the emitting block seek, seek_to_first)
-inline void Reader::load_big(size_t i, ReaderIntoIter::Loaded& L) const {
+inline void Reader::load_big(uint64_t boff, ReaderIntoIter::Loaded& L) const {
   if (meta_.compression_algorithm != 0) throw std::runtime_error("compressed block >= 4 GiB");
-  uint64_t boff = 0;
-  for (const auto& e : big_)
-    if (e.first == i) boff = e.second;
   uint64_t coff = 0, clen = 0;
   int panic = 0;
   if (mtblx_frame_block(file_.data(), file_.size(), version_, boff, verify_ ? 1 : 0, &coff, &clen, &panic) != MTBLX_OK) {
@@ -570,21 +653,54 @@ inline mtblx_index_seek Reader::index_seek(const Bytes& key) const {
   return download<mtblx_index_seek>(d_out.p, 1)[0];
 }
 
-inline size_t Reader::ordinal(uint64_t entry) const {
+// the index scan chain's entry offsets and whether the index block is regular (mtblx.h)
+inline void Reader::index_chain() const {
   using namespace detail;
-  if (!eoffs_known_) {
-    DevBuf d_offs(8ull * std::max<uint32_t>(nent_, 1)), d_cnt(8);
-    abi_check(mtblx_entry_offsets(dfile_.as<uint8_t>() + index_off_, index_len_, d_offs.as<uint64_t>(), nent_,
-                                  d_cnt.as<uint64_t>(), nullptr),
-              "mtblx_entry_offsets");
-    hip_check(hipDeviceSynchronize(), "sync");
-    const uint64_t cnt = std::min<uint64_t>(download<uint64_t>(d_cnt.p, 1)[0], nent_);
-    eoffs_ = download<uint64_t>(d_offs.p, cnt);
-    eoffs_known_ = true;
-  }
+  if (eoffs_known_) return;
+  const uint64_t cap = index_len_ / 3 + 1;   // an entry takes >= 3 bytes
+  DevBuf d_offs(8ull * cap), d_cnt(8), d_reg(4);
+  abi_check(mtblx_entry_offsets(dfile_.as<uint8_t>() + index_off_, index_len_, d_offs.as<uint64_t>(), cap,
+                                d_cnt.as<uint64_t>(), d_reg.as<uint32_t>(), nullptr),
+            "mtblx_entry_offsets");
+  hip_check(hipDeviceSynchronize(), "sync");
+  const uint64_t cnt = std::min<uint64_t>(download<uint64_t>(d_cnt.p, 1)[0], cap);
+  eoffs_ = download<uint64_t>(d_offs.p, cnt);
+  regular_ = download<uint32_t>(d_reg.p, 1)[0] == 1 && index_status_ == MTBLX_ST_OK;
+  eoffs_known_ = true;
+}
+
+inline std::optional<size_t> Reader::chain_ordinal(uint64_t entry) const {
+  index_chain();
   const auto it = std::lower_bound(eoffs_.begin(), eoffs_.end(), entry);
-  if (it == eoffs_.end() || *it != entry) throw std::runtime_error("index seek landed off the index scan chain");
+  if (it == eoffs_.end() || *it != entry) return std::nullopt;
   return (size_t)(it - eoffs_.begin());
+}
+
+inline size_t Reader::ordinal(uint64_t entry) const {   // a regular index's landing
+  const auto o = chain_ordinal(entry);
+  if (!o || *o >= nent_) throw std::runtime_error("index seek landed off the directory of a regular index");
+  return *o;
+}
+
+// Reader::block (src/reader.rs:139-175) at the offset an index value names: framing and
+// checksum (host), decompression (host) -> the content BlockIter reads; throws like the crate
+inline ReaderIntoIter::Content Reader::value_content(const Bytes& value) const {
+  using namespace detail;
+  uint64_t boff = 0;
+  if (mtblx_varint_decode64(value.data(), value.size(), &boff) < 0) throw Panic("varint_decode64 of the index value");
+  uint64_t coff = 0, clen = 0;
+  int panic = 0;
+  mtblx_frame_block(file_.data(), file_.size(), version_, boff, verify_ ? 1 : 0, &coff, &clen, &panic);
+  if (panic) throw Panic("Reader::block: framing / checksum");
+  if (meta_.compression_algorithm == 0) return ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), coff, clen};
+  uint8_t* out = nullptr;
+  uint64_t n = 0;
+  if (mtblx_decompress(static_cast<uint32_t>(meta_.compression_algorithm), file_.data() + coff, clen, &out, &n) !=
+      MTBLX_CODEC_OK)
+    throw Error(MtblError::Io);
+  auto own = std::make_shared<DevBuf>(upload(out, n ? n : 1));
+  mtblx_free(out);
+  return ReaderIntoIter::Content{own, own->as<uint8_t>(), 0, n};
 }
 
 inline ReaderIntoIter::Content Reader::seek_content(const mtblx_index_seek& s) const {
@@ -606,18 +722,20 @@ inline ReaderIntoIter::Content Reader::seek_content(const mtblx_index_seek& s) c
   return ReaderIntoIter::Content{own, own->as<uint8_t>(), 0, n};
 }
 
-inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Bytes* key, uint64_t kcap) {
+inline ReaderIntoIter::EmitResult ReaderIntoIter::emit(const Content& c, const Bytes* key, int first, uint64_t kcap,
+                                                       uint64_t max_records, uint64_t resume_off) {
   using namespace detail;
   mtblx_block_seek q{};
   q.data_off = c.off;
   q.data_len = c.len;
   q.kcap = kcap;
-  q.max_records = ~0ull >> 2;
-  q.first = key ? 0 : 1;
+  q.max_records = max_records;
+  q.first = first;
+  q.resume_off = resume_off;
   // output sized exactly from a first counting pass when the block is big (>= 4 GiB blocks)
   const bool big = c.len > (64ull << 20);
-  uint64_t rec_cap = big ? 4096 : c.len / 3 + 1, keys_cap = big ? 1 << 20 : 2 * c.len + 64,
-           vals_cap = big ? 1 << 20 : c.len + 16;
+  uint64_t rec_cap = std::min<uint64_t>(max_records, big ? 4096 : c.len / 3 + 1),
+           keys_cap = big ? 1 << 20 : 2 * c.len + 64, vals_cap = big ? 1 << 20 : c.len + 16;
   const Bytes none;
   const uint64_t kend = key ? key->size() : 0;
   DevBuf d_key = upload_key(key ? *key : none), d_kend = upload(&kend, 1);
@@ -629,31 +747,37 @@ inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Byt
                                      d_ve.as<uint64_t>(), d_kc.as<uint64_t>(), rec_cap, nullptr),
               "mtblx_block_seek_batch");
     hip_check(hipDeviceSynchronize(), "sync");
-    const mtblx_block_seek res = download<mtblx_block_seek>(d_q.p, 1)[0];
-    if (res.end == MTBLX_EMIT_OVERFLOW) {
-      rec_cap = res.nrec;
-      keys_cap = res.key_bytes;
-      vals_cap = res.val_bytes;
+    EmitResult r;
+    r.res = download<mtblx_block_seek>(d_q.p, 1)[0];
+    if (r.res.end == MTBLX_EMIT_OVERFLOW) {
+      rec_cap = r.res.nrec;
+      keys_cap = r.res.key_bytes;
+      vals_cap = r.res.val_bytes;
       continue;
     }
-    if (res.status == MTBLX_SEEK_ERR) throw Error(MtblError::InvalidBlock);
-    if (res.status == MTBLX_SEEK_PANIC) throw Panic("BlockIter::seek");
-    if (res.status == MTBLX_SEEK_LOOP) throw Panic("BlockIter::seek never returns");
-    if (res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: block >= 4 GiB or key > 64 KiB");
-    Bi b;
+    Bi& b = r.b;
     b.c = c;
-    b.end = res.end;
-    b.ke = download<uint64_t>(d_ke.p, res.nrec);
-    b.ve = download<uint64_t>(d_ve.p, res.nrec);
-    b.kcaps = download<uint64_t>(d_kc.p, res.nrec);
+    b.end = r.res.end;
+    b.ke = download<uint64_t>(d_ke.p, r.res.nrec);
+    b.ve = download<uint64_t>(d_ve.p, r.res.nrec);
+    b.kcaps = download<uint64_t>(d_kc.p, r.res.nrec);
     b.kcaps_known = true;
-    b.kcap_end = res.kcap;
-    b.keys = download<uint8_t>(d_k.p, res.key_bytes);
-    b.vals = download<uint8_t>(d_v.p, res.val_bytes);
-    if (res.has_val) b.last_val = download<uint8_t>(c.base + c.off + res.last_voff, res.last_vlen);
-    return b;
+    b.kcap_end = r.res.kcap;
+    b.keys = download<uint8_t>(d_k.p, r.res.key_bytes);
+    b.vals = download<uint8_t>(d_v.p, r.res.val_bytes);
+    if (r.res.has_val) b.last_val = download<uint8_t>(c.base + c.off + r.res.last_voff, r.res.last_vlen);
+    return r;
   }
   throw std::runtime_error("mtblx_block_seek_batch: output sizes did not converge");
+}
+
+inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Bytes* key, uint64_t kcap) {
+  EmitResult r = emit(c, key, key ? 0 : 1, kcap, ~0ull >> 2);
+  if (r.res.status == MTBLX_SEEK_ERR) throw Error(MtblError::InvalidBlock);
+  if (r.res.status == MTBLX_SEEK_PANIC) throw Panic("BlockIter::seek");
+  if (r.res.status == MTBLX_SEEK_LOOP) throw Panic("BlockIter::seek never returns");
+  if (r.res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: block >= 4 GiB or key > 64 KiB");
+  return std::move(r.b);
 }
 
 // the key Vec's capacity of the held iterator now (parse_next_key's END leaves it unchanged)
@@ -699,22 +823,99 @@ inline ReaderIntoIter::Bi ReaderIntoIter::load(size_t i) {
   return L.bi;
 }
 
+inline ReaderIntoIter::IxList ReaderIntoIter::ix_list(EmitResult&& e, int64_t ord0) const {
+  if (e.res.status == MTBLX_SEEK_PANIC) throw Panic("index seek");
+  if (e.res.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
+  if (e.res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: index key > 64 KiB");
+  IxList l;
+  l.b = std::move(e.b);
+  l.stop_off = e.res.stop_off;
+  l.ord0 = ord0;
+  return l;
+}
+
 inline void ReaderIntoIter::init_iter() {   // new (src/reader.rs:231-254)
   if (r_->nent_ == 0) {
     if (r_->index_status_ == MTBLX_ST_CORRUPT) throw Panic("index block: first entry");
+    if (!r_->regular()) ix_ = IxList{};
     return;
   }
-  e_ = 0;
+  if (r_->regular()) {
+    e_ = 0;
+  } else {   // the scan's own chain = the directory, with its key capacities
+    ix_ = ix_list(emit(r_->index_content(), nullptr, 1, 0, kIxEmit), 0);
+  }
   bi_ = load(0);
 }
 
 inline void ReaderIntoIter::init_from(const Bytes& key) {   // new_from (src/reader.rs:256-279)
+  if (!r_->regular()) {   // a fresh live index iterator, seeked
+    ix_ = IxList{};
+    ix_seek(key);
+    if (!ix_->valid()) return;
+    bi_ = seek_block(r_->value_content(ix_->b.rec(ix_->b.pos).val_bytes()), &key, 0);
+    return;
+  }
   const mtblx_index_seek s = r_->index_seek(key);
   if (s.status == MTBLX_SEEK_PANIC) throw Panic("index seek");
   if (s.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
   if (!s.valid) return;
   e_ = (int64_t)r_->ordinal(s.entry);
   bi_ = seek_block(r_->seek_content(s), &key, 0);
+}
+
+// index_iter.seek(key) on the live iterator of an irregular index (src/block.rs:154-194)
+inline void ReaderIntoIter::ix_seek(const Bytes& key) {
+  EmitResult e = emit(r_->index_content(), &key, 0, ix_->kcap(), kIxEmit);
+  if (e.res.status == MTBLX_SEEK_OK && e.res.early) return;   // corrupt restart: the old position stays
+  int64_t ord0 = -1;
+  if (e.res.status == MTBLX_SEEK_OK && e.res.nrec) {
+    const auto o = r_->chain_ordinal(e.res.entry);
+    if (o) ord0 = (int64_t)*o;
+  }
+  ix_ = ix_list(std::move(e), ord0);
+  vchunk_.clear();
+}
+
+// index_iter.next() (src/block.rs:196-202) on the live iterator
+inline bool ReaderIntoIter::ix_next() {
+  IxList& ix = *ix_;
+  if (!ix.valid()) return false;
+  if (ix.b.pos + 1 < ix.b.n()) { ++ix.b.pos; return true; }
+  if (ix.b.end == MTBLX_EMIT_END) { ix.b.pos = ix.b.n(); return false; }
+  if (ix.b.end == MTBLX_EMIT_PANIC) throw Panic("index block: next entry");
+  if (ix.b.end == MTBLX_EMIT_LOOP) return true;   // a zero-progress entry: the same record again
+  // EMIT_MAX: the entry after the last record, parsed from that record's key and capacity
+  const Bytes k = ix.b.rec(ix.b.n() - 1).key_bytes();
+  EmitResult e = emit(r_->index_content(), &k, 2, ix.b.kcaps.back(), kIxEmit, ix.stop_off);
+  if (e.res.status == MTBLX_SEEK_PANIC) throw Panic("index block: next entry");
+  const int64_t ord0 = ix.ord0 < 0 ? -1 : ix.ord0 + (int64_t)ix.b.n();
+  ix_ = ix_list(std::move(e), ord0);
+  vchunk_.clear();
+  return ix_->valid();
+}
+
+// block_at_index of the live index iterator's record (Reader::block + seek_to_first)
+inline ReaderIntoIter::Bi ReaderIntoIter::ix_load() {
+  const IxList& ix = *ix_;
+  const size_t pos = ix.b.pos;
+  if (ix.ord0 >= 0 && (size_t)ix.ord0 + pos < r_->nent_) return load((size_t)ix.ord0 + pos);
+  if (vchunk_.empty() || pos < vchunk0_ || pos >= vchunk0_ + vchunk_.size()) {
+    const size_t n = std::min<size_t>(ix.b.n() - pos, grow_);
+    grow_ = std::min<size_t>(2 * grow_, 256);
+    std::vector<Bytes> vals;
+    for (size_t q = pos; q < pos + n; ++q) vals.push_back(ix.b.rec(q).val_bytes());
+    vchunk_ = r_->load_framed(r_->frame_values(vals));
+    vchunk0_ = pos;
+  }
+  Loaded& L = vchunk_[pos - vchunk0_];
+  switch (L.code) {
+    case 1: throw Panic("Reader::block: framing / checksum");
+    case 2: throw Error(MtblError::Io);
+    case 3: throw Error(MtblError::InvalidBlock);
+    case 4: throw std::runtime_error("block >= 4 GiB");
+  }
+  return L.bi;
 }
 
 inline std::optional<Record> ReaderIntoIter::next() {   // src/reader.rs:337-405
@@ -726,16 +927,22 @@ inline std::optional<Record> ReaderIntoIter::next() {   // src/reader.rs:337-405
   if (b->pos == b->n() && b->end == MTBLX_EMIT_LOOP) throw Panic("zero-progress entry: the reference never returns");
   if (b->pos == b->n()) {
     valid_ = false;
-    if (e_ < 0) return std::nullopt;
-    if ((size_t)e_ + 1 >= r_->nent_) {       // index_iter.next() past the last entry
-      e_ = -1;
-      if (r_->index_status_ == MTBLX_ST_CORRUPT) throw Panic("index block: next entry");
-      if (r_->index_status_ == MTBLX_ST_LOOP) throw Panic("index block never returns");
-      return std::nullopt;
+    if (ix_) {                                // irregular index: the live index iterator
+      if (!ix_next()) return std::nullopt;
+      Bi nb = ix_load();                      // Some(Err(e)) throws; valid stays false
+      bi_ = std::move(nb);
+    } else {
+      if (e_ < 0) return std::nullopt;
+      if ((size_t)e_ + 1 >= r_->nent_) {       // index_iter.next() past the last entry
+        e_ = -1;
+        if (r_->index_status_ == MTBLX_ST_CORRUPT) throw Panic("index block: next entry");
+        if (r_->index_status_ == MTBLX_ST_LOOP) throw Panic("index block never returns");
+        return std::nullopt;
+      }
+      ++e_;
+      Bi nb = load((size_t)e_);                // Some(Err(e)) throws; valid stays false
+      bi_ = std::move(nb);
     }
-    ++e_;
-    Bi nb = load((size_t)e_);                // Some(Err(e)) throws; valid stays false
-    bi_ = std::move(nb);
     b = &*bi_;
     if (b->n() == 0 && b->end == MTBLX_EMIT_PANIC) throw Panic("BlockIter::seek_to_first / get");
     if (b->n() == 0) return std::nullopt;
@@ -743,30 +950,52 @@ inline std::optional<Record> ReaderIntoIter::next() {   // src/reader.rs:337-405
   }
   const Record rec = b->rec(b->pos);
   const size_t kl = k_.size();
-  const int c = std::memcmp(rec.key, k_.data(), std::min(rec.key_len, kl));
-  if (type_ == kGet) valid_ = c == 0 && rec.key_len == kl;
-  else if (type_ == kPrefix) valid_ = rec.key_len >= kl && (kl == 0 || std::memcmp(rec.key, k_.data(), kl) == 0);
-  else if (type_ == kRange) valid_ = !(c > 0 || (c == 0 && rec.key_len > kl));
+  if (type_ == kGet) {
+    valid_ = rec.key_len == kl && (kl == 0 || std::memcmp(rec.key, k_.data(), kl) == 0);
+  } else if (type_ == kPrefix) {
+    valid_ = rec.key_len >= kl && (kl == 0 || std::memcmp(rec.key, k_.data(), kl) == 0);
+  } else if (type_ == kRange) {
+    const size_t m = std::min(rec.key_len, kl);
+    const int c = m ? std::memcmp(rec.key, k_.data(), m) : 0;
+    valid_ = !(c > 0 || (c == 0 && rec.key_len > kl));
+  }
   if (!valid_) return std::nullopt;
   return rec;
 }
 
-inline bool ReaderIntoIter::seek(const Bytes& key) {   // src/reader.rs:302-335
-  const mtblx_index_seek s = r_->index_seek(key);
-  if (s.status == MTBLX_SEEK_PANIC) throw Panic("index seek");
-  if (s.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
-  if (!s.valid) {   // past the last key: next() returns None
-    valid_ = false;
-    e_ = -1;
-    return true;
+// src/reader.rs:302-335: the block is seeked to the landed index entry's key (:305 shadows `key`)
+inline bool ReaderIntoIter::seek(const Bytes& key) {
+  Bytes ikey;
+  uint64_t new_off = 0;
+  std::optional<mtblx_index_seek> s;
+  if (ix_) {                        // irregular index: the live index iterator
+    ix_seek(key);
+    if (!ix_->valid()) {
+      valid_ = false;
+      return true;
+    }
+    const Record ir = ix_->b.rec(ix_->b.pos);
+    ikey = ir.key_bytes();
+    if (mtblx_varint_decode64(ir.val, ir.val_len, &new_off) < 0) throw Panic("varint_decode64 of the index value");
+  } else {
+    s = r_->index_seek(key);
+    if (s->status == MTBLX_SEEK_PANIC) throw Panic("index seek");
+    if (s->status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
+    if (!s->valid) {   // past the last key: next() returns None
+      valid_ = false;
+      e_ = -1;
+      return true;
+    }
+    e_ = (int64_t)r_->ordinal(s->entry);
+    ikey = r_->index_key((size_t)e_);
+    new_off = s->block_off;
   }
-  e_ = (int64_t)r_->ordinal(s.entry);
-  if (block_offset_ != s.block_off) {
-    block_offset_ = s.block_off;   // updated before the load (:322)
-    Bi nb = seek_block(r_->seek_content(s), &key, 0);
+  if (block_offset_ != new_off) {
+    block_offset_ = new_off;   // updated before the load (:322)
+    Bi nb = seek_block(s ? r_->seek_content(*s) : r_->value_content(ix_->b.rec(ix_->b.pos).val_bytes()), &ikey, 0);
     bi_ = std::move(nb);
   } else if (bi_) {                 // the held block, whatever it is
-    Bi nb = seek_block(bi_->c, &key, kcap_now(*bi_));
+    Bi nb = seek_block(bi_->c, &ikey, kcap_now(*bi_));
     bi_ = std::move(nb);
   }
   first_ = true;

@@ -232,7 +232,10 @@ typedef struct mtblx_block_seek {
   uint64_t data_off, data_len;   /* in: block content in `data`                                  */
   uint64_t kcap;                 /* in: key capacity (0 = fresh); out: after the emitted records  */
   uint64_t max_records;          /* in                                                            */
-  int32_t first;                 /* in: 1 = seek_to_first instead of seek(key)                    */
+  int32_t first;                 /* in: 0 = seek(key); 1 = seek_to_first; 2 = resume: the iterator
+                                    holds key = keys[q] (its current key bytes) and kcap, and its
+                                    next() parses the entry at resume_off (BlockIter::next,
+                                    src/block.rs:196-202) -- the records from there are emitted  */
   int32_t status;                /* out: MTBLX_SEEK_* of Block::init / BlockIter::init / the seek */
   int32_t end;                   /* out: MTBLX_EMIT_*                                             */
   int32_t has_val;               /* out: an entry was parsed (BlockIter::val is Some)             */
@@ -240,6 +243,14 @@ typedef struct mtblx_block_seek {
   uint64_t nrec, key_bytes, val_bytes;   /* out                                                   */
   uint64_t last_voff, last_vlen; /* out: `val` of the last parsed entry (content offsets) -- what
                                     Reader::get returns when next() hits Err (src/reader.rs:111-122) */
+  uint64_t resume_off;           /* in (first == 2): offset of the entry next() parses            */
+  uint64_t stop_off;             /* out: the iterator's current entry offset when the emission
+                                    stopped; after MTBLX_EMIT_MAX: the entry after the last
+                                    emitted record (resume there with that record's key / kcap) */
+  int32_t early;                 /* out (first == 0): the binary search returned early on a restart
+                                    entry with shared != 0 (src/block.rs:167-170): a live iterator
+                                    keeps its previous position; nothing after it applies       */
+  int32_t pad;
 } mtblx_block_seek;
 int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end, uint32_t nq,
                            mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
@@ -250,9 +261,16 @@ int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, const uint6
  *     i <-> index record i <-> directory entry i), so a seek's landed entry maps to its index
  *     position.  Parallel over restart intervals when every interval's chain lands on the next
  *     restart point; otherwise one serial walk.  Writes min(count, cap) offsets; *count (device)
- *     = entries up to the end of the block or the first entry the scan cannot decode. */
+ *     = entries up to the end of the block or the first entry the scan cannot decode.
+ *     *regular (device u32, may be NULL) = 1 when every interval's chain lands on the next
+ *     restart point, every restart entry has shared == 0 and every other entry shared <= the
+ *     previous key's length.  For such an index block a seek from ANY iterator state (fresh or
+ *     live, any key capacity) never returns early, lands on the scan chain, rebuilds the scan's
+ *     keys and cannot hit the key-capacity assert: the host may then follow the directory
+ *     (entries i+1, i+2, ...) after a seek.  Otherwise the host drives the live index iterator
+ *     with mtblx_block_seek_batch (seek / resume) over the index block. */
 int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t* offs, uint64_t cap, uint64_t* count,
-                        void* stream);
+                        uint32_t* regular, void* stream);
 
 /* (4) ReaderIntoIter's stop rules (src/reader.rs:385-402) over decoded records: the index of
  *     the first record whose key fails (type 1 Get: != k, 2 GetPrefix: !starts_with(k), 3

@@ -1020,7 +1020,11 @@ out:
  * block only when the landed index entry's offset differs from `block_offset` -- a field
  * that new/new_from set to 0 and next() never updates (:244-246, :269-271, :362-366) -- so a
  * seek can re-seek whatever block the iterator currently holds; the re-seeked BlockIter
- * keeps its key Vec capacity (:327-329, src/block.rs:106-112). */
+ * keeps its key Vec capacity (:327-329, src/block.rs:106-112).  The index iterator is the
+ * LIVE one (:303): a seek whose binary search returns early on a restart entry with
+ * shared != 0 (src/block.rs:167-170) leaves it where it was, key capacity included, and
+ * next() continues from wherever the seek's linear scan left it, on the scan chain or not.
+ * The data block is seeked with the landed index entry's key (:305 shadows `key`). */
 typedef struct {
   oreader r;
   oiter idx, bi;
@@ -1089,7 +1093,9 @@ static int ostate_seek(ostate* s, const uint8_t* key, uint64_t kl) {
     s->bi = nb;
     s->have_bi = 1;
   }
-  if (s->have_bi && oseek(&s->bi, key, kl) < 0) return PANIC;
+  /* :305 shadows `key` with the landed INDEX entry's key (index_iter.get()), so :328 seeks
+   * the data block to that separator, not to the caller's target */
+  if (s->have_bi && oseek(&s->bi, s->idx.key, s->idx.klen) < 0) return PANIC;
   s->first = 1;
   s->valid = 1;
   return 0;

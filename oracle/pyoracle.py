@@ -249,6 +249,15 @@ def decode_block(block: bytes):
     return int(d.status[0]), d.records(0)
 
 
+def index_records(data: bytes):
+    """the index block's records (separator, value) of a V2 file: footer -> framing -> scan
+    (src/metadata.rs:27-59, src/reader.rs:51-76)"""
+    off = int.from_bytes(data[len(data) - 512: len(data) - 504], "little")
+    n, ll = varint_decode64(data[off: off + 10])
+    st, recs = decode_block(data[off + ll + 4: off + ll + 4 + n])
+    return recs
+
+
 def bench_scan(data: np.ndarray, blk_off, blk_len, nthreads=1, iters=1):
     """CPU baseline timing -> (seconds, records, fold)"""
     off = np.ascontiguousarray(blk_off, dtype=np.uint64)

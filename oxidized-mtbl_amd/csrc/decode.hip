@@ -375,6 +375,8 @@ struct TileArgs {
   uint32_t hw_other;
   unsigned long long inject;   // debug: bits ORed into totals[3] (MTBLX_DEBUG_FLAGS, mtblx_impl_run)
   uint32_t flags_direct;       // k_decode_pipe: flags go straight to totals[3] (pipe_zero_flags)
+  uint64_t wait_ticks;         // WaitBound's limit (kWaitTicks; MTBLX_DEBUG_WAIT_MS shortens it)
+  uint64_t dbg_delay0;         // debug: workgroup 0 starts this many ticks late (MTBLX_DEBUG_DELAY0_MS)
 };
 
 // Workspace header (byte 128 of the workspace).  The workspace carries state from call to
@@ -388,6 +390,7 @@ struct WsHdr {
   uint32_t done;
   uint32_t hw[2];
   unsigned long long flags;   // bit0 overflow, bit1 look-back timeout (-> totals[3])
+  unsigned long long tflags[2];   // k_decode_pipe: flags of the launch of each parity (pipe_zero_flags)
 };
 
 // Blocks of tile t: [b0, b0 + nb) with b0 = floor(t nblk / ntiles), ntiles = ceil(nblk / bpt)
@@ -419,10 +422,39 @@ __device__ __forceinline__ void ws_begin(TileArgs& a) {
   const uint32_t n = blockDim.x, tid = threadIdx.x;
   for (uint64_t t = (uint64_t)blockIdx.x * n + tid; t < a.hw_other; t += (uint64_t)gridDim.x * n)
     a.lbw[kTileWords * t + (a.par ^ 1u)] = 0;
+  // the next launch's flag word (the previous launch of that parity has ended: stream order)
+  if (blockIdx.x == 0 && tid == 0)
+    __hip_atomic_store(&a.hdr->tflags[a.par ^ 1u], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// test knob (MTBLX_DEBUG_DELAY0_MS): workgroup 0 starts late, as if it were not resident.  Not in
+// the fused-verify kernels: any extra code there pushes PipeLargeV past its 128 VGPRs.
+__device__ __forceinline__ void ws_debug_delay(const TileArgs& a) {
+  if (blockIdx.x == 0 && a.dbg_delay0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < a.dbg_delay0) __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+// A flag of this launch: k_decode_pipe (flags_direct) ORs it straight into totals[3], other
+// kernels into the workspace header (ws_end publishes it).
 __device__ __forceinline__ void ws_flag(const TileArgs& a, unsigned long long bit) {
   atomicOr(a.flags_direct ? reinterpret_cast<unsigned long long*>(a.totals + 3) : &a.hdr->flags, bit);
+}
+
+// A timeout (bit 1).  Tile 0's walker zeroes totals[3] at a time nobody waits for -- a
+// workgroup whose look-back on A(0) gives up because workgroup 0 is late / not resident flags
+// BEFORE the zeroing -- so k_decode_pipe also records the timeout in the launch's workspace word,
+// which pipe_zero_flags re-reads after its zeroing store: store-buffering with s_waitcnt
+// between the two accesses on each side (agent-scope atomics are performed at the device's
+// coherence point), so either the re-read sees this timeout or this OR into totals[3] lands
+// after the zeroing.  (Overflow flags, bit 0, are set after a look-back that waited on A(0).)
+__device__ __forceinline__ void ws_timeout(const TileArgs& a) {
+  if (a.flags_direct) {
+    __hip_atomic_fetch_or(&a.hdr->tflags[a.par], 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  ws_flag(a, 2ull);
 }
 
 // Bounded waits.  A wait on another workgroup (look-back) or on another wave gives up after
@@ -436,11 +468,11 @@ constexpr uint64_t kWaitTicks = 20ull * 100000000ull;   // 20 s
 struct WaitBound {
   uint64_t t0 = 0;
   uint32_t n = 0;
-  __device__ __forceinline__ bool expired() {
+  __device__ __forceinline__ bool expired(uint64_t ticks) {
     if ((++n & 63u) != 0u) return false;
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     if (t0 == 0) t0 = t;
-    return t - t0 > kWaitTicks;
+    return t - t0 > ticks;
   }
 };
 
@@ -478,8 +510,14 @@ __device__ __forceinline__ void ws_end(const TileArgs& a) {
 //  - the workgroup owning the last tile bumps the epoch and the high-water mark at its own
 //    end: that tile's look-back waited on the aggregate of the G-1 tiles before it, one from
 //    every other workgroup (G <= ntiles), so all of them have passed ws_begin by then.
+//    A flag set before the zeroing (a look-back on A(0) that timed out because workgroup 0 was
+//    not resident) is re-read from the launch's workspace word right after it (ws_flag).
 __device__ __forceinline__ void pipe_zero_flags(const TileArgs& a) {   // walker of tile 0, lane 0
-  __hip_atomic_store(a.totals + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long* tot = reinterpret_cast<unsigned long long*>(a.totals + 3);
+  __hip_atomic_store(tot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zeroing is performed before the re-read
+  const unsigned long long early = __hip_atomic_load(&a.hdr->tflags[a.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (early) __hip_atomic_fetch_or(tot, early, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // performed before A(0) is published
 }
 
@@ -950,11 +988,11 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         while (!(w & kReady)) {
           __builtin_amdgcn_s_sleep(2);
           w = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (wb.expired()) { timeout = true; w = kReady; }
+          if (wb.expired(a.wait_ticks)) { timeout = true; w = kReady; }
         }
         if (i >= (int64_t)lo) lb_take(a, (uint64_t)i, w, sr, sk, sv);
       }
-      if (timeout) ws_flag(a, 2ull);
+      if (timeout) ws_timeout(a);
       // per-thread sums are < 2^23 (4 tiles x 21-bit fields) unless a tile published exact words
       sr = lb_wave_sum(sr);
       sv = lb_wave_sum(sv);
@@ -1652,12 +1690,12 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
     while (!(w & kReady)) {
       __builtin_amdgcn_s_sleep(2);
       w = __hip_atomic_load(lb_slot(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (wb.expired()) { timeout = true; w = kReady; }
+      if (wb.expired(a.wait_ticks)) { timeout = true; w = kReady; }
     }
     if (i < lo) continue;
     lb_take(a, (uint64_t)i, w, sr, sk, sv);
   }
-  if (timeout) ws_flag(a, 2ull);
+  if (timeout) ws_timeout(a);
   sr = lb_wave_sum(sr);
   sv = lb_wave_sum(sv);
   sk = lb_wave_sum(sk);
@@ -1892,12 +1930,16 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
 }
 
 // Wait for a workgroup-local LDS counter.  Bounded: giving up means this launch's outputs are
-// not trustworthy (look-back / hand-off timeout, totals[3] bit 1), never a hang.
+// not trustworthy (look-back / hand-off timeout, totals[3] bit 1), never a hang.  Hand-offs
+// inside a workgroup wait 4x as long as a look-back on other workgroups (kHandoffMul), so a
+// look-back that gives up (and still releases its copy waves) never cascades into a hand-off
+// that gives up with the LDS state unwritten.
+constexpr uint64_t kHandoffMul = 4;
 __device__ __forceinline__ void wait_flag(const TileArgs& a, const uint32_t* flag, uint32_t want) {
   WaitBound wb;
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
     __builtin_amdgcn_s_sleep(1);
-    if (wb.expired()) { ws_flag(a, 2ull); break; }
+    if (wb.expired(kHandoffMul * a.wait_ticks)) { ws_timeout(a); break; }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
@@ -2074,8 +2116,21 @@ constexpr bool kLargeSerial = false;
 #define MTBLX_LATE_LOADCOPY 0
 #endif
 
+// MTBLX_SPILL (diagnostic build only, `make spill`): keep kSpillPad extra VGPRs live across the
+// whole pipeline kernel, which pushes it past its 128 VGPRs into scratch -- checks that a
+// spilling build is still correct (tests/test_spill_gpu.py)
+#ifdef MTBLX_SPILL
+constexpr int kSpillPad = MTBLX_SPILL;
+#else
+constexpr int kSpillPad = 0;
+#endif
 template <class P>
 __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
+  uint32_t spill_pad[kSpillPad > 0 ? kSpillPad : 1];
+  if constexpr (kSpillPad > 0) {
+#pragma unroll
+    for (int i = 0; i < kSpillPad; ++i) spill_pad[i] = a.blk_len[((uint32_t)threadIdx.x + 7u * i) % a.nblk];   // loads: not rematerialisable
+  }
   __shared__ PipeLds<P> S;
   // Two buffers, serial: tile it is walked, looked back and copied in iteration it while the
   // loaders stage tile it+1 (PipeLargeV: its fused CRC reads the tile being copied).  Otherwise
@@ -2096,6 +2151,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   ST.init();
   TL(0);
   ws_begin(a);
+  if constexpr (!P::VERIFY) ws_debug_delay(a);
   a.flags_direct = 1;
   if (tid == 0) { S.ready = 0; S.pub = 0; S.cdone = 0; S.crcdone = 0; S.staged = 0; }
   if constexpr (P::VERIFY) {
@@ -2223,7 +2279,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
             WaitBound wb;
             while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
               __builtin_amdgcn_s_sleep(1);
-              if (wb.expired()) { ws_flag(a, 2ull); break; }
+              if (wb.expired(kHandoffMul * a.wait_ticks)) { ws_timeout(a); break; }
             }
             pipe_lookback_issue(a, tc + G, G, lbv, lane);
             pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kCopyW);
@@ -2293,7 +2349,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           WaitBound wb;
           while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
             __builtin_amdgcn_s_sleep(1);
-            if (wb.expired()) { ws_flag(a, 2ull); break; }
+            if (wb.expired(kHandoffMul * a.wait_ticks)) { ws_timeout(a); break; }
           }
           pipe_lookback_issue(a, tc + G, G, lbv, lane);
           pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kCopyW);
@@ -2322,6 +2378,10 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   if (wv >= P::COPY0) TLW(12 + (wv & 1));   // copy waves' drains (two of them)
   TLW(14 + (wv == 1));                       // wave 0 / wave 1 drains (the slots race; diagnostic)
   if (g == (a.ntiles - 1) % G && tid == 0) pipe_close(a);
+  if constexpr (kSpillPad > 0) {
+#pragma unroll
+    for (int i = 0; i < kSpillPad; ++i) asm volatile("" ::"v"(spill_pad[i]));
+  }
   TL(5);
 #ifdef MTBLX_STAMPS
   if (tid == 0 && blockIdx.x < 1024) g_tl[blockIdx.x][6] = nloc;
@@ -2452,6 +2512,13 @@ static unsigned long long debug_flags() {
   const char* e = getenv("MTBLX_DEBUG_FLAGS");
   return e ? strtoull(e, nullptr, 0) : 0ull;
 }
+// MTBLX_DEBUG_WAIT_MS / MTBLX_DEBUG_DELAY0_MS (test knobs): the bounded waits give up after
+// that many ms instead of 20 s; workgroup 0 starts (and publishes A(0)) that many ms late
+// (tests/test_robust_gpu.py: a look-back timeout that happens before tile 0 starts survives)
+static uint64_t debug_ms(const char* name, uint64_t dflt) {
+  const char* e = getenv(name);
+  return e ? strtoull(e, nullptr, 0) * 100000ull : dflt;   // s_memrealtime: 100 MHz
+}
 
 extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* out, void* ws, size_t ws_bytes,
                               int write, hipStream_t s, int verify, uint32_t* crc, uint8_t* crc_bad, int framed) {
@@ -2467,6 +2534,8 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
              out->val_end, out->rec_cap,  out->keys,    out->keys_cap, out->vals,    out->vals_cap, out->totals,
              lbw,          hdr,           dbg,          write ? 1 : 0, crc,         crc_bad,       framed ? 1 : 0,
              wscap,        0,             0,            debug_flags()};
+  a.wait_ticks = debug_ms("MTBLX_DEBUG_WAIT_MS", kWaitTicks);
+  a.dbg_delay0 = debug_ms("MTBLX_DEBUG_DELAY0_MS", 0);
   if (p.kind == 0) {
     if (verify)
       hipLaunchKernelGGL(k_decode_pipe<PipeSmallV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);

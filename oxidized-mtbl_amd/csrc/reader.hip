@@ -485,15 +485,18 @@ __device__ int s_parse(const Blk& b, SIt& it, uint8_t* K, int lane) {
   return R_OK;
 }
 
-// BlockIter::seek (src/block.rs:154-194) with the key materialised
-__device__ int s_seek(const Blk& b, SIt& it, uint8_t* K, const uint8_t* t, uint64_t tl, int lane) {
+// BlockIter::seek (src/block.rs:154-194) with the key materialised.  early: the binary search
+// returned on a restart entry with shared != 0 -- the iterator is left as it was (the caller
+// keeps its previous state; this matters for the live index iterator, src/reader.rs:303)
+__device__ int s_seek(const Blk& b, SIt& it, uint8_t* K, const uint8_t* t, uint64_t tl, int lane, bool& early) {
   uint32_t left = 0, right = b.n - 1;
+  early = false;
   while (left < right) {
     const uint32_t mid = (uint32_t)(((uint64_t)left + right + 1) / 2);
     uint32_t sh, ns, vl;
     uint64_t ko;
     if (decode_entry(b, restart_point(b, mid), b.R, sh, ns, vl, ko) != R_OK) return R_PANIC;
-    if (sh != 0) return R_OK;                                 // "corruption": early return
+    if (sh != 0) { early = true; return R_OK; }               // "corruption": early return
     if (ko + ns > b.L) return R_PANIC;
     if (wave_cmp(b.d + ko, ns, t, tl, lane) < 0) left = mid;
     else right = mid - 1;
@@ -525,6 +528,8 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
     Q.end = MTBLX_EMIT_END;
     Q.nrec = Q.key_bytes = Q.val_bytes = 0;
     Q.entry = 0;
+    Q.early = 0;
+    Q.stop_off = 0;
     const uint64_t L = Q.data_len;
     const uint8_t* src = data + Q.data_off;
     const uint8_t* d = src;
@@ -544,15 +549,29 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
       it.has_next = false;
       it.kcap = Q.kcap;
       int r;
-      if (Q.first) {                                               // seek_to_first
+      bool early = false;
+      if (Q.first == 1) {                                          // seek_to_first
         it.klen = 0;
         it.has_next = true;
         it.next = restart_point(b, 0);
         r = s_parse(b, it, K, lane);
         if (r == R_END) r = R_OK;
+      } else if (Q.first == 2) {                                   // resume: next() from a held state
+        if (tl > kSeekKey) {
+          r = R_TOOLONG;
+        } else {
+          for (uint64_t j = (uint64_t)lane; j < tl; j += 64) K[j] = t[j];
+          __syncthreads();
+          it.klen = tl;
+          it.has_next = true;
+          it.next = Q.resume_off;
+          r = s_parse(b, it, K, lane);
+          if (r == R_END) r = R_OK;
+        }
       } else {
-        r = s_seek(b, it, K, t, tl, lane);
+        r = s_seek(b, it, K, t, tl, lane, early);
       }
+      Q.early = early ? 1 : 0;
       if (r != R_OK) {
         Q.status = r == R_LOOP ? MTBLX_SEEK_LOOP : r == R_TOOLONG ? MTBLX_SEEK_UNSUPPORTED : MTBLX_SEEK_PANIC;
         break;
@@ -596,6 +615,7 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
       if (ovf && Q.status == MTBLX_SEEK_OK) Q.end = MTBLX_EMIT_OVERFLOW;
     } while (false);
     Q.kcap = it.kcap;
+    Q.stop_off = it.current;
     Q.has_val = it.has_val ? 1 : 0;
     Q.last_voff = it.voff;
     Q.last_vlen = it.vlen;
@@ -604,44 +624,60 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
 }
 
 // chain of entry offsets from restart 0 (seek_to_first + next), see mtblx_entry_offsets
-__device__ __forceinline__ bool chain_step(const Blk& b, uint64_t cur, uint64_t& nxt) {
-  uint32_t sh, ns, vl;
+__device__ __forceinline__ bool chain_step(const Blk& b, uint64_t cur, uint64_t& nxt, uint32_t& sh, uint32_t& ns) {
+  uint32_t vl;
   uint64_t p;
   if (decode_entry(b, cur, b.R, sh, ns, vl, p) != R_OK) return false;
   if (p + ns > b.L) return false;
   nxt = p + ns + vl;
   return true;
 }
+__device__ __forceinline__ bool chain_step(const Blk& b, uint64_t cur, uint64_t& nxt) {
+  uint32_t sh, ns;
+  return chain_step(b, cur, nxt, sh, ns);
+}
 
 __global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint64_t L, uint64_t* offs, uint64_t cap,
-                                                        uint64_t* count, uint64_t* scratch) {
-  __shared__ int irregular;
+                                                        uint64_t* count, uint64_t* scratch, uint32_t* regular_out) {
+  __shared__ int irregular, keys_irregular;
   __shared__ uint64_t wsum[16];
   __shared__ uint64_t carry;
   Blk b{};
   const int tid = threadIdx.x;
-  if (tid == 0) { irregular = 0; carry = 0; }
+  if (tid == 0) { irregular = 0; keys_irregular = 0; carry = 0; }
   __syncthreads();
   if (block_init(blk, L, b) != 0 || b.n == 0) {
-    if (tid == 0) *count = 0;
+    if (tid == 0) {
+      *count = 0;
+      if (regular_out) *regular_out = 0;
+    }
     return;
   }
   const uint32_t n = b.n;
-  // pass 1: count each restart interval's chain; it must land exactly on the next restart point
+  // pass 1: count each restart interval's chain; it must land exactly on the next restart point.
+  // Also: every restart entry has shared == 0 and every other entry shared <= the previous
+  // key's length -- then a seek starting at any restart point rebuilds the scan's own keys and
+  // the key-capacity assert (src/block.rs:132) can never fire (see mtblx.h)
   for (uint32_t r = tid; r < n; r += blockDim.x) {
     const uint64_t s0 = restart_point(b, r), e0 = (r + 1 < n) ? restart_point(b, r + 1) : b.R;
-    uint64_t c = 0, cur = s0;
+    uint64_t c = 0, cur = s0, klen = 0;
     bool ok = s0 < e0 || (r + 1 == n && s0 == b.R);
+    bool kok = true;
     while (ok && cur < e0) {
       uint64_t nx;
-      if (!chain_step(b, cur, nx)) { ok = false; break; }
+      uint32_t sh, ns;
+      if (!chain_step(b, cur, nx, sh, ns)) { ok = false; break; }
+      if (c == 0 ? sh != 0 : sh > klen) kok = false;
+      klen = (sh < klen ? sh : klen) + ns;
       cur = nx;
       ++c;
     }
     if (!ok || cur != e0) irregular = 1;
+    if (!kok) keys_irregular = 1;
     scratch[r] = c;
   }
   __syncthreads();
+  if (tid == 0 && regular_out) *regular_out = (irregular || keys_irregular) ? 0u : 1u;
   if (!irregular) {
     // exclusive scan of scratch[0..n) in chunks of blockDim.x
     for (uint32_t base = 0; base < n; base += blockDim.x) {
@@ -764,14 +800,15 @@ extern "C" int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, 
 }
 
 extern "C" int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t* offs, uint64_t cap, uint64_t* count,
-                                   void* stream) {
+                                   uint32_t* regular, void* stream) {
   if (!block || !count || (cap && !offs)) return MTBLX_E_INVAL;
   if (len > mtblx_rd::kU32) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint64_t nr = len / 4 + 1;   // restart count bound: 4 bytes per restart point
   uint64_t* scratch = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&scratch), nr * sizeof(uint64_t), s) != hipSuccess) return MTBLX_E_HIP;
-  hipLaunchKernelGGL(mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch);
+  hipLaunchKernelGGL(mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch,
+                     regular);
   const bool ok = hipGetLastError() == hipSuccess;
   (void)hipFreeAsync(scratch, s);
   return ok ? MTBLX_OK : MTBLX_E_HIP;

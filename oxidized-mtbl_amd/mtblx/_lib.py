@@ -75,7 +75,8 @@ class BlockSeek(C.Structure):   # mtblx_block_seek
     _fields_ = [("data_off", C.c_uint64), ("data_len", C.c_uint64), ("kcap", C.c_uint64), ("max_records", C.c_uint64),
                 ("first", C.c_int32), ("status", C.c_int32), ("end", C.c_int32), ("has_val", C.c_int32),
                 ("entry", C.c_uint64), ("nrec", C.c_uint64), ("key_bytes", C.c_uint64), ("val_bytes", C.c_uint64),
-                ("last_voff", C.c_uint64), ("last_vlen", C.c_uint64)]
+                ("last_voff", C.c_uint64), ("last_vlen", C.c_uint64), ("resume_off", C.c_uint64),
+                ("stop_off", C.c_uint64), ("early", C.c_int32), ("pad", C.c_int32)]
 
 
 class Footer(C.Structure):
@@ -201,7 +202,8 @@ def lib() -> C.CDLL:
                                              C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_uint64, C.c_void_p]
         L.mtblx_block_seek_batch.restype = C.c_int
-        L.mtblx_entry_offsets.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.mtblx_entry_offsets.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]
         L.mtblx_entry_offsets.restype = C.c_int
         L.mtblx_key_filter.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64,
                                        C.c_void_p, C.c_void_p]

@@ -23,10 +23,19 @@ Two surfaces:
   * `ReaderIntoIter`: the stateful iterator (next() -> (key, value) | None, seek(key)), host
     records, for callers that interleave seeks and nexts.
 
-One documented approximation: the index seek runs on a fresh index iterator.  The reference
-re-seeks its live index iterator, which differs only when the INDEX block's restart entries
-are corrupt (BlockIter::seek's early return keeps the old position); such index blocks fail
-the checksum at open unless verification is off.
+ReaderIntoIter::seek (:302-335) re-seeks the LIVE index iterator (:303) and then seeks the
+data block with the landed INDEX entry's key -- `key` is shadowed at :305 -- so seek(k) +
+next() yields the first record >= the separator, not >= k.
+
+The index iterator.  When the index block is *regular* (mtblx_entry_offsets: chains land on
+the restart points, restart entries have shared == 0, no entry has shared > the previous key's
+length), a seek from any index iterator state lands on the scan chain with the scan's own key
+and the key-capacity assert cannot fire, so the index position is a directory entry and the
+blocks after it come from the directory (batched decode).  Otherwise (a corrupt index, read
+with verification off) the live index iterator is driven on the device exactly:
+mtblx_block_seek_batch seeks the index block with the iterator's key capacity (an early return
+keeps the old position) and emits the records next() visits from the landing, on the scan
+chain or not; `_IxList` holds them, resuming the emission when it runs out.
 """
 from __future__ import annotations
 
@@ -68,6 +77,7 @@ class Emitted:
     def __init__(self, q: _lib.BlockSeek, keys, vals, key_end, val_end, kcaps):
         self.status, self.end, self.entry = int(q.status), int(q.end), int(q.entry)
         self.nrec, self.kcap_end = int(q.nrec), int(q.kcap)
+        self.early, self.stop_off = bool(q.early), int(q.stop_off)
         self.has_val, self.last_voff, self.last_vlen = bool(q.has_val), int(q.last_voff), int(q.last_vlen)
         self.keys, self.vals, self.key_end, self.val_end, self.kcaps = keys, vals, key_end, val_end, kcaps
 
@@ -84,16 +94,19 @@ class Emitted:
 
 
 def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 << 62,
-               small_caps: bool = False) -> Emitted:
+               small_caps: bool = False, resume_off: int | None = None) -> Emitted:
     """BlockIter::seek(key) (key None: seek_to_first) on content = (tensor, off, len) with the
-    given key capacity, then the records it yields until get() is None.  small_caps: start
-    from small output buffers and size them exactly from the first pass's counts (blocks of
-    GiBs)."""
+    given key capacity, then the records it yields until get() is None.  resume_off: instead
+    of seeking, an iterator holding key bytes `key` and capacity kcap calls next(), which
+    parses the entry at resume_off.  small_caps: start from small output buffers and size them
+    exactly from the first pass's counts (blocks of GiBs)."""
     data, off, ln = content
     dev = data.device
     kb = _dev_bytes(key or b"", dev)
     ke = torch.tensor([len(key or b"")], dtype=torch.int64, device=dev)
-    q = _lib.BlockSeek(data_off=off, data_len=ln, kcap=kcap, max_records=max_records, first=1 if key is None else 0)
+    first = 2 if resume_off is not None else (1 if key is None else 0)
+    q = _lib.BlockSeek(data_off=off, data_len=ln, kcap=kcap, max_records=max_records, first=first,
+                       resume_off=resume_off or 0)
     rec_cap = min(max_records, ln // 3 + 1)
     keys_cap, vals_cap = 2 * ln + 64, ln + 16
     if small_caps:
@@ -137,6 +150,16 @@ def key_filter(keys: torch.Tensor, key_end: torch.Tensor, n: int, typ: int, k: b
     return int(ff.item())
 
 
+def _varint_decode64(v: bytes) -> int:
+    """varint_decode64(val, &mut offset) of an index value (src/varint.rs:78-97, host C++)"""
+    from .reader import ReferencePanic
+    out = C.c_uint64(0)
+    b = np.frombuffer(v or b"\0", np.uint8)
+    if _lib.lib().mtblx_varint_decode64(b.ctypes.data_as(_lib.u8p), len(v), C.byref(out)) < 0:
+        raise ReferencePanic("varint_decode64 of the index value")
+    return int(out.value)
+
+
 def prefix_successor(p: bytes):
     """smallest key greater than every key starting with p (None: no such key)"""
     b = bytearray(p)
@@ -156,6 +179,8 @@ def bulk(r, kind: str, key: bytes, key2: bytes = b""):
     typ = KINDS[kind]
     k = key2 if typ == RANGE else key
     dev = r.file.device
+    if not r.index_regular():
+        return _bulk_stateful(r, kind, key, key2)
 
     def empty(end, err="None"):
         z = torch.zeros(0, dtype=torch.uint8, device=dev)
@@ -225,6 +250,48 @@ def bulk(r, kind: str, key: bytes, key2: bytes = b""):
     return _assemble(parts, end, err, dev)
 
 
+def _bulk_stateful(r, kind: str, key: bytes, key2: bytes):
+    """new_from / new_get_prefix / new_get_range run to the end on a corrupt (irregular) index:
+    the stateful iterator below, which follows the live index iterator exactly; the records
+    are uploaded as a Scan"""
+    from .reader import END_ERR_NEXT, END_ERR_OPEN, END_LOOP, END_NONE, END_PANIC, MtblError, ReferenceLoop, \
+        ReferencePanic
+    recs, end, err = [], END_NONE, "None"
+    try:
+        it = ReaderIntoIter(r, kind, key, key2)
+    except MtblError as x:
+        it, end, err = None, END_ERR_OPEN, x.args[0]
+    except ReferencePanic:
+        it, end = None, END_PANIC
+    except ReferenceLoop:
+        it, end = None, END_LOOP
+    if it is not None:
+        it.bulk = True
+        try:
+            while True:
+                rec = it.next()
+                if rec is None:
+                    break
+                recs.append(rec)
+        except MtblError as x:
+            end, err = END_ERR_NEXT, x.args[0]
+        except ReferencePanic:
+            end = END_PANIC
+        except ReferenceLoop:
+            end = END_LOOP
+    return _from_host(recs, end, err, r.file.device)
+
+
+def _from_host(recs, end, err, dev):
+    from .reader import Scan
+    kb = b"".join(k for k, _ in recs)
+    vb = b"".join(v for _, v in recs)
+    ke = np.cumsum([len(k) for k, _ in recs], dtype=np.int64)
+    ve = np.cumsum([len(v) for _, v in recs], dtype=np.int64)
+    return Scan(end, err, len(recs), _dev_bytes(kb, dev)[: len(kb)], _dev_bytes(vb, dev)[: len(vb)],
+                torch.from_numpy(ke).to(dev), torch.from_numpy(ve).to(dev))
+
+
 def _cut_part(part, n):
     keys, vals, ke, ve, _ = part
     kl = int(ke[n - 1].item()) if n else 0
@@ -275,6 +342,39 @@ class _Bi:
         return int(self.kcaps[min(self.pos, len(self.recs) - 1)])
 
 
+class _IxList:
+    """the live index iterator of an irregular index (src/reader.rs:223): the records its
+    next() visits from its current position on, with the key capacity at each, as
+    mtblx_block_seek_batch emitted them; `end` says what the next() after the last one does.
+    ord0: directory entry of record 0 when the landing lies on the scan chain (the records
+    then name the directory's blocks, which next() may load from the batched decode)"""
+
+    EMIT = 256   # records per emission
+
+    def __init__(self, em: "Emitted | None", ord0):
+        if em is None:                     # BlockIter::init: invalid, key capacity 0
+            self.recs, self.kcaps, self.end, self.stop_off, self.kcap_end = [], [], _lib.EMIT_END, 0, 0
+        else:
+            self.recs = em.host_records()
+            self.kcaps = em.kcaps.cpu().numpy().tolist()
+            self.end, self.stop_off, self.kcap_end = em.end, em.stop_off, em.kcap_end
+        self.pos = 0
+        self.ord0 = ord0
+
+    def valid(self) -> bool:
+        return self.pos < len(self.recs)
+
+    def kcap(self) -> int:
+        return int(self.kcaps[self.pos]) if self.valid() else int(self.kcap_end)
+
+    def ordinal(self, r):
+        """directory entry of the current record, or None (off the chain / past the directory)"""
+        if self.ord0 is None:
+            return None
+        j = self.ord0 + self.pos
+        return j if j < r.nent else None
+
+
 class ReaderIntoIter:
     """src/reader.rs:219-405.  kind: "iter" (Reader::into_iter), "from", "get", "prefix",
     "range" (end key = key2, inclusive).  next() -> (key, value) or None; raises MtblError for
@@ -290,27 +390,103 @@ class ReaderIntoIter:
         self.first = True
         self.valid = True
         self.bi = None
-        self.e = None                # index position (directory entry), None: index iterator invalid
+        self.e = None                # regular index: index position (directory entry), None: invalid
+        self.ix = None               # irregular index: the live index iterator (_IxList)
+        self.bulk = False            # driven to the end by bulk(): a looping index never returns
         self._chunk = None           # prefetched blocks: (i0, [ _Bi | exception ])
         self._grow = 1
+        self._vchunk = None          # irregular index: prefetched blocks of the current _IxList
+        regular = kind == "iter" or r.index_regular()
         if kind == "iter":           # new (:231-254): index seek_to_first, block_at_index, seek_to_first
             if r.nent == 0:
                 if r.index_status == _lib.ST_CORRUPT:
                     raise ReferencePanic("index block: first entry")
+                if not r.index_regular():
+                    self.ix = _IxList(None, None)
                 return
-            self.e = 0
+            if not r.index_regular():   # the scan's own chain = the directory, with its key capacities
+                self.ix = _IxList(block_seek(r.index_content(), None, 0, _IxList.EMIT), 0)
+            else:
+                self.e = 0
             self.bi = self._load(0)
             return
         key = bytes(key)
-        s = index_seek(r, key)       # new_from (:256-279)
-        if s.status == _lib.SEEK_PANIC:
-            raise ReferencePanic("index seek")
-        if s.status == _lib.SEEK_LOOP:
-            raise ReferenceLoop("index seek")
-        if not s.valid:
+        if regular:
+            s = index_seek(r, key)       # new_from (:256-279)
+            if s.status == _lib.SEEK_PANIC:
+                raise ReferencePanic("index seek")
+            if s.status == _lib.SEEK_LOOP:
+                raise ReferenceLoop("index seek")
+            if not s.valid:
+                return
+            self.e = r._ordinal(int(s.entry))
+            self.bi = self._seek_block(r._seek_content(s), key, 0)
             return
-        self.e = r._ordinal(int(s.entry))
-        self.bi = self._seek_block(r._seek_content(s), key, 0)
+        self.ix = _IxList(None, None)    # a fresh index iterator, seeked
+        self._ix_seek(key)
+        if not self.ix.valid():
+            return
+        self.bi = self._seek_block(r._value_content(self.ix.recs[self.ix.pos][1]), key, 0)
+
+    # ---------------------------------------------------------------- the index iterator
+    def _ix_seek(self, key: bytes):
+        """index_iter.seek(key) on the live iterator of an irregular index (src/block.rs:154-194)"""
+        from .reader import ReferenceLoop, ReferencePanic
+        em = block_seek(self.r.index_content(), key, self.ix.kcap(), _IxList.EMIT)
+        if em.status == _lib.SEEK_PANIC:
+            raise ReferencePanic("index seek")
+        if em.status == _lib.SEEK_LOOP:
+            raise ReferenceLoop("index seek")
+        if em.status == _lib.SEEK_UNSUPPORTED:
+            raise NotImplementedError("emitting seek: index key > 64 KiB")
+        if em.early:                 # returned on a corrupt restart entry: the old position stays
+            return
+        self.ix = _IxList(em, self.r._chain_ordinal(em.entry) if em.nrec else None)
+        self._vchunk = None
+
+    def _ix_next(self) -> bool:
+        """index_iter.next() (src/block.rs:196-202) on the live iterator"""
+        from .reader import ReferenceLoop, ReferencePanic
+        ix = self.ix
+        if not ix.valid():
+            return False
+        if ix.pos + 1 < len(ix.recs):
+            ix.pos += 1
+            return True
+        if ix.end == _lib.EMIT_END:
+            ix.pos = len(ix.recs)
+            return False
+        if ix.end == _lib.EMIT_PANIC:
+            raise ReferencePanic("index block: next entry")
+        if ix.end == _lib.EMIT_LOOP:   # a zero-progress entry: next() parses it again, same record
+            if self.bulk:
+                raise ReferenceLoop("index block: next entry")
+            return True
+        # EMIT_MAX: the entry after the last record, parsed from that record's key / capacity
+        k, _ = ix.recs[-1]
+        em = block_seek(self.r.index_content(), k, int(ix.kcaps[-1]), _IxList.EMIT, resume_off=ix.stop_off)
+        if em.status == _lib.SEEK_PANIC:
+            raise ReferencePanic("index block: next entry")
+        if em.status == _lib.SEEK_UNSUPPORTED:
+            raise NotImplementedError("emitting seek: index key > 64 KiB")
+        self.ix = _IxList(em, None if ix.ord0 is None else ix.ord0 + len(ix.recs))
+        self._vchunk = None
+        return self.ix.valid()
+
+    def _ix_load(self) -> "_Bi":
+        """block_at_index of the live index iterator's record (Reader::block + seek_to_first)"""
+        ix = self.ix
+        j = ix.ordinal(self.r)
+        if j is not None:
+            return self._load(j)
+        if self._vchunk is None or not (self._vchunk[0] <= ix.pos < self._vchunk[0] + len(self._vchunk[1])):
+            n = min(len(ix.recs) - ix.pos, self._grow)
+            self._grow = min(2 * self._grow, 256)
+            self._vchunk = (ix.pos, self.r._value_blocks([v for _, v in ix.recs[ix.pos: ix.pos + n]]))
+        b = self._vchunk[1][ix.pos - self._vchunk[0]]
+        if isinstance(b, Exception):
+            raise b
+        return _Bi(b[0], list(b[1]), b[2])
 
     # the block of directory entry i as next() loads it (Reader::block + seek_to_first)
     def _load(self, i: int) -> _Bi:
@@ -365,18 +541,23 @@ class ReaderIntoIter:
             rec = bi.recs[bi.pos]
         else:
             self.valid = False
-            if self.e is None:
-                return None
-            if self.e + 1 >= self.r.nent:                 # index_iter.next() past the last entry
-                st = self.r.index_status
-                self.e = None
-                if st == _lib.ST_CORRUPT:
-                    raise ReferencePanic("index block: next entry")
-                if st == _lib.ST_LOOP:
-                    raise ReferenceLoop("index block: next entry")
-                return None
-            self.e += 1
-            nb = self._load(self.e)                       # Some(Err(e)) raises; valid stays false
+            if self.ix is not None:                       # irregular index: the live iterator
+                if not self._ix_next():
+                    return None
+                nb = self._ix_load()                      # Some(Err(e)) raises; valid stays false
+            else:
+                if self.e is None:
+                    return None
+                if self.e + 1 >= self.r.nent:             # index_iter.next() past the last entry
+                    st = self.r.index_status
+                    self.e = None
+                    if st == _lib.ST_CORRUPT:
+                        raise ReferencePanic("index block: next entry")
+                    if st == _lib.ST_LOOP:
+                        raise ReferenceLoop("index block: next entry")
+                    return None
+                self.e += 1
+                nb = self._load(self.e)                   # Some(Err(e)) raises; valid stays false
             self.bi = nb
             if nb.end == _lib.EMIT_PANIC and not nb.recs:
                 raise ReferencePanic("BlockIter::seek_to_first / get")
@@ -394,24 +575,38 @@ class ReaderIntoIter:
         return rec if self.valid else None
 
     def seek(self, key: bytes) -> bool:
-        """ReaderIntoIter::seek (:302-335): Ok(true), or raises (Err / panic / loop)."""
+        """ReaderIntoIter::seek (:302-335): Ok(true), or raises (Err / panic / loop).  The data
+        block is seeked with the landed index entry's key (`key` is shadowed at :305)."""
         from .reader import ReferenceLoop, ReferencePanic
         key = bytes(key)
-        s = index_seek(self.r, key)
-        if s.status == _lib.SEEK_PANIC:
-            raise ReferencePanic("index seek")
-        if s.status == _lib.SEEK_LOOP:
-            raise ReferenceLoop("index seek")
-        if not s.valid:
-            self.valid = False
-            self.e = None
-            return True
-        self.e = self.r._ordinal(int(s.entry))
-        if self.block_offset != int(s.block_off):
-            self.block_offset = int(s.block_off)          # updated before the load (:322)
-            self.bi = self._seek_block(self.r._seek_content(s), key, 0)
+        r = self.r
+        if self.ix is not None:                           # irregular index: the live iterator
+            self._ix_seek(key)
+            if not self.ix.valid():
+                self.valid = False
+                return True
+            ikey, ival = self.ix.recs[self.ix.pos]
+            new_off = _varint_decode64(ival)
+            content = lambda: r._value_content(ival)      # noqa: E731
+        else:
+            s = index_seek(r, key)
+            if s.status == _lib.SEEK_PANIC:
+                raise ReferencePanic("index seek")
+            if s.status == _lib.SEEK_LOOP:
+                raise ReferenceLoop("index seek")
+            if not s.valid:
+                self.valid = False
+                self.e = None
+                return True
+            self.e = r._ordinal(int(s.entry))
+            ikey = r._index_keys()[self.e]
+            new_off = int(s.block_off)
+            content = lambda: r._seek_content(s)          # noqa: E731
+        if self.block_offset != new_off:
+            self.block_offset = new_off                   # updated before the load (:322)
+            self.bi = self._seek_block(content(), ikey, 0)
         elif self.bi is not None:                         # the held block, whatever it is
-            self.bi = self._seek_block(self.bi.content, key, self.bi.kcap())
+            self.bi = self._seek_block(self.bi.content, ikey, self.bi.kcap())
         self.first = True
         self.valid = True
         return True

@@ -148,7 +148,9 @@ class Reader:
         self._dir3 = None
         self._scan = None
         self._eoffs = None
+        self._regular = None
         self._ikeys = None
+        self._irecs = None
 
     # ------------------------------------------------------------------ directory
     def directory(self):
@@ -331,8 +333,10 @@ class Reader:
     def _big_frame(self, i: int):
         """Reader::block framing of directory entry i from its index value (host, a few bytes)
         -> (block offset, content start, content length, stored crc)"""
+        return self._big_frame_value(self._index_records()[i][1])
+
+    def _big_frame_value(self, v: bytes):
         L = _lib.lib()
-        v = self.index.to_host().records(0)[i][1]
         off = C.c_uint64(0)
         vb = np.frombuffer(v or b"\0", np.uint8)
         L.mtblx_varint_decode64(vb.ctypes.data_as(_lib.u8p), len(v), C.byref(off))
@@ -366,10 +370,13 @@ class Reader:
         """Reader::block + Block::init + the scan for a block >= 4 GiB (u64 restart array,
         src/block.rs:25-42): decoded on the device by the emitting block seek (seek_to_first).
         -> ("ok", Emitted) | ("panic", None) | ("loop", None) | (error name, None)"""
+        return self._big_block_value(self._index_records()[i][1])
+
+    def _big_block_value(self, value: bytes):
         from . import iterator
         if self.compression != 0:
             raise NotImplementedError("compressed block >= 4 GiB")
-        off, start, size, stored = self._big_frame(i)
+        off, start, size, stored = self._big_frame_value(value)
         if start > self.len or size > self.len - start:
             return "panic", None
         if self.verify and self._crc_big(start, size) != stored:
@@ -473,28 +480,108 @@ class Reader:
         from . import iterator
         return iterator.ReaderIntoIter(self, kind, key, key2)
 
+    def _index_records(self):
+        """the index block's records (separator key, value) on the host, cached"""
+        if self._irecs is None:
+            self._irecs = self.index.to_host().records(0) if self.nent else []
+        return self._irecs
+
     def _index_keys(self):
         if self._ikeys is None:
-            self._ikeys = [k for k, _ in self.index.to_host().records(0)] if self.nent else []
+            self._ikeys = [k for k, _ in self._index_records()]
         return self._ikeys
 
-    def _ordinal(self, entry: int) -> int:
-        """index position of the entry an index seek landed on (mtblx_entry_offsets)"""
+    def _index_chain(self):
+        """(entry offsets of the index scan chain, regular) from mtblx_entry_offsets: regular =
+        a seek from any index iterator state lands on the chain and continues along the
+        directory (include/mtblx.h); otherwise the iterators drive the live index iterator on
+        the device (iterator._IxList)"""
         if self._eoffs is None:
             dev = self.file.device
-            offs = torch.zeros(max(self.nent, 1), dtype=torch.int64, device=dev)
+            cap = max(self.index_len // 3 + 1, 1)          # an entry takes >= 3 bytes
+            offs = torch.zeros(cap, dtype=torch.int64, device=dev)
             cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            reg = torch.zeros(1, dtype=torch.int32, device=dev)
             rc = _lib.lib().mtblx_entry_offsets(C.c_void_p(self.file.data_ptr() + self.index_off), self.index_len,
-                                                C.c_void_p(offs.data_ptr()), self.nent, C.c_void_p(cnt.data_ptr()),
-                                                C.c_void_p(codec._stream_handle(None)))
+                                                C.c_void_p(offs.data_ptr()), cap, C.c_void_p(cnt.data_ptr()),
+                                                C.c_void_p(reg.data_ptr()), C.c_void_p(codec._stream_handle(None)))
             if rc != 0:
                 raise RuntimeError(f"mtblx_entry_offsets failed: {rc}")
-            n = min(int(cnt.item()), self.nent)
+            n = min(int(cnt.item()), cap)
             self._eoffs = offs[:n].cpu().numpy()
-        i = int(np.searchsorted(self._eoffs, entry))
-        if i < self._eoffs.size and int(self._eoffs[i]) == entry:
+            self._regular = bool(reg.item()) and self.index_status == _lib.ST_OK
+        return self._eoffs, self._regular
+
+    def index_regular(self) -> bool:
+        return self._index_chain()[1]
+
+    def _chain_ordinal(self, entry: int):
+        """position on the index scan chain of the entry at `entry` (the index seek's landing),
+        or None when it lies off the chain (a corrupt index)"""
+        eoffs = self._index_chain()[0]
+        i = int(np.searchsorted(eoffs, entry))
+        if i < eoffs.size and int(eoffs[i]) == entry:
             return i
-        raise NotImplementedError("index seek landed off the index block's scan chain (corrupt index)")
+        return None
+
+    def _ordinal(self, entry: int) -> int:
+        """directory entry of a regular index's seek landing (always on the chain)"""
+        i = self._chain_ordinal(entry)
+        if i is None or i >= self.nent:
+            raise RuntimeError("index seek landed off the directory of a regular index")
+        return i
+
+    def index_content(self):
+        """the index block content on the device as (tensor, off, len)"""
+        return self.file, self.index_off, self.index_len
+
+    def _frame_values(self, values):
+        """block_at_index + Reader::block framing (src/reader.rs:177-186, :139-157) of arbitrary
+        index values (the live index iterator's records) on the device: (off, len, status)"""
+        dev = self.file.device
+        n = len(values)
+        blob = b"".join(values) or b"\0"
+        vals = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+        vend = torch.tensor(np.cumsum([len(v) for v in values], dtype=np.int64).astype(np.uint32).view(np.int32),
+                            dtype=torch.int32, device=dev)
+        off = torch.zeros(n, dtype=torch.int64, device=dev)
+        ln = torch.zeros(n, dtype=torch.int32, device=dev)
+        st = torch.zeros(n, dtype=torch.int32, device=dev)
+        rc = _lib.lib().mtblx_block_dir(C.c_void_p(self.file.data_ptr()), self.len, self.version,
+                                        C.c_void_p(vals.data_ptr()), C.c_void_p(vend.data_ptr()), 0, n,
+                                        C.c_void_p(off.data_ptr()), C.c_void_p(ln.data_ptr()),
+                                        C.c_void_p(st.data_ptr()), C.c_void_p(codec._stream_handle(None)))
+        if rc != 0:
+            raise RuntimeError(f"mtblx_block_dir failed: {rc}")
+        return off, ln, st
+
+    def _value_blocks(self, values):
+        """the blocks of index values as next() loads them (see _host_blocks)"""
+        off, ln, st = self._frame_values(values)
+        return self._host_blocks_framed(off, ln, st, values)
+
+    def _value_content(self, value: bytes):
+        """Reader::block (src/reader.rs:139-175) at the offset an index value names -> the
+        content (tensor, off, len) BlockIter reads; raises the reference's panics / Err"""
+        off, ln, st = self._frame_values([value])
+        s = int(st[0].item())
+        if s == _lib.DIR_UNSUPPORTED:                   # content >= 4 GiB
+            if self.compression != 0:
+                raise NotImplementedError("compressed block >= 4 GiB")
+            _, start, size, stored = self._big_frame_value(value)
+            if self.verify and self._crc_big(start, size) != stored:
+                raise ReferencePanic("Reader::block: checksum")
+            return self.file, start, size
+        if s != _lib.DIR_OK:
+            raise ReferencePanic("Reader::block: framing")
+        if self.verify:
+            batch = codec.DeviceBatch(self.file, off, ln, int(ln[0].item()))
+            if int(codec.crc32c_blocks(batch, framed=True)[1][0].item()):
+                raise ReferencePanic("Reader::block: checksum")
+        o, n = int(off[0].item()), int(ln[0].item()) & 0xFFFFFFFF
+        if self.compression == 0:
+            return self.file, o, n
+        return self._decompressed(o, n)
 
     def _seek_content(self, s):
         """Reader::block of an index seek's landed entry -> (tensor, off, len) of the content
@@ -509,34 +596,50 @@ class Reader:
             return self.file, int(s.data_off), int(s.data_len)
         # compressed: Block::init runs on the decompressed content (mtblx_block_seek_batch);
         # block_status's ERR / UNSUPPORTED judged the compressed bytes and do not apply
-        raw = self.file[int(s.data_off): int(s.data_off) + int(s.data_len)].cpu().numpy()
+        return self._decompressed(int(s.data_off), int(s.data_len))
+
+    def _decompressed(self, off: int, n: int):
+        """src/compression.rs:57-68 on the host for one stored block -> content on the device"""
+        raw = self.file[off: off + n].cpu().numpy()
         L = _lib.lib()
         out = _lib.u8p()
-        n = C.c_uint64(0)
+        un = C.c_uint64(0)
         src = raw if raw.size else np.zeros(1, np.uint8)
-        if L.mtblx_decompress(self.compression, src.ctypes.data, raw.size, C.byref(out), C.byref(n)) != 0:
+        if L.mtblx_decompress(self.compression, src.ctypes.data, raw.size, C.byref(out), C.byref(un)) != 0:
             raise MtblError(7)
-        b = C.string_at(out, n.value)
+        buf = np.empty(max(int(un.value), 1), np.uint8)   # no bytes object: blocks of GiBs
+        C.memmove(buf.ctypes.data, out, int(un.value))
         L.mtblx_free(out)
-        t = torch.frombuffer(bytearray(b or b"\0"), dtype=torch.uint8).to(self.file.device)
-        return t, 0, len(b)
+        t = torch.from_numpy(buf).to(self.file.device)
+        return t, 0, int(un.value)
 
     def _decode_range(self, i0: int, i1: int):
         """decode directory entries [i0, i1) -> (dir status, crc bad, decompress errors, decoded,
         (base tensor, content offsets, content lengths)) with host arrays"""
         off, ln, st = self._framing()
-        n = i1 - i0
-        dst = st[i0:i1].cpu().numpy()
         bad = self._bad_range(i0, i1)
+        return self._decode_framed(off[i0:i1], ln[i0:i1], st[i0:i1], bad)
+
+    def _decode_framed(self, off, ln, st, bad="verify"):
+        """decode framed blocks (off, len, dir status: device tensors); bad: the checksum
+        assert per block (device uint8), None when not verifying, "verify" to compute it"""
+        n = int(off.numel())
+        dst = st.cpu().numpy()
+        if isinstance(bad, str):
+            bad = None
+            if self.verify and n:
+                okl = torch.where(st == _lib.DIR_OK, ln, torch.zeros_like(ln))
+                batch = codec.DeviceBatch(self.file, off, okl, int(okl.max().item()))
+                bad = codec.crc32c_blocks(batch, framed=True)[1]
         bad = bad.cpu().numpy() if bad is not None else np.zeros(n, np.uint8)
         if self.compression != 0:
-            buf, uoff, uln, zerr = self._host_stage(off[i0:i1], ln[i0:i1], st[i0:i1])
+            buf, uoff, uln, zerr = self._host_stage(off, ln, st)
             batch = codec.DeviceBatch.from_host(buf, uoff, uln, device=self.file.device)
             where = (batch.data, uoff.astype(np.int64), uln.astype(np.int64))
         else:
             zerr = np.zeros(n, np.int32)
-            batch = codec.DeviceBatch(self.file, off[i0:i1], ln[i0:i1], int(ln[i0:i1].max().item()))
-            where = (self.file, off[i0:i1].cpu().numpy(), ln[i0:i1].cpu().numpy().view(np.uint32).astype(np.int64))
+            batch = codec.DeviceBatch(self.file, off, ln, int(ln.max().item()))
+            where = (self.file, off.cpu().numpy(), ln.cpu().numpy().view(np.uint32).astype(np.int64))
         data = codec.decode_blocks(batch)
         return dst, bad, zerr, data, where
 
@@ -551,16 +654,22 @@ class Reader:
     def _host_blocks(self, i0: int, i1: int):
         """blocks [i0, i1) as next() loads them, for the stateful iterator: per block an
         exception to raise (Err / panic) or ((tensor, off, len), records, emit end)"""
-        dst, bad, zerr, data, (base, boff, blen) = self._decode_range(i0, i1)
+        off, ln, st = self._framing()
+        recs = self._index_records()
+        return self._host_blocks_framed(off[i0:i1], ln[i0:i1], st[i0:i1], [recs[i][1] for i in range(i0, i1)],
+                                        self._bad_range(i0, i1))
+
+    def _host_blocks_framed(self, off, ln, st, values, bad="verify"):
+        dst, bad, zerr, data, (base, boff, blen) = self._decode_framed(off, ln, st, bad)
         h = data.to_host()
         out = []
-        for i in range(i1 - i0):
+        for i in range(len(values)):
             content = (base, int(boff[i]), int(blen[i]))
             if dst[i] == _lib.DIR_UNSUPPORTED:   # content >= 4 GiB
-                kind, em = self._big_block(i0 + i)
+                kind, em = self._big_block_value(values[i])
                 if kind == "ok":
-                    out.append(((self.file, self._big_frame(i0 + i)[1], self._big_frame(i0 + i)[2]),
-                                em.host_records(), em.end))
+                    fr = self._big_frame_value(values[i])
+                    out.append(((self.file, fr[1], fr[2]), em.host_records(), em.end))
                 elif kind in ("panic", "loop"):
                     out.append(ReferencePanic("Reader::block / BlockIter") if kind == "panic"
                                else ReferenceLoop("BlockIter::next"))

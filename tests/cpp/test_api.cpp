@@ -117,16 +117,19 @@ static void test_cfg1(mtbl::CompressionType c) {   // examples/dump.rs + get-key
   auto it = reader.iter_from(B("0000005000"));
   auto r0 = it.next();
   CHECK(r0 && S(r0->key, r0->key_len) == "0000005000");
-  CHECK(it.seek(B("0000009000")));                 // another block: loaded and seeked
+  // another block: loaded and seeked to the landed SEPARATOR (src/reader.rs:305,328); between
+  // keys that differ only in their last digit it is the block's last key
+  CHECK(it.seek(B("0000009000")));
   auto r1 = it.next();
-  CHECK(r1 && S(r1->key, r1->key_len) == "0000009000");
+  CHECK(r1 && S(r1->key, r1->key_len) >= "0000009000");
+  const std::string k1 = S(r1->key, r1->key_len);
   auto r2 = it.next();
-  CHECK(r2 && S(r2->key, r2->key_len) == "0000009001");
-  // block_offset is still 0 (next() never sets it, the seek above set it to 9000's block):
-  // a seek into block 0 now reloads block 0
+  CHECK(r2 && std::stoll(S(r2->key, r2->key_len)) == std::stoll(k1) + 1);   // the next block's first
+  // block_offset is now 9000's block: a seek into block 0 reloads block 0, seeked to its
+  // separator (its last key)
   CHECK(it.seek(B("0000000003")));
   auto r3 = it.next();
-  CHECK(r3 && S(r3->key, r3->key_len) == "0000000003");
+  CHECK(r3 && S(r3->key, r3->key_len) > "0000000003" && S(r3->key, r3->key_len) < "0000000100");
   // the block_offset quirk: a fresh iter_from keeps block_offset 0, so seeking into block 0
   // (offset 0) re-seeks the block it holds instead of loading block 0
   auto q = reader.iter_from(B("0000005000"));
@@ -135,6 +138,55 @@ static void test_cfg1(mtbl::CompressionType c) {   // examples/dump.rs + get-key
   auto r4 = q.next();
   CHECK(r4 && S(r4->key, r4->key_len) != "0000000003" && S(r4->key, r4->key_len) <= "0000005000");
   CHECK(q.seek(B("zzz")) && !q.next().has_value());   // past the last key
+}
+
+// the hand-derived vectors of tests/golden/kat.json (seek_kat, make_golden.py): separators
+// equal to the last key, bumped, and appended by write_u16 (src/writer.rs:239-265)
+static void test_seek_kat() {
+  const char* keys[] = {"key-0000", "key-0001", "key-0002", "key-0003", "key-0004", "key-0005",
+                        "key-0007", "key-0008", "key-0009ab", "key-000:ac", "key-000;"};
+  mtbl::Writer w = mtbl::WriterBuilder().block_size(1024).block_restart_interval(16).memory();
+  for (int i = 0; i < 11; ++i) w.insert(std::string(keys[i]), std::string(300, (char)(0x41 + i)));
+  const mtbl::Reader r = mtbl::Reader::open(w.into_inner());
+  CHECK(r.metadata().count_data_blocks == 4);
+  auto keys_of = [](mtbl::ReaderIntoIter& it, int n) {
+    std::vector<std::string> out;
+    for (int i = 0; i < n; ++i) {
+      auto x = it.next();
+      if (!x) break;
+      out.push_back(S(x->key, x->key_len));
+    }
+    return out;
+  };
+  using V = std::vector<std::string>;
+  {
+    auto it = r.into_iter();
+    it.seek(B("key-0001"));
+    CHECK((keys_of(it, 3) == V{"key-0002", "key-0003", "key-0004"}));
+  }
+  {
+    auto it = r.into_iter();
+    it.seek(B("key-0004"));
+    CHECK((keys_of(it, 2) == V{"key-0007", "key-0008"}));
+  }
+  {
+    auto it = r.into_iter();
+    it.seek(B("key-0008"));
+    CHECK((keys_of(it, 1) == V{"key-000:ac"}));
+  }
+  {
+    auto it = r.into_iter();
+    it.seek(B("key-000;"));
+    CHECK((keys_of(it, 2) == V{"key-000;"}));
+    it.seek(B("key-000<"));
+    CHECK(keys_of(it, 1).empty());
+  }
+  {
+    auto it = r.iter_from(B("key-0005"));
+    CHECK((keys_of(it, 3) == V{"key-0005", "key-0007", "key-0008"}));
+    it.seek(B("key-0000"));
+    CHECK((keys_of(it, 4) == V{"key-0007", "key-0008", "key-0009ab", "key-0003"}));
+  }
 }
 
 static void test_errors() {
@@ -167,6 +219,7 @@ int main() {
   test_cfg1(mtbl::CompressionType::None);
   test_cfg1(mtbl::CompressionType::Snappy);
   test_errors();
+  test_seek_kat();
   std::printf("OK %d\n", g_checks);
   return 0;
 }

@@ -83,6 +83,53 @@ QUIRKS = [
 ]
 
 
+# --- ReaderIntoIter::seek (src/reader.rs:302-335), hand-derived ---
+# Writer(block_size 1024, restart interval 16, None); every value is 300 bytes, so the flush
+# rule (src/writer.rs:125-130) cuts a block after three 8-byte keys (311 + 304 + 304 B).
+# Separators (src/writer.rs:239-265):
+#   block 0 key-0000 .. key-0002 | next key-0003: '2'+1 == '3', no u16 room -> "key-0002" (= last key)
+#   block 1 key-0003 .. key-0005 | next key-0007: '5'+1 <  '7'              -> "key-0006" (bumped)
+#   block 2 key-0007, key-0008, key-0009ab | next key-000:ac: '9'+1 == ':', diff 7 < 10-2 ->
+#           write_u16 APPENDS BE16("9a")+1 = "9b"                           -> "key-0009ab9b"
+#   block 3 key-000:ac, key-000;  (last index entry = the last key, :158-162)
+# seek(k) lands the index iterator on the first separator >= k and seeks the data block to
+# that SEPARATOR (`key` is shadowed at :305), so seek + next() yields the landed block's last
+# record when the separator equals it, else the next block's first record.
+SEEK_KAT = {
+    "block_size": 1024, "restart_interval": 16, "value_len": 300,
+    "keys": ["key-0000", "key-0001", "key-0002", "key-0003", "key-0004", "key-0005", "key-0007", "key-0008",
+             "key-0009ab", "key-000:ac", "key-000;"],
+    "separators": ["key-0002", "key-0006", "key-0009ab9b", "key-000;"],
+    "scripts": [
+        {"mode": "iter", "key": "", "ops": [["seek", "key-0001"], 3],
+         "yields": ["key-0002", "key-0003", "key-0004"],
+         "why": "index entry 0 (sep key-0002 = last key), block 0 already held (offset 0): seek(key-0002)"},
+        {"mode": "iter", "key": "", "ops": [["seek", "key-0004"], 2], "yields": ["key-0007", "key-0008"],
+         "why": "entry 1, sep key-0006 past block 1's keys: next() moves to block 2"},
+        {"mode": "iter", "key": "", "ops": [["seek", "key-0008"], 1], "yields": ["key-000:ac"],
+         "why": "entry 2, appended sep key-0009ab9b > key-0009ab: next() moves to block 3"},
+        {"mode": "iter", "key": "", "ops": [["seek", "key-000;"], 2], "yields": ["key-000;"],
+         "why": "last entry: the last record, then None"},
+        {"mode": "iter", "key": "", "ops": [["seek", "key-000<"], 1], "yields": [],
+         "why": "past the last separator: valid = false"},
+        {"mode": "from", "key": "key-0005", "ops": [3, ["seek", "key-0000"], 4],
+         "yields": ["key-0005", "key-0007", "key-0008", "key-0007", "key-0008", "key-0009ab", "key-0003"],
+         "why": "new_from seeks block 1 with the CALLER's key; seek(key-0000) lands entry 0 at offset 0 = "
+                "block_offset: the held block 2 is seeked to key-0002 -> key-0007; after block 2 the index "
+                "iterator (at entry 0) moves to entry 1 -> block 1"},
+    ],
+}
+
+
+def seek_kat_records():
+    v = SEEK_KAT["value_len"]
+    return [(k.encode(), bytes([0x41 + i]) * v) for i, k in enumerate(SEEK_KAT["keys"])]
+
+
+def seek_kat_ops(script):
+    return [o if isinstance(o, int) else ("seek", o[1].encode()) for o in script["ops"]]
+
+
 def build_files():
     import pyoracle as o
     one = o.write_file([(b"hello", b"I'm the one")])
@@ -115,7 +162,7 @@ def main():
         return
     open(os.path.join(HERE, "one_key.mtbl"), "wb").write(one)
     open(os.path.join(HERE, "empty.mtbl"), "wb").write(empty)
-    json.dump(KAT, open(os.path.join(HERE, "kat.json"), "w"), indent=1)
+    json.dump(dict(KAT, seek_kat=SEEK_KAT), open(os.path.join(HERE, "kat.json"), "w"), indent=1)
     json.dump(QUIRKS, open(os.path.join(HERE, "quirk_blocks.json"), "w"), indent=1)
     print("wrote tests/golden/{one_key,empty}.mtbl, kat.json, quirk_blocks.json")
 

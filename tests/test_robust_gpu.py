@@ -143,3 +143,36 @@ def test_lookback_timeout_rejected_everywhere(oracle, monkeypatch, tmp_path):
     if os.path.exists(dump):
         r = subprocess.run([dump, str(path)], capture_output=True, timeout=120)
         assert r.returncode == 0 and r.stdout.count(b"\n") == 2000
+
+
+def test_timeout_before_tile0_survives(oracle, monkeypatch):
+    """tile 0's walker zeroes totals[3] right before it publishes A(0); a
+    workgroup whose look-back on A(0) gave up BEFORE that (workgroup 0 late / not resident) must
+    still see its timeout reported.  Knobs: the bounded waits give up after 20 ms and tile 0's
+    walker publishes 300 ms late, so every other workgroup's first look-back times out first."""
+    codec = _codec()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(600)          # 50 tiles: one round of look-backs on A(0)
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    ref = codec.decode_blocks(batch)
+    torch.cuda.synchronize()
+    tot = ref.totals_host()
+    assert tot[3] == 0
+    ws = codec.Workspace(batch.nblk)
+    out = codec.decode_blocks(batch)              # outputs of the right size
+    torch.cuda.synchronize()
+    monkeypatch.setenv("MTBLX_DEBUG_WAIT_MS", "20")
+    monkeypatch.setenv("MTBLX_DEBUG_DELAY0_MS", "300")
+    codec.decode_into(batch, out, ws)
+    torch.cuda.synchronize()
+    assert out.totals_host(check=False)[3] & 2
+    with pytest.raises(codec.LaunchTimeout):
+        out.to_host()
+    monkeypatch.delenv("MTBLX_DEBUG_DELAY0_MS")
+    monkeypatch.delenv("MTBLX_DEBUG_WAIT_MS")
+    codec.decode_into(batch, out, ws)             # the workspace and outputs work again
+    torch.cuda.synchronize()
+    assert out.totals_host() == tot
+    h, r = out.to_host(), ref.to_host()
+    assert np.array_equal(h.keys, r.keys) and np.array_equal(h.key_end, r.key_end)

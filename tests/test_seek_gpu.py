@@ -232,6 +232,112 @@ def test_stateful_random_scripts(oracle, comp):
             _script_check(oracle, d, verify, mode, k if mode != "prefix" else k[:2], k + b"\x80", ops)
 
 
+def _index_window(data):
+    """(content offset, length) of the index block (footer -> varint64 length | crc | content)"""
+    off = int.from_bytes(data[len(data) - 512: len(data) - 504], "little")
+    n, sh, p = 0, 0, off
+    while True:
+        b = data[p]
+        n |= (b & 0x7F) << sh
+        sh += 7
+        p += 1
+        if b < 128:
+            break
+    return p + 4, n
+
+
+def test_seek_kat_gpu(oracle):
+    """the hand-derived ReaderIntoIter::seek vectors (tests/golden/kat.json seek_kat): the data
+    block is seeked to the landed separator (src/reader.rs:305,328) -- equal to the last key,
+    bumped, and write_u16-appended"""
+    import json
+    import os
+    kat = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kat.json")))["seek_kat"]
+    recs = [(k.encode(), bytes([0x41 + i]) * kat["value_len"]) for i, k in enumerate(kat["keys"])]
+    data, _ = _write(recs, kat["block_size"], kat["restart_interval"])
+    assert data == oracle.write_file(recs, kat["block_size"], kat["restart_interval"])
+    for sc in kat["scripts"]:
+        ops = [o if isinstance(o, int) else ("seek", o[1].encode()) for o in sc["ops"]]
+        got = _run_script(data, True, sc["mode"], sc["key"].encode(), b"", ops)
+        assert [k.decode() for k, _ in got["records"]] == sc["yields"], sc["why"]
+        _script_check(oracle, data, True, sc["mode"], sc["key"].encode(), b"", ops)
+
+
+def _corrupt_index(data, rng, kind):
+    """a copy whose INDEX block is damaged: "restart" sets shared != 0 in entries at restart
+    points (BlockIter::seek's early return on the live index iterator, src/block.rs:167-170;
+    key-capacity asserts), "shared" raises shared past the previous key's length in plain
+    entries (truncate no-ops: keys rebuilt from another restart differ), "bytes" flips bytes"""
+    d = bytearray(data)
+    o, L = _index_window(data)
+    nr = int.from_bytes(d[o + L - 4: o + L], "little")
+    ro = L - 4 * (nr + 1)
+    if kind == "bytes":
+        for _ in range(3):
+            d[o + int(rng.integers(0, max(ro, 1)))] ^= int(rng.integers(1, 256))
+        return bytes(d)
+    rps = [int.from_bytes(d[o + ro + 4 * i: o + ro + 4 * i + 4], "little") for i in range(nr)]
+    if kind == "restart":
+        for i in rng.choice(nr, size=min(nr, 4), replace=False):
+            p = rps[int(i)]
+            if p + 3 < ro and d[o + p] == 0 and d[o + p + 1] < 128 and d[o + p + 2] < 128:
+                d[o + p] = int(rng.integers(1, 12))
+        return bytes(d)
+    p, n = rps[0], 0                                  # walk the chain, bump some shared fields
+    while p + 3 <= ro and n < 100000:
+        sh, ns, vl = d[o + p], d[o + p + 1], d[o + p + 2]
+        if sh >= 128 or ns >= 128 or vl >= 128:
+            break
+        if p not in rps and rng.random() < 0.15:
+            d[o + p] = min(127, sh + int(rng.integers(1, 20)))
+        p += 3 + ns + vl
+        n += 1
+    return bytes(d)
+
+
+@pytest.mark.parametrize("kind", ["restart", "shared", "bytes"])
+def test_stateful_live_index_iterator(oracle, kind):
+    """ReaderIntoIter::seek re-seeks the LIVE index iterator (src/reader.rs:303): on a corrupt
+    index (verification off) an early return keeps its old position and key capacity, and
+    next() continues from wherever the seek left it, on or off the scan chain"""
+    rng = np.random.default_rng({"restart": 11, "shared": 12, "bytes": 13}[kind])
+    recs = corpus.random_records(rng, 3000, 1, 20, 0, 40)
+    data, _ = _write(recs, 256, 2)             # many blocks: an index with many restart points
+    seen_irregular = 0
+    for t in range(6):
+        bad = _corrupt_index(data, rng, kind)
+        rd = _mods()
+        try:
+            r = rd.ReaderBuilder().verify_checksums(False).read(bad)
+            seen_irregular += not r.index_regular()
+        except (rd.MtblError, rd.ReferencePanic):
+            pass
+        for _ in range(5):
+            keys = _probe_keys(rng, recs, 8)
+            ops = []
+            for _ in range(int(rng.integers(3, 10))):
+                if rng.random() < 0.5:
+                    ops.append(("seek", keys[int(rng.integers(0, len(keys)))]))
+                else:
+                    ops.append(int(rng.choice([1, 3, 20, 200])))
+            mode = str(rng.choice(["iter", "from", "prefix", "range"]))
+            k = keys[int(rng.integers(0, len(keys)))]
+            _script_check(oracle, bad, False, mode, k if mode != "prefix" else k[:2], k + b"\x80", ops)
+        for k in _probe_keys(rng, recs, 6):
+            for mode, k1, k2 in (("from", k, b""), ("prefix", k[:2], b""), ("range", k, k + b"\xff")):
+                try:
+                    r = rd.ReaderBuilder().verify_checksums(False).read(bad)
+                except (rd.MtblError, rd.ReferencePanic):
+                    break
+                exp = oracle.file_scan(bad, mode, k1, k2, verify=False)
+                sc = {"from": lambda: r.iter_from(k1), "prefix": lambda: r.iter_prefix(k1),
+                      "range": lambda: r.iter_range(k1, k2)}[mode]()
+                assert sc.end == exp["end"], (kind, mode, k1, k2)
+                assert sc.records() == exp["records"], (kind, mode, k1, k2)
+    if kind != "bytes":
+        assert seen_irregular > 0
+
+
 def test_compressed_get_matches_oracle(oracle):
     rd = _mods()
     rng = np.random.default_rng(5)

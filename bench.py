@@ -10,9 +10,11 @@ A step = one full decode of the resident batch through the C ABI (mtblx_decode_b
 one single-pass k_decode_pipe launch for blocks <= 48 KiB, k_decode_tiles above), i.e. every block's records reconstructed and laid
 out contiguously in HBM.  Inputs are in HBM before timing starts.
 
-Multi-GPU (torchrun, one rank per GPU): blocks are independent, so every rank decodes
-its own 100 k-block shard (weak scaling, no data-path collective); the only collectives
-are the timing barrier and the max-over-ranks reduction.
+Multi-GPU: `--gpus N` runs N ranks, one per GPU -- launched here with torch.distributed.run
+when the environment does not already hold them (WORLD_SIZE must equal N otherwise).  Blocks
+are independent, so rank r decodes its own 100 k-block shard of one rank-partitioned key space
+(synth.cfg2_shard: weak scaling, no data-path collective); the only collectives are the timing
+barrier, the max-over-ranks reduction of the time and the sum of the bytes / records decoded.
 
 Prints ONE JSON line on rank 0.
 """
@@ -39,16 +41,30 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(data, off, ln, budget_s: float):
-    """CPU restatement of src/block.rs (oracle/, reference semantics) on this host's cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    pyoracle.build()
+def host_cores():
+    """(CPUs in this process's affinity mask, the cgroup CPU quota in whole CPUs or None)"""
     try:
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+    quota = None
+    try:   # cgroup v2 "max period" / "quota period"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return ncpu, quota
+
+
+def cpu_baseline(data, off, ln, budget_s: float):
+    """CPU restatement of src/block.rs (oracle/, reference semantics) on this host's cores:
+    one thread per CPU of the affinity mask (fewer only if a cgroup CPU quota caps the process)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pyoracle.build()
+    ncpu, quota = host_cores()
+    threads = max(1, min(ncpu, quota) if quota else ncpu)
     nblk = off.size
     # 1 thread on a bounded sample, repeated to take >= 1.5 s
     sample = min(nblk, 20_000)
@@ -65,6 +81,8 @@ def cpu_baseline(data, off, ln, budget_s: float):
         "value": bytesT / tT / 2**30,
         "unit": "GiB/s",
         "cores": threads,
+        "affinity_cpus": ncpu,
+        "cgroup_cpu_quota": quota,
         "kind": "port",
         "records_per_s": rT / tT,
         "single_thread_GiBs": bytes1 / t1 / 2**30,
@@ -364,12 +382,73 @@ def _timed(fn, stream, reps):
     return e0.elapsed_time(e1) / reps
 
 
-def _max_over_ranks(x, dist):
+def _reduce_over_ranks(x, dist, op: str, device="cuda"):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def _max_over_ranks(x, dist, device="cuda"):
+    return _reduce_over_ranks(x, dist, "max", device)
+
+
+def _sum_over_ranks(x, dist, device="cuda"):
+    return _reduce_over_ranks(x, dist, "sum", device)
+
+
+def launch_command(args_list, gpus: int, port: int):
+    """the torch.distributed.run command that runs this script as `gpus` ranks"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(args_list)
+
+
+def maybe_launch(args, argv) -> int | None:
+    """--gpus N > 1 outside torchrun: start the N ranks as a child process (before this process
+    touches the GPU: torch.cuda.device_count() does not initialise it) and return its exit code;
+    None when this process is a rank (or N == 1) and goes on."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    nvis = torch.cuda.device_count()
+    if nvis < args.gpus:
+        log(f"--gpus {args.gpus}: only {nvis} GPU(s) visible")
+        return 2
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    import subprocess
+    return subprocess.call(launch_command(argv, args.gpus, port))
+
+
+def init_ranks(args, backend: str = "nccl"):
+    """rank set-up from the torchrun environment -> (dist or None, world, rank, local).  The
+    world must be the --gpus the run was asked for."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: launch with --nproc-per-node {args.gpus}")
+    if backend == "nccl":
+        if torch.cuda.device_count() < world:
+            raise SystemExit(f"--gpus {world}: only {torch.cuda.device_count()} GPU(s) visible")
+        torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return dist, world, rank, local
+
+
+def rank_totals(block_bytes: int, nrec: int, elapsed: float, dist, device="cuda"):
+    """whole-job totals: (bytes over all ranks, records over all ranks, max elapsed)"""
+    return (int(_sum_over_ranks(float(block_bytes), dist, device)), int(_sum_over_ranks(float(nrec), dist, device)),
+            _max_over_ranks(elapsed, dist, device))
 
 
 def run_cfg3(args, dist, world, rank):
@@ -614,7 +693,7 @@ def run_cfg4(args, dist, world, rank):
     return res
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -642,7 +721,15 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per decode launch (profiles/, written by scripts/pmc_traffic.py "
                          "from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    rc = maybe_launch(args, argv)
+    if rc is not None:
+        sys.exit(rc)
 
     if args.stamps or (args.lib and not os.environ.get("MTBLX_AB_CRC")):
         args.no_crc = True    # diagnostic builds: decode timing only (MTBLX_AB_CRC=1: keep the CRC legs)
@@ -650,14 +737,7 @@ def main():
         os.environ["MTBLX_LIB"] = args.lib or os.path.join(ROOT, "oxidized-mtbl_amd", "mtblx", "libmtblx_stamps.so")
     elif args.lib:
         os.environ["MTBLX_LIB"] = args.lib
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist, world, rank, local = init_ranks(args)
 
     from mtblx import codec, synth
 
@@ -670,7 +750,7 @@ def main():
         return
 
     t = time.time()
-    data, off, ln = synth.cfg2_file(args.blocks, block_size=args.block_size, seed=synth.SEED_CFG2 + rank)
+    data, off, ln = synth.cfg2_shard(rank, world, args.blocks, block_size=args.block_size)
     exp_nrec = int(synth.cfg2_file.last_block_nrec.sum(dtype=np.uint64))  # records the Writer put in these blocks
     log(f"[rank {rank}] generated {off.size} blocks / {data.size / 2**20:.1f} MiB in {time.time() - t:.1f}s")
     batch = codec.DeviceBatch.from_host(data, off, ln)
@@ -822,9 +902,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    block_bytes = int(ln.sum(dtype=np.uint64))
+    total_bytes, total_recs, elapsed = rank_totals(block_bytes, int(nrec), elapsed, dist)
 
     k_decode_ms = e_start.elapsed_time(e_end) / args.steps
     if out.totals_host() != h:   # the timed launches decoded the same totals
@@ -844,8 +923,6 @@ def main():
         log(f"wall: preload end -> timed start {1e3 * (t0 - _T_PRE_END):.2f} ms")
         log(f"timed region {k_decode_ms:.4f} ms/launch; chunks of 20 after: {cs}")
     ms_per_step = elapsed * 1e3 / args.steps
-    total_bytes = block_bytes * world
-    total_recs = nrec * world
     value = total_bytes / (elapsed / args.steps) / 2**30
 
     # roofline of the (only) decode kernel: algorithmic bytes per launch / its launch duration
@@ -886,7 +963,9 @@ def main():
                                ", 16 B keys / 64 B values, restart_interval=16, compression=none, device-resident decode",
                    "blocks_per_gpu": int(batch.nblk), "block_bytes_per_gpu": block_bytes,
                    "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
-                   "parallelism": f"block-sharded x{world}, no collective"},
+                   "parallelism": f"block-sharded x{world}, no collective" + (
+                       f" (rank-partitioned key space, synth.cfg2_shard; {total_bytes} block bytes over all ranks)"
+                       if world > 1 else "")},
         "kernels_ms": {f"{kernel} (HIP events around the timed region / steps)": round(k_decode_ms, 4)},
         "host_enqueue_ms_per_step": round(t_enq * 1e3 / args.steps, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

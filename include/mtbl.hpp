@@ -350,6 +350,7 @@ class Reader {
   static Reader open(const Bytes& data);
   static Reader open(const uint8_t* data, size_t len);
   Metadata metadata() const { return meta_; }
+  uint32_t file_version() const { return version_; }   // Metadata::file_version: 0 FormatV1, 1 FormatV2
   // Reader::into_iter (src/reader.rs:124-126)
   ReaderIntoIter into_iter() const {
     ReaderIntoIter it(this, ReaderIntoIter::kIter, {});

@@ -59,17 +59,33 @@ int zlib_decompress(const uint8_t* src, uint64_t n, std::vector<uint8_t>& out) {
   return MTBLX_CODEC_OK;
 }
 
+// flate2's ZlibEncoder streams any length; zlib's avail_in / avail_out are 32-bit, so the input
+// is fed in pieces of <= 1 GiB (Z_NO_FLUSH), then Z_FINISH, the output grown as needed
 int zlib_compress(uint32_t level, const uint8_t* src, uint64_t n, std::vector<uint8_t>& out) {
   z_stream z;
   memset(&z, 0, sizeof z);
   if (deflateInit(&z, (int)std::min<uint32_t>(level, 9)) != Z_OK) return MTBLX_CODEC_CORRUPT;
-  out.resize(deflateBound(&z, (uLong)n) + 64);
-  z.next_in = const_cast<Bytef*>(src);
-  z.avail_in = (uInt)n;
-  z.next_out = out.data();
-  z.avail_out = (uInt)out.size();
-  const int r = deflate(&z, Z_FINISH);
-  out.resize(z.total_out);
+  constexpr uint64_t kPiece = 1ull << 30;
+  out.resize(std::min<uint64_t>(deflateBound(&z, (uLong)std::min<uint64_t>(n, kPiece)) + 64, n + (1u << 20)) + 64);
+  uint64_t in_left = n, done = 0;
+  int r = Z_OK;
+  for (;;) {
+    if (z.avail_in == 0 && in_left) {
+      const uint64_t take = std::min(in_left, kPiece);
+      z.next_in = const_cast<Bytef*>(src + (n - in_left));
+      z.avail_in = (uInt)take;
+      in_left -= take;
+    }
+    if (out.size() - done < (1u << 16)) out.resize(out.size() + std::max<uint64_t>(out.size() / 2, 1u << 20));
+    z.next_out = out.data() + done;
+    z.avail_out = (uInt)std::min<uint64_t>(out.size() - done, kPiece);
+    const uInt before = z.avail_out;
+    r = deflate(&z, in_left == 0 ? Z_FINISH : Z_NO_FLUSH);
+    done += before - z.avail_out;
+    if (r == Z_STREAM_END) break;
+    if (r != Z_OK && r != Z_BUF_ERROR) break;
+  }
+  out.resize(done);
   deflateEnd(&z);
   return r == Z_STREAM_END ? MTBLX_CODEC_OK : MTBLX_CODEC_CORRUPT;
 }

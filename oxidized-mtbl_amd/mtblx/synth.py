@@ -26,11 +26,11 @@ def cfg1_records(n=10_000):
         yield k.encode(), (k * (1 + i % 8)).encode()
 
 
-def cfg2_arrays(nrec: int, seed: int = SEED_CFG2, key_tail: int = 8, val_len: int = 64):
-    """keys (nrec*16 u8), values (nrec*64 u8) in record order."""
+def cfg2_arrays(nrec: int, seed: int = SEED_CFG2, key_tail: int = 8, val_len: int = 64, c0: int = 0):
+    """keys (nrec*16 u8), values (nrec*64 u8) in record order; the key counter starts at c0."""
     rng = np.random.default_rng(seed)
     gaps = rng.integers(1, 1 << 20, nrec, dtype=np.uint64)
-    c = np.cumsum(gaps, dtype=np.uint64)
+    c = np.cumsum(gaps, dtype=np.uint64) + np.uint64(c0)
     klen = 8 + key_tail
     keys = np.empty((nrec, klen), np.uint8)
     keys[:, :8] = c.astype(">u8").view(np.uint8).reshape(nrec, 8)
@@ -51,20 +51,35 @@ def write_arrays(keys, vals, klen, vlen, block_size=4096, restart_interval=16):
     return data, off, ln
 
 
-def cfg2_file(nblocks: int = 100_000, block_size: int = 4096, seed: int = SEED_CFG2):
+def cfg2_file(nblocks: int = 100_000, block_size: int = 4096, seed: int = SEED_CFG2, c0: int = 0):
     """-> (file bytes as uint8 array, blk_off[nblocks], blk_len[nblocks]); exactly `nblocks` data blocks
-    of the file are returned in the directory (the file may hold a few more)."""
+    of the file are returned in the directory (the file may hold a few more).  c0: first key
+    counter (shards of one key space: cfg2_shard)."""
     # ~51 records per 4 KiB block; generous estimate then trim the directory
     per_block = max(1, (block_size - 64) // 79)
     nrec = int(nblocks * per_block * 1.02) + 64
-    keys, vals, kl, vl = cfg2_arrays(nrec, seed)
+    keys, vals, kl, vl = cfg2_arrays(nrec, seed, c0=c0)
     data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
     while off.size < nblocks:  # extremely unlikely; extend
         nrec = int(nrec * 1.1)
-        keys, vals, kl, vl = cfg2_arrays(nrec, seed)
+        keys, vals, kl, vl = cfg2_arrays(nrec, seed, c0=c0)
         data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
     cfg2_file.last_block_nrec = write_arrays.last_block_nrec[:nblocks].copy()
     return data, off[:nblocks].copy(), ln[:nblocks].copy()
+
+
+SHARD_KEY_BITS = 56   # rank r's key counters start at r << 56 (a shard holds < 2^43 of them)
+
+
+def cfg2_shard(rank: int, world: int, nblocks: int = 100_000, block_size: int = 4096):
+    """Rank `rank`'s shard of a multi-GPU cfg2 workload: the key space is partitioned by rank
+    (counters from rank << 56, seed SEED_CFG2 + rank), so the shards in rank order are one
+    strictly increasing record stream -- the blocks of one logical file cut at block
+    boundaries -- and every rank generates and decodes only its own `nblocks` blocks (weak
+    scaling: per-GPU work fixed as the GPU count grows; no data-path collective)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    return cfg2_file(nblocks, block_size, seed=SEED_CFG2 + rank, c0=rank << SHARD_KEY_BITS)
 
 
 def cfg3_key_len_probs():

@@ -15,7 +15,7 @@ BIN = os.path.join(PKG, "build")
 
 
 def _built():
-    for b in ("dump", "get_key", "test_api"):
+    for b in ("dump", "get_key", "info", "test_api"):
         if not os.path.exists(os.path.join(BIN, b)):
             pytest.skip(f"{b} not built (make -C oxidized-mtbl_amd cpp)")
 
@@ -25,7 +25,7 @@ def test_cpp_surface_builds():
         pytest.skip("no hipcc")
     subprocess.run(["make", "-s", "-C", PKG, "cpp"], check=True)
     _built()
-    for b in ("dump", "get_key", "test_api"):
+    for b in ("dump", "get_key", "info", "test_api"):
         out = subprocess.run(["ldd", os.path.join(BIN, b)], capture_output=True, text=True).stdout
         assert "libmtblx.so" in out and "not found" not in out.split("libmtblx.so")[1].splitlines()[0], out
 
@@ -69,3 +69,20 @@ def test_cpp_dump_and_get_key(tmp_path, oracle, compression):
     assert r.returncode == 0 and r.stdout == b'"' + k + b'" "' + v + b'"\n', r
     r = subprocess.run([os.path.join(BIN, "get_key"), str(path), "nope"], capture_output=True, timeout=60)
     assert r.returncode == 0 and r.stdout == b"entry not found\n", r
+
+
+@pytest.mark.gpu
+def test_cpp_info_golden():
+    """examples/info.rs (Reader::new + `{:#?}` of the Metadata) on the one_key golden file, whose
+    footer is hand-derived in SURVEY.md §2.2 / tests/golden/kat.json"""
+    _gpu()
+    gold = os.path.join(ROOT, "tests", "golden", "one_key.mtbl")
+    r = subprocess.run([os.path.join(BIN, "info"), gold], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == ("Metadata {\n    file_version: FormatV2,\n    index_block_offset: 32,\n"
+                        "    data_block_size: 8192,\n    compression_algorithm: None,\n    count_entries: 1,\n"
+                        "    count_data_blocks: 1,\n    bytes_data_blocks: 32,\n    bytes_index_block: 22,\n"
+                        "    bytes_keys: 5,\n    bytes_values: 11,\n}\n")
+    r = subprocess.run([os.path.join(BIN, "info"), os.path.join(ROOT, "tests", "golden", "kat.json")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 101 and "InvalidMetadataSize" not in r.stdout   # not an mtbl file: unwrap panics

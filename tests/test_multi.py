@@ -91,3 +91,81 @@ def test_gpu_two_shards_concat_equals_single_batch():
     cat = shard.concat_shards(parts)
     for k in ("nrec", "status", "rec_base", "key_base", "val_base", "key_end", "val_end", "keys", "vals"):
         assert np.array_equal(cat[k], getattr(full, k)), k
+
+
+def _bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _bench_rank(rank, world, port, q):
+    """bench.py's own rank path (init_ranks, the rank's cfg2 shard, rank_totals) on gloo, with
+    the oracle's scan standing in for the device decode step"""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import pyoracle
+    bench = _bench()
+    args = bench.parse_args(["--gpus", str(world), "--blocks", "120", "--steps", "3"])
+    dist_, w, r, _ = bench.init_ranks(args, backend="gloo")
+    assert (w, r) == (world, rank) and dist_ is not None
+    data, off, ln = synth.cfg2_shard(r, w, args.blocks)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        d = pyoracle.decode_blocks(data, off, ln)
+    el = time.perf_counter() - t0 + 0.05 * rank          # ranks finish at different times
+    nrec = int(d.nrec.sum())
+    tb, tr, tmax = bench.rank_totals(int(ln.sum()), nrec, el, dist_, device="cpu")
+    first = bytes(d.records(0)[0][0])
+    b = int(np.nonzero(d.nrec)[0][-1])
+    last = bytes(d.records(b)[-1][0])
+    edges = [None] * w
+    dist_.all_gather_object(edges, (first, last, int(ln.sum()), nrec, el))   # checking only
+    if r == 0:
+        q.put((tb, tr, tmax, edges))
+    dist_.barrier()
+    dist_.destroy_process_group()
+
+
+def test_gloo_bench_rank_path(oracle):
+    """bench.py --gpus N runs N ranks that each decode their own shard; the line's
+    value is the bytes of ALL ranks over the slowest rank's time.  Driven through bench.py's
+    own functions on world_size-2 gloo (CPU); the shards continue one strictly increasing key
+    space in rank order (one logical file cut at block boundaries)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    tb, tr, tmax, edges = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert tb == sum(e[2] for e in edges) and tr == sum(e[3] for e in edges)
+    assert tmax == max(e[4] for e in edges)
+    assert edges[0][1] < edges[1][0]                      # rank 0's last key < rank 1's first key
+    assert all(e[0] < e[1] for e in edges)
+
+
+def test_bench_launch_and_world_checks(monkeypatch):
+    """--gpus N outside torchrun re-launches through torch.distributed.run (N ranks); inside a
+    launch, WORLD_SIZE must equal --gpus"""
+    bench = _bench()
+    args = bench.parse_args(["--gpus", "4", "--steps", "7"])
+    cmd = bench.launch_command(["--gpus", "4", "--steps", "7"], 4, 29555)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=4" in cmd
+    assert "--master-addr" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "7"] and cmd[-5].endswith("bench.py")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.maybe_launch(args, []) is None                 # already a rank: no re-launch
+    with pytest.raises(SystemExit):
+        bench.init_ranks(args, backend="gloo")                   # WORLD_SIZE 2 != --gpus 4
+    monkeypatch.delenv("WORLD_SIZE")
+    one = bench.parse_args([])
+    assert one.gpus == 1 and bench.maybe_launch(one, []) is None

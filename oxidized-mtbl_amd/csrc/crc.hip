@@ -10,6 +10,7 @@
 // and the wave XOR-reduces; see k_crc32c_blocks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "crc_dev.h"
 #include "mtblx.h"
@@ -150,7 +151,192 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Round 3: the block's first window (k = lane) is loaded one block AHEAD (the loads of block
+// b + waves are in flight while block b is computed), and S72 computes a window's raw CRC
+// without a serial chain: byte i of the 72-byte window is followed by 71 - i bytes, so
+//   crc_raw(window) = XOR_i T72[71 - i][byte_i],   T72[d][x] = crc_raw(x followed by d zeros)
+// -- 72 independent lookups instead of 9 dependent slicing-by-8 steps.  T72 (72 KiB) and the
+// shift tables (40 KiB) fill 112 KiB of LDS: one 1024-thread workgroup per CU, as the VGPRs
+// allowed before.
+struct Slice72 {
+  uint32_t t[kCrcWin][256];
+  constexpr Slice72() : t() {
+    for (uint32_t x = 0; x < 256; ++x) {
+      uint32_t c = x;
+      for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
+      t[0][x] = c;
+    }
+    for (int d = 1; d < kCrcWin; ++d)
+      for (uint32_t x = 0; x < 256; ++x) t[d][x] = (t[d - 1][x] >> 8) ^ t[0][t[d - 1][x] & 0xFFu];
+  }
+};
+static __constant__ Slice72 kS72 = Slice72();
+struct Slice72Lds {
+  uint32_t t[kCrcWin][256];
+};
+
+// the 18 words of the window [hi - kCrcWin, hi) of block d (bytes before the block as zeros,
+// the 0xFFFFFFFF init folded into bytes 0..3)
+__device__ __forceinline__ void window_words(const uint8_t* d, int64_t hi, bool safe, uint32_t (&w)[kWords]) {
+  const int64_t lo = hi - kCrcWin;
+  if (safe) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const v4u x = crc_ld16(d + lo + 16 * q);
+      w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+    }
+    const v2u y = crc_ld8(d + lo + 64);
+    w[16] = y.x; w[17] = y.y;
+  } else {
+#pragma unroll
+    for (int m = 0; m < kWords; ++m) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int64_t p = lo + 4 * m + b;
+        v |= (p >= 0 ? (uint32_t)d[p] : 0u) << (8 * b);
+      }
+      w[m] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void window_fold(int64_t lo, uint32_t (&w)[kWords]) {
+  if (lo < 4) {
+#pragma unroll
+    for (int m = 0; m < kWords; ++m) {
+      const int64_t pos = lo + 4 * m;
+      if (pos < 4) {
+        const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+        const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8 * (uint32_t)pos);
+        w[m] = (w[m] & keep) ^ fold;
+      }
+    }
+  }
+}
+
+template <bool S72>
+__device__ __forceinline__ uint32_t window_raw(const uint32_t (&w)[kWords], const uint32_t (*T)[256]) {
+  uint32_t c = 0;
+  if constexpr (S72) {
+#pragma unroll
+    for (int m = 0; m < kWords; ++m) {
+      const uint32_t x = w[m];
+      const int d = kCrcWin - 1 - 4 * m;
+      c ^= T[d][x & 0xFFu] ^ T[d - 1][(x >> 8) & 0xFFu] ^ T[d - 2][(x >> 16) & 0xFFu] ^ T[d - 3][x >> 24];
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < kWords; m += 2) {
+      const uint32_t x = c ^ w[m], y = w[m + 1];
+      c = T[7][x & 0xFFu] ^ T[6][(x >> 8) & 0xFFu] ^ T[5][(x >> 16) & 0xFFu] ^ T[4][x >> 24] ^
+          T[3][y & 0xFFu] ^ T[2][(y >> 8) & 0xFFu] ^ T[1][(y >> 16) & 0xFFu] ^ T[0][y >> 24];
+    }
+  }
+  return c;
+}
+
+template <bool S72>
+struct CrcLds {
+  uint32_t t[S72 ? kCrcWin : 8][256];
+  MulLds m;
+};
+
+template <bool S72>
+__global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks_pf(const uint8_t* data, uint64_t data_len,
+                                                                  const uint64_t* blk_off, const uint32_t* blk_len,
+                                                                  uint32_t nblk, uint32_t* crc_out, uint8_t* bad,
+                                                                  int framed) {
+  __shared__ CrcLds<S72> S;
+  {
+    const uint4* src = S72 ? reinterpret_cast<const uint4*>(&kS72) : reinterpret_cast<const uint4*>(&kTab.slice[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&S.t[0][0]);
+    const int n16 = S72 ? (int)(sizeof(Slice72Lds) / 16) : 4 * 256 / 4;
+    for (int i = threadIdx.x; i < n16; i += kCrcThreads) dst[i] = src[i];
+    const uint4* ms = reinterpret_cast<const uint4*>(&kMul);
+    uint4* md = reinterpret_cast<uint4*>(&S.m);
+    for (int i = threadIdx.x; i < (int)(sizeof(MulLds) / 16); i += kCrcThreads) md[i] = ms[i];
+  }
+  if constexpr (!S72) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * 256; i += kCrcThreads) {   // tables 4..7 from table 3
+      uint32_t t = S.t[3][i & 255];
+      for (int k = 0; k <= (i >> 8); ++k) t = (t >> 8) ^ S.t[0][t & 0xFFu];
+      S.t[4 + (i >> 8)][i & 255] = t;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves = gridDim.x * (kCrcThreads / kWave);
+  uint32_t b = blockIdx.x * (kCrcThreads / kWave) + (threadIdx.x >> 6);
+  // the first window (k = lane) of block b, loaded one block ahead
+  uint32_t w[kWords];
+  auto issue = [&](uint32_t bb) {
+    if (bb >= nblk) return;
+    const uint64_t off = blk_off[bb], L = blk_len[bb];
+    if (off + L > data_len || L < (uint64_t)kCrcWin || (uint64_t)lane * kCrcWin >= L) return;
+    const int64_t hi = (int64_t)(L - (uint64_t)lane * kCrcWin);
+    window_words(data + off, hi, (int64_t)off + hi - kCrcWin >= 0, w);
+  };
+  issue(b);
+  for (; b < nblk; b += waves) {
+    const uint64_t off = blk_off[b];
+    const uint64_t L = blk_len[b];
+    const uint8_t* d = data + off;
+    const bool oob = off + L > data_len;   // the reference's slice panics before the checksum
+    uint32_t cw[kWords];
+#pragma unroll
+    for (int m = 0; m < kWords; ++m) cw[m] = w[m];
+    issue(b + waves);
+    uint32_t acc = 0;
+    if (!oob && L >= (uint64_t)kCrcWin) {
+      if ((uint64_t)lane * kCrcWin < L) {
+        const int64_t hi = (int64_t)(L - (uint64_t)lane * kCrcWin);
+        window_fold(hi - kCrcWin, cw);
+        acc = mul_nib(window_raw<S72>(cw, S.t), S.m.a[lane]);
+      }
+      for (uint64_t k = lane + kWave; k * kCrcWin < L; k += kWave) {   // blocks > 4.5 KiB
+        const int64_t hi = (int64_t)(L - k * kCrcWin);
+        uint32_t xw[kWords];
+        window_words(d, hi, (int64_t)off + hi - kCrcWin >= 0, xw);
+        window_fold(hi - kCrcWin, xw);
+        const uint32_t c = window_raw<S72>(xw, S.t);
+        if (k < 1024) acc ^= mul_nib(mul_nib(c, S.m.a[k & 63]), S.m.b[k >> 6]);
+        else acc ^= dmultmodp(xpow8(k * kCrcWin), c);
+      }
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, sh, kWave);
+      acc ^= 0xFFFFFFFFu;
+    } else if (!oob) {
+      acc = wave_crc32c(d, L, S.t[0], lane);   // < kCrcWin bytes
+    }
+    if (lane == 0) {
+      if (crc_out) crc_out[b] = acc;
+      if (bad && oob) {
+        bad[b] = 1;
+      } else if (bad) {
+        uint32_t stored = 0;
+        if (framed && off >= 4)
+          stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
+        bad[b] = (framed && off >= 4) ? (uint8_t)(stored != acc) : (uint8_t)0;
+      }
+    }
+  }
+}
+
 }  // namespace mtblx_crc
+
+// MTBLX_CRC_KERNEL (A/B knob, read once): 0 = the round-2 kernel, 1 = prefetch + slicing-by-8,
+// 2 = prefetch + slicing-by-72 (default)
+static int crc_kernel_choice() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MTBLX_CRC_KERNEL");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
+}
 
 extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed,
                                    void* stream) {
@@ -165,8 +351,17 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     grid = (ncu > 0 ? ncu : 256) * 2;   // 32 waves per CU
   }
   const uint32_t need = (in->nblk + 15u) / 16u;
-  hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, dim3(need < (uint32_t)grid ? need : (uint32_t)grid),
-                     dim3(mtblx_crc::kCrcThreads), 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
-                     in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
+  const int kc = crc_kernel_choice();
+  const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (kc == 2)
+    hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks_pf<true>, g, t, 0, s, in->data, in->data_len, in->blk_off,
+                       in->blk_len, in->nblk, crc, bad, framed);
+  else if (kc == 1)
+    hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks_pf<false>, g, t, 0, s, in->data, in->data_len, in->blk_off,
+                       in->blk_len, in->nblk, crc, bad, framed);
+  else
+    hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, g, t, 0, s, in->data, in->data_len, in->blk_off, in->blk_len,
+                       in->nblk, crc, bad, framed);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

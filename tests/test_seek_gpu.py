@@ -295,6 +295,16 @@ def _corrupt_index(data, rng, kind):
     return bytes(d)
 
 
+def _dump_failure(data, *what):
+    """keep a failing corrupted file for offline analysis (gpurun_out/ travels back)"""
+    import os
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "failures")
+    os.makedirs(d, exist_ok=True)
+    n = len(os.listdir(d))
+    open(os.path.join(d, f"f{n}.mtbl"), "wb").write(data)
+    open(os.path.join(d, f"f{n}.txt"), "w").write(repr(what))
+
+
 @pytest.mark.parametrize("kind", ["restart", "shared", "bytes"])
 def test_stateful_live_index_iterator(oracle, kind):
     """ReaderIntoIter::seek re-seeks the LIVE index iterator (src/reader.rs:303): on a corrupt
@@ -332,7 +342,9 @@ def test_stateful_live_index_iterator(oracle, kind):
                 exp = oracle.file_scan(bad, mode, k1, k2, verify=False)
                 sc = {"from": lambda: r.iter_from(k1), "prefix": lambda: r.iter_prefix(k1),
                       "range": lambda: r.iter_range(k1, k2)}[mode]()
-                assert sc.end == exp["end"], (kind, mode, k1, k2)
+                if sc.end != exp["end"] or sc.records() != exp["records"]:
+                    _dump_failure(bad, kind, mode, k1, k2)
+                assert sc.end == exp["end"], (kind, mode, k1, k2, sc.nrec, len(exp["records"]), r.index_regular())
                 assert sc.records() == exp["records"], (kind, mode, k1, k2)
     if kind != "bytes":
         assert seen_irregular > 0

@@ -139,7 +139,7 @@ def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
     res["pcie_ceiling"] = pcie_ceiling()
     pc = res["pcie_ceiling"]
     out = pipe.HostOutputs(off.size, nrec, kbytes, vbytes)
-    p = pipe.HostPipe(chunk_bytes=64 << 20, max_blocks=1 << 16, threads=16)
+    p = pipe.HostPipe(chunk_bytes=64 << 20, max_blocks=1 << 16, threads=16, device_snappy=False)
 
     def run(d, o, l, comp, tag, extra=None, pp=None):
         pp = pp or p

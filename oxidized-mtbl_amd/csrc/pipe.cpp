@@ -38,6 +38,9 @@
 #include "mtblx.h"
 #include "mtblx_host.h"
 
+// MTBLX_PIPE_DEVICE_SNAPPY auto: device decompression when uncompressed / stored <= this
+static constexpr uint64_t kAutoDeviceMaxRatio = 2;
+
 namespace {
 
 constexpr int kSlots = 3;
@@ -167,7 +170,7 @@ struct mtblx_pipe {
   uint64_t chunk_bytes = 64ull << 20;
   uint32_t max_blocks = 1u << 16;
   int dev = 0;
-  bool dev_snappy = false;   // MTBLX_PIPE_DEVICE_SNAPPY
+  int dev_snappy = 2;   // MTBLX_PIPE_DEVICE_SNAPPY: 0 host, 1 device, 2 auto (device for poorly compressed files)
   hipStream_t s_h2d = nullptr, s_dec = nullptr, s_d2h = nullptr;
   Slot slot[kSlots];
   void* ws = nullptr;
@@ -350,7 +353,17 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
       ulen[b] = u;
     }
   }
-  const bool dz_mode = compression == 1 && p->dev_snappy;   // stored bytes H2D, device decompression
+  // stored bytes H2D + device decompression (mtblx_snappy_decompress_dev) or host decompression.
+  // auto: the device only where it wins -- a PCIe-bound pipe on poorly compressed blocks (the
+  // stored bytes cross PCIe once, the host stage vanishes); on compressible streams the device
+  // decompressor (~170 GB/s of output) loses to 16 host threads (~110 GB/s of
+  // input), so they stay on the host.
+  bool dz_mode = compression == 1 && p->dev_snappy == 1;
+  if (compression == 1 && p->dev_snappy == 2) {
+    uint64_t su = 0, ss = 0;
+    for (uint32_t b = 0; b < nblk; ++b) { su += ulen[b]; ss += blk_len[b]; }
+    dz_mode = ss > 0 && su <= kAutoDeviceMaxRatio * ss;
+  }
   const bool ranged = compression == 0 || dz_mode;
   std::vector<Chunk> chunks;
   Caps need;
@@ -591,7 +604,8 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
 extern "C" int mtblx_pipe_set(mtblx_pipe* p, int option, int64_t value) {
   if (!p) return MTBLX_E_INVAL;
   if (option == MTBLX_PIPE_DEVICE_SNAPPY) {
-    p->dev_snappy = value != 0;
+    if (value < 0 || value > 2) return MTBLX_E_INVAL;
+    p->dev_snappy = (int)value;
     return MTBLX_OK;
   }
   return MTBLX_E_INVAL;

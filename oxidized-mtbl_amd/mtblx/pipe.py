@@ -75,13 +75,15 @@ class HostPipe:
     """mtblx_pipe: chunked host -> device -> host decode with three chunks in flight."""
 
     def __init__(self, chunk_bytes: int = 64 << 20, max_blocks: int = 1 << 16, threads: int = 16,
-                 device_snappy: bool = False):
+                 device_snappy="auto"):
         codec._require_device()
         self._p = _lib.lib().mtblx_pipe_new(int(chunk_bytes), int(max_blocks), int(threads))
         if not self._p:
             raise RuntimeError("mtblx_pipe_new failed")
         # MTBLX_PIPE_DEVICE_SNAPPY: snappy blocks cross PCIe compressed, decompressed on the device
-        if _lib.lib().mtblx_pipe_set(self._p, 1, 1 if device_snappy else 0) != 0:
+        # (True), on the host (False), or "auto": the device only for poorly compressed batches
+        mode = 2 if device_snappy == "auto" else (1 if device_snappy else 0)
+        if _lib.lib().mtblx_pipe_set(self._p, 1, mode) != 0:
             raise RuntimeError("mtblx_pipe_set failed")
         self.stats = PipeStats()
 

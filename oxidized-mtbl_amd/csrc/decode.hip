@@ -538,6 +538,8 @@ __device__ __forceinline__ void tile_range(const TileArgs& a, uint32_t t, uint32
   r0 = ((base + s) & ~15ull) - base;   // may be "negative" (wraps) if data is unaligned: clamp
   if (base + s < 16 || ((base + s) & ~15ull) < base) r0 = 0;
   r1 = (e > s && e - r0 + 48 <= tb) ? e : 0;
+  for (uint32_t j = 1; r1 && j + 1 < nb; ++j)   // every block inside [s, e) (see pipe_dma)
+    if (a.blk_off[b0 + j] < s || a.blk_off[b0 + j] + a.blk_len[b0 + j] > e) r1 = 0;
 }
 
 // prefetch chunk c (16 B) of a contiguous range into v (zero-filled outside the buffer)
@@ -1421,7 +1423,11 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end_l, (int)nb - 1);
   uint64_t r0 = ((base + s) & ~15ull) - base;
   if (base + s < 16 || ((base + s) & ~15ull) < base) r0 = 0;
-  const bool contig = e > s && e - r0 + 48 <= (uint64_t)P::TB;
+  // one contiguous range only if EVERY block of the tile lies inside [first start, last end):
+  // the directory is the caller's (a corrupt index can point a block anywhere, before its
+  // predecessor or into it); lanes >= nb repeat the last block
+  const bool inside = off_l >= s && end_l <= e;
+  const bool contig = e > s && e - r0 + 48 <= (uint64_t)P::TB && __ballot(!inside) == 0ull;
   if (contig) {
     // range byte x at stage offset 16 + x; wave-instruction m writes chunks [64m, 64m + 64)
     const uint32_t nch = (uint32_t)((e - r0 + 15) >> 4);
@@ -1992,8 +1998,16 @@ __device__ __forceinline__ uint32_t crc_word4(const PipeLds<P>& S, uint32_t c, u
   return S.crcT[3][c & 0xffu] ^ S.crcT[2][(c >> 8) & 0xffu] ^ S.crcT[1][(c >> 16) & 0xffu] ^ S.crcT[0][c >> 24];
 }
 
+// Always inlined: under register pressure the compiler outlined one call site (PipeLargeV's
+// look-back wave) and the out-of-line call is what faulted ("the spill fault");
+// MTBLX_CRC_NOINLINE (diagnostic builds only) forces the call.
+#ifdef MTBLX_CRC_NOINLINE
+#define MTBLX_PIPE_CRC_INLINE __attribute__((noinline))
+#else
+#define MTBLX_PIPE_CRC_INLINE __forceinline__
+#endif
 template <class P>
-__device__ void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, int cw, int lane, uint32_t par) {
+__device__ MTBLX_PIPE_CRC_INLINE void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, int cw, int lane, uint32_t par) {
   const uint32_t nb = B.nb, b0 = B.b0;
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(B.stage);
   const uint32_t gl = (uint32_t)cw * kWave + (uint32_t)lane;

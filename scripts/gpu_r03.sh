@@ -30,4 +30,7 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = spill ]; then
   step spill 700 python -u -m pytest tests/test_spill_gpu.py -v --timeout 650 --timeout-method thread
 fi
+if [ "$MODE" = noinline ]; then   # diagnostic, may fault: always the last step of a call
+  step noinline 300 env MTBLX_LIB=oxidized-mtbl_amd/build/libmtblx_crcnoinline.so python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider tests/test_decode_gpu.py::test_fused_verify_decode
+fi
 echo ALL DONE

@@ -390,3 +390,36 @@ def test_pipelarge_tile_counts_one_workspace(oracle):
         codec.decode_into(batch, out, ws)
         torch.cuda.synchronize()
         assert_same(out.to_host(), oracle.decode_blocks(d, o[:n], l[:n]), n)
+
+
+@pytest.mark.parametrize("block_size", [4096, 65536])
+def test_directory_in_any_order(oracle, block_size):
+    """The directory is the caller's: windows out of file order, repeated, overlapping, or
+    pointing into another block (a corrupt index does all of these, src/reader.rs:177-186).
+    A tile whose blocks do not all lie in [first start, last end) must not be staged as one
+    contiguous range (it was: a block before its tile's first one was read at a wrapped stage
+    offset).  PipeSmall (4 KiB) and PipeLarge (64 KiB) batches, plain and fused-verify."""
+    codec = _dev()
+    import torch
+    from mtblx import synth
+    rng = np.random.default_rng(block_size)
+    data, off, ln = synth.cfg2_file(400 if block_size == 4096 else 60, block_size=block_size)
+    n = off.size
+    o2, l2 = off.astype(np.uint64).copy(), ln.astype(np.uint32).copy()
+    perm = rng.permutation(n)
+    o2, l2 = o2[perm], l2[perm]                              # out of file order
+    for _ in range(n // 8):                                  # windows inside other blocks
+        i, j = int(rng.integers(0, n)), int(rng.integers(0, n))
+        sh = int(rng.integers(1, max(2, int(l2[j]) // 2)))
+        o2[i] = o2[j] + sh
+        l2[i] = int(rng.integers(0, max(1, int(l2[j]) - sh)))
+    o2 = np.concatenate([o2, o2[:5], np.sort(o2)[:7]])       # repeated entries
+    l2 = np.concatenate([l2, l2[:5], l2[np.argsort(o2[:n])][:7]])
+    orc = oracle.decode_blocks(data, o2, l2)
+    assert_same(device_decode(data, o2, l2), orc, o2.size)
+    batch = codec.DeviceBatch.from_host(data, o2, l2)
+    out, crc, bad = codec.decode_verify(batch, framed=False, fused=True)
+    torch.cuda.synchronize()
+    assert_same(out.to_host(), orc, o2.size)
+    exp = np.array([oracle.crc32c(bytes(data[int(a): int(a) + int(b)])) for a, b in zip(o2, l2)], np.uint32)
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), exp)

@@ -30,6 +30,7 @@ def test_spilling_build_is_exact():
            os.path.join(ROOT, "tests", "test_decode_gpu.py") + "::test_mutated_blocks",
            os.path.join(ROOT, "tests", "test_decode_gpu.py") + "::test_64k_blocks_long_keys",
            os.path.join(ROOT, "tests", "test_decode_gpu.py") + "::test_key_tails_dense_and_planes",
+           os.path.join(ROOT, "tests", "test_decode_gpu.py") + "::test_directory_in_any_order",
            os.path.join(ROOT, "tests", "test_cfg4_gpu.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -631,10 +631,16 @@ def run_cfg4(args, dist, world, rank):
         h = P["out"].totals_host()
         if h != (P["nr"], 16 * P["nr"], 64 * P["nr"], 0) or not bool((P["out"].status[: P["nb"]] == 0).all().item()):
             raise RuntimeError(f"cfg4 piece {P['bs']}: decode mismatch {h}")
+    # per leg: its own preload first.  The host checks above leave the GPU idle for ~40 ms, and
+    # the first ~30 back-to-back launches after an idle period run up to 35 % slow while the
+    # clocks settle (profiles/r03/a: cfg2 at this leg's size goes 1.25 -> 1.65 -> 1.20 ms); timing
+    # 10 launches straight after the checks measured that transient, not the leg
     per_leg_ms = {}
     with torch.cuda.stream(s):
         for P in pieces:
-            per_leg_ms[P["bs"]] = _timed(lambda: codec.decode_into(P["batch"], P["out"], P["ws"], s), s, 10)
+            leg = lambda P=P: codec.decode_into(P["batch"], P["out"], P["ws"], s)  # noqa: E731
+            _preload(leg, s, args.preload_ms)
+            per_leg_ms[P["bs"]] = _timed(leg, s, 20)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()

@@ -2006,13 +2006,21 @@ __device__ __forceinline__ uint32_t crc_word4(const PipeLds<P>& S, uint32_t c, u
 #else
 #define MTBLX_PIPE_CRC_INLINE __forceinline__
 #endif
+// MTBLX_ABL_CRC (diagnostic ablation builds only; results are wrong by construction):
+// bit 0 skips the chunk loop, bit 1 the stored-checksum reads of the finalisation, bit 2 the
+// whole pipe_crc
+#ifndef MTBLX_ABL_CRC
+#define MTBLX_ABL_CRC 0
+#endif
 template <class P>
 __device__ MTBLX_PIPE_CRC_INLINE void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, int cw, int lane, uint32_t par) {
+  if constexpr ((MTBLX_ABL_CRC & 4) != 0) return;
   const uint32_t nb = B.nb, b0 = B.b0;
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(B.stage);
   const uint32_t gl = (uint32_t)cw * kWave + (uint32_t)lane;
   // chunks of staged blocks of >= 4 bytes, numbered across the tile
   uint32_t total = 0;
+  if constexpr ((MTBLX_ABL_CRC & 1) == 0)
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t L = B.blen[j];
     total += (B.boff[j] < kOutOfBounds && L >= 4u) ? (L + 63u) / 64u : 0u;
@@ -2105,7 +2113,7 @@ __device__ MTBLX_PIPE_CRC_INLINE void pipe_crc(const PipeBuf<P>& B, const TileAr
       const uint64_t off = a.blk_off[b];
       if (o == kOutOfBounds) {
         bad = 1;   // the reference's slice of the block panics before its checksum
-      } else if (a.crc_framed && off >= 4) {
+      } else if (a.crc_framed && off >= 4 && (MTBLX_ABL_CRC & 2) == 0) {
         const uint8_t* d = a.data + off;
         const uint32_t stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
         bad = stored != crc;

@@ -109,6 +109,21 @@ struct DevBuf {
   void reset() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
+// one query of mtblx_block_seek_batch, or -- kbuf allocated: the iterator's key past 64 KiB --
+// of mtblx_block_seek_batch_kbuf with the key in kbuf
+inline int block_seek_call(const uint8_t* base, const DevBuf& key, const DevBuf& kend, const DevBuf& q, const DevBuf& k,
+                           uint64_t keys_cap, const DevBuf& v, uint64_t vals_cap, const DevBuf& ke, const DevBuf& ve,
+                           const DevBuf& kc, uint64_t rec_cap, const DevBuf& kbuf) {
+  const auto* kk = static_cast<const uint8_t*>(key.p);
+  const auto* kn = static_cast<const uint64_t*>(kend.p);
+  auto* qq = static_cast<mtblx_block_seek*>(q.p);
+  if (kbuf.p)
+    return mtblx_block_seek_batch_kbuf(base, kk, kn, 1, qq, k.as<uint8_t>(), keys_cap, v.as<uint8_t>(), vals_cap,
+                                       ke.as<uint64_t>(), ve.as<uint64_t>(), kc.as<uint64_t>(), rec_cap,
+                                       kbuf.as<uint8_t>(), kbuf.n, nullptr);
+  return mtblx_block_seek_batch(base, kk, kn, 1, qq, k.as<uint8_t>(), keys_cap, v.as<uint8_t>(), vals_cap,
+                                ke.as<uint64_t>(), ve.as<uint64_t>(), kc.as<uint64_t>(), rec_cap, nullptr);
+}
 template <class T>
 inline DevBuf upload(const T* src, size_t count) {
   DevBuf b(count * sizeof(T));
@@ -187,7 +202,9 @@ class Writer {
  public:
   Writer(uint64_t block_size, uint64_t restart_interval, CompressionType c, uint32_t level = 0)
       : w_(mtblx_writer_new(block_size, restart_interval, static_cast<uint32_t>(c))) {
-    if (!w_) throw std::invalid_argument("CompressionType: None, Snappy, Zlib, Zstd only (Lz4: the crate's Err)");
+    // Lz4 / Lz4hc build a writer whose data-block flushes return Err (Error(Io) below), as the
+    // crate's do; NULL = an unknown type, or Zstd without libzstd.so.1 on this host
+    if (!w_) throw std::invalid_argument("CompressionType: unknown, or Zstd without libzstd.so.1");
     mtblx_writer_set_level(w_, level);
   }
   Writer(const Writer&) = delete;
@@ -196,9 +213,11 @@ class Writer {
   ~Writer() { if (w_) mtblx_writer_free(w_); }
   static Writer memory();   // WriterBuilder::default().memory()
 
-  // src/writer.rs:112-149; "out-of-order key" panics
+  // src/writer.rs:112-149: "out-of-order key" panics; a flush whose compressor returns Err is
+  // Err(Io) (the record is not inserted), and the insert after it panics on the data block's
+  // `assert!(!self.finished)` (src/block_builder.rs:51)
   void insert(const uint8_t* key, size_t klen, const uint8_t* val, size_t vlen) {
-    if (mtblx_writer_insert(w_, key, klen, val, vlen) != MTBLX_OK) throw Panic("out-of-order key");
+    check(mtblx_writer_insert(w_, key, klen, val, vlen));
   }
   void insert(const Bytes& k, const Bytes& v) { insert(k.data(), k.size(), v.data(), v.size()); }
   void insert(const std::string& k, const std::string& v) {
@@ -208,13 +227,19 @@ class Writer {
   Bytes into_inner() {
     uint8_t* p = nullptr;
     uint64_t n = 0;
-    detail::abi_check(mtblx_writer_finish(w_, &p, &n), "mtblx_writer_finish");
+    check(mtblx_writer_finish(w_, &p, &n));
     Bytes out(p, p + n);
     mtblx_free(p);
     return out;
   }
 
  private:
+  static void check(int rc) {
+    if (rc == MTBLX_OK) return;
+    if (rc == MTBLX_E_IO) throw Error(MtblError::Io);
+    if (rc == MTBLX_E_FORMAT) throw Panic("out-of-order key");
+    throw Panic("BlockBuilder::add: assertion failed (or the writer already panicked)");
+  }
   mtblx_writer* w_;
 };
 
@@ -403,6 +428,7 @@ class Reader {
   std::vector<ReaderIntoIter::Loaded> load_range(size_t i0, size_t i1) const;
   std::vector<ReaderIntoIter::Loaded> load_framed(const Framing& f) const;
   void load_big(uint64_t block_off, ReaderIntoIter::Loaded& L) const;
+  void load_content(const ReaderIntoIter::Content& c, ReaderIntoIter::Loaded& L) const;
   Bytes file_;
   detail::DevBuf dfile_;
   bool verify_;
@@ -553,9 +579,10 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_framed(const Framing& f)
   std::shared_ptr<DevBuf> ubuf;
   std::vector<uint64_t> uoff(n, 0);
   std::vector<uint32_t> ul(n, 0);
+  std::vector<uint64_t> ulen(n, 0);
   Decoded dec;
   if (meta_.compression_algorithm != 0) {
-    std::vector<uint64_t> so(n, 0), ulen(n, 0);
+    std::vector<uint64_t> so(n, 0);
     std::vector<uint32_t> sn(n, 0);
     std::vector<int32_t> zst(n, 0);
     for (uint32_t i = 0; i < n; ++i)
@@ -568,12 +595,13 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_framed(const Framing& f)
     uint64_t tot = 0;
     for (uint32_t i = 0; i < n; ++i) {
       zerr[i] = sn[i] && zst[i] != MTBLX_CODEC_OK;
-      if (ulen[i] > 0xFFFFFFFFull) { mtblx_free(hb); throw std::runtime_error("decompressed block >= 4 GiB"); }
-      ul[i] = zerr[i] ? 0u : (uint32_t)ulen[i];
+      // a content >= 4 GiB stays out of the batch (u32 lengths): the emitting seek decodes it below
+      ul[i] = zerr[i] || ulen[i] > 0xFFFFFFFFull ? 0u : (uint32_t)ulen[i];
       umx = std::max(umx, ul[i]);
       tot = std::max(tot, uoff[i] + ulen[i]);
     }
-    ubuf = std::make_shared<DevBuf>(upload(hb, tot + 1));
+    ubuf = std::make_shared<DevBuf>(tot + 1);
+    if (tot) hip_check(hipMemcpy(ubuf->p, hb, tot, hipMemcpyHostToDevice), "H2D");
     mtblx_free(hb);
     DevBuf d_uo = upload(uoff.data(), n), d_ul = upload(ul.data(), n);
     dec = decode_batch(ubuf->as<uint8_t>(), tot + 1, d_uo.as<uint64_t>(), d_ul.as<uint32_t>(), n, umx);
@@ -588,6 +616,10 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_framed(const Framing& f)
     }
     if (f.st[i] != MTBLX_DIR_OK || bad[i]) { L.code = 1; continue; }
     if (zerr[i]) { L.code = 2; continue; }
+    if (ubuf && ulen[i] > 0xFFFFFFFFull) {   // decompressed content >= 4 GiB (u64 restart array)
+      load_content(ReaderIntoIter::Content{ubuf, ubuf->as<uint8_t>(), uoff[i], ulen[i]}, L);
+      continue;
+    }
     const int32_t s = dec.status[i];
     if (s == MTBLX_ST_INVALID_BLOCK) { L.code = 3; continue; }
     if (s == MTBLX_ST_UNSUPPORTED) { L.code = 4; continue; }
@@ -612,15 +644,35 @@ inline std::vector<ReaderIntoIter::Loaded> Reader::load_framed(const Framing& f)
 // Reader::block + Block::init + the scan of a block >= 4 GiB: framing and checksum on the host
 // (mtblx_frame_block), the scan on the device (the emitting block seek, seek_to_first)
 inline void Reader::load_big(uint64_t boff, ReaderIntoIter::Loaded& L) const {
-  if (meta_.compression_algorithm != 0) throw std::runtime_error("compressed block >= 4 GiB");
+  using namespace detail;
   uint64_t coff = 0, clen = 0;
   int panic = 0;
   if (mtblx_frame_block(file_.data(), file_.size(), version_, boff, verify_ ? 1 : 0, &coff, &clen, &panic) != MTBLX_OK) {
     L.code = 1;
     return;
   }
+  if (meta_.compression_algorithm == 0) {
+    load_content(ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), coff, clen}, L);
+    return;
+  }
+  uint8_t* hb = nullptr;   // src/reader.rs:166-170 on the host, any size
+  uint64_t un = 0;
+  if (mtblx_decompress(static_cast<uint32_t>(meta_.compression_algorithm), file_.data() + coff, clen, &hb, &un) !=
+      MTBLX_CODEC_OK) {
+    if (hb) mtblx_free(hb);
+    L.code = 2;
+    return;
+  }
+  auto buf = std::make_shared<DevBuf>(un + 1);
+  if (un) hip_check(hipMemcpy(buf->p, hb, un, hipMemcpyHostToDevice), "H2D");
+  mtblx_free(hb);
+  load_content(ReaderIntoIter::Content{buf, buf->as<uint8_t>(), 0, un}, L);
+}
+
+// Block::init + seek_to_first + the records of one content (any size) on the device
+inline void Reader::load_content(const ReaderIntoIter::Content& c, ReaderIntoIter::Loaded& L) const {
   try {
-    L.bi = ReaderIntoIter::seek_block(ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), coff, clen}, nullptr, 0);
+    L.bi = ReaderIntoIter::seek_block(c, nullptr, 0);
   } catch (const Error&) {
     L.code = 3;
   } catch (const Panic&) {
@@ -709,7 +761,7 @@ inline ReaderIntoIter::Content Reader::seek_content(const mtblx_index_seek& s) c
   if (s.block_status == MTBLX_SEEK_PANIC) throw Panic("Reader::block");
   if (meta_.compression_algorithm == 0) {
     if (s.block_status == MTBLX_SEEK_ERR) throw Error(MtblError::InvalidBlock);
-    if (s.block_status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("block >= 4 GiB");
+    if (s.block_status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("index seek: unexpected block status");
     return ReaderIntoIter::Content{nullptr, dfile_.as<uint8_t>(), s.data_off, s.data_len};
   }
   // compressed: decompress on the host, Block::init runs on the result (mtblx_block_seek_batch)
@@ -740,16 +792,19 @@ inline ReaderIntoIter::EmitResult ReaderIntoIter::emit(const Content& c, const B
   const Bytes none;
   const uint64_t kend = key ? key->size() : 0;
   DevBuf d_key = upload_key(key ? *key : none), d_kend = upload(&kend, 1);
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  DevBuf kbuf;   // allocated once a key runs past the 64 KiB LDS key
+  for (int attempt = 0; attempt < 4; ++attempt) {
     DevBuf d_q = upload(&q, 1), d_k(keys_cap + 1), d_v(vals_cap + 1), d_ke(8 * rec_cap + 8), d_ve(8 * rec_cap + 8),
         d_kc(8 * rec_cap + 8);
-    abi_check(mtblx_block_seek_batch(c.base, d_key.as<uint8_t>(), d_kend.as<uint64_t>(), 1, d_q.as<mtblx_block_seek>(),
-                                     d_k.as<uint8_t>(), keys_cap, d_v.as<uint8_t>(), vals_cap, d_ke.as<uint64_t>(),
-                                     d_ve.as<uint64_t>(), d_kc.as<uint64_t>(), rec_cap, nullptr),
+    abi_check(block_seek_call(c.base, d_key, d_kend, d_q, d_k, keys_cap, d_v, vals_cap, d_ke, d_ve, d_kc, rec_cap, kbuf),
               "mtblx_block_seek_batch");
     hip_check(hipDeviceSynchronize(), "sync");
     EmitResult r;
     r.res = download<mtblx_block_seek>(d_q.p, 1)[0];
+    if (r.res.status == MTBLX_SEEK_UNSUPPORTED && !kbuf.p) {   // any key this iterator can build fits
+      kbuf = DevBuf(kend + c.len + 64);
+      continue;
+    }
     if (r.res.end == MTBLX_EMIT_OVERFLOW) {
       rec_cap = r.res.nrec;
       keys_cap = r.res.key_bytes;
@@ -777,7 +832,7 @@ inline ReaderIntoIter::Bi ReaderIntoIter::seek_block(const Content& c, const Byt
   if (r.res.status == MTBLX_SEEK_ERR) throw Error(MtblError::InvalidBlock);
   if (r.res.status == MTBLX_SEEK_PANIC) throw Panic("BlockIter::seek");
   if (r.res.status == MTBLX_SEEK_LOOP) throw Panic("BlockIter::seek never returns");
-  if (r.res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: block >= 4 GiB or key > 64 KiB");
+  if (r.res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: key buffer too small");
   return std::move(r.b);
 }
 
@@ -795,12 +850,16 @@ inline uint64_t ReaderIntoIter::kcap_now(Bi& b) {
     const uint8_t z = 0;
     DevBuf d_key = upload(&z, 1), d_kend = upload(&kend, 1), d_q = upload(&q, 1);
     DevBuf d_k(2 * b.c.len + 65), d_v(b.c.len + 17), d_ke(8 * b.n() + 8), d_ve(8 * b.n() + 8), d_kc(8 * b.n() + 8);
-    abi_check(mtblx_block_seek_batch(b.c.base, d_key.as<uint8_t>(), d_kend.as<uint64_t>(), 1,
-                                     d_q.as<mtblx_block_seek>(), d_k.as<uint8_t>(), 2 * b.c.len + 64,
-                                     d_v.as<uint8_t>(), b.c.len + 16, d_ke.as<uint64_t>(), d_ve.as<uint64_t>(),
-                                     d_kc.as<uint64_t>(), b.n(), nullptr),
-              "mtblx_block_seek_batch");
-    hip_check(hipDeviceSynchronize(), "sync");
+    DevBuf kbuf;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      abi_check(block_seek_call(b.c.base, d_key, d_kend, d_q, d_k, 2 * b.c.len + 64, d_v, b.c.len + 16, d_ke, d_ve, d_kc,
+                                b.n(), kbuf),
+                "mtblx_block_seek_batch");
+      hip_check(hipDeviceSynchronize(), "sync");
+      if (download<mtblx_block_seek>(d_q.p, 1)[0].status != MTBLX_SEEK_UNSUPPORTED || kbuf.p) break;
+      kbuf = DevBuf(b.c.len + 64);   // a key past 64 KiB: again with the key in device memory
+      hip_check(hipMemcpy(d_q.p, &q, sizeof(q), hipMemcpyHostToDevice), "H2D");
+    }
     b.kcaps = download<uint64_t>(d_kc.p, b.n());
     b.kcaps_known = true;
   }
@@ -827,7 +886,7 @@ inline ReaderIntoIter::Bi ReaderIntoIter::load(size_t i) {
 inline ReaderIntoIter::IxList ReaderIntoIter::ix_list(EmitResult&& e, int64_t ord0) const {
   if (e.res.status == MTBLX_SEEK_PANIC) throw Panic("index seek");
   if (e.res.status == MTBLX_SEEK_LOOP) throw Panic("index seek never returns");
-  if (e.res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: index key > 64 KiB");
+  if (e.res.status == MTBLX_SEEK_UNSUPPORTED) throw std::runtime_error("emitting seek: key buffer too small");
   IxList l;
   l.b = std::move(e.b);
   l.stop_off = e.res.stop_off;

@@ -43,6 +43,9 @@ extern "C" {
 #define MTBLX_E_FORMAT (-4)   /* host-side file/format error (reader API)               */
 #define MTBLX_E_TIMEOUT (-5)  /* a decode launch reported a look-back timeout (totals[3] bit 1) twice:
                                  its outputs were discarded (synchronous entry points only)  */
+#define MTBLX_E_IO (-6)       /* the writer's compressor returned Err (Writer::insert / into_inner's
+                                 io::Error: Lz4 / Lz4hc "unsupported", src/compression.rs:70-81;
+                                 a codec failure); nothing was written, the writer is unchanged */
 
 /* ---- per-block status (status[b]) ----
  * Exact correspondence with the reference's behaviour on the same bytes:         */
@@ -198,8 +201,9 @@ int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int veri
 #define MTBLX_SEEK_ERR 1          /* Err(InvalidBlock) from Block::init                       */
 #define MTBLX_SEEK_PANIC 2        /* the reference panics                                     */
 #define MTBLX_SEEK_LOOP 3         /* the reference never returns (zero-progress entry)        */
-#define MTBLX_SEEK_UNSUPPORTED 4  /* a key > 64 KiB in the emitting seek (blocks >= 4 GiB with u64
-                                     restart arrays are handled: src/block.rs:25-42, :95-104)   */
+#define MTBLX_SEEK_UNSUPPORTED 4  /* a key > 64 KiB in mtblx_block_seek_batch's LDS key (retry with
+                                     mtblx_block_seek_batch_kbuf); blocks >= 4 GiB with u64
+                                     restart arrays are handled: src/block.rs:25-42, :95-104    */
 typedef struct mtblx_index_seek {
   int32_t status;          /* of the index seek: OK / PANIC / LOOP                               */
   int32_t valid;           /* index_iter.get() is Some after the seek                             */
@@ -256,6 +260,15 @@ int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, const uint6
                            mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
                            uint64_t vals_cap, uint64_t* key_end_out, uint64_t* val_end_out, uint64_t* kcap_out,
                            uint64_t rec_cap, void* stream);
+/* (2') the same with the iterator's key kept in a caller buffer, key_buf + q * key_buf_cap
+ *      (device), instead of 64 KiB of LDS: keys of any length.  mtblx_block_seek_batch reports a
+ *      key past 64 KiB as status MTBLX_SEEK_UNSUPPORTED; here that means past key_buf_cap.  A
+ *      key never exceeds len(keys[q]) + data_len bytes (every byte after the target's comes from
+ *      a distinct suffix in the block), so that capacity always suffices. */
+int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end, uint32_t nq,
+                                mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
+                                uint64_t vals_cap, uint64_t* key_end_out, uint64_t* val_end_out, uint64_t* kcap_out,
+                                uint64_t rec_cap, uint8_t* key_buf, uint64_t key_buf_cap, void* stream);
 
 /* (3) the offsets of the entries seek_to_first + next visit in a block (the index block: entry
  *     i <-> index record i <-> directory entry i), so a seek's landed entry maps to its index

@@ -1227,6 +1227,10 @@ struct alignas(16) PipeLds {
   // the count of CRC waves done (monotonic; the last of a tile finalises it)
   uint32_t crcT[P::VERIFY ? 4 : 1][P::VERIFY ? 256 : 1];
   uint32_t cacc[2][P::VERIFY ? P::MAXBLK : 1];
+  uint32_t cst[2][P::VERIFY ? P::MAXBLK : 1];   // stored checksums (copy wave 0), by tile parity
+  uint32_t cfr[2][P::VERIFY ? P::MAXBLK : 1];   // ... present (framed batch, offset >= 4)
+  uint32_t shK[P::VERIFY ? 64 : 1];              // window shifts x^(8 W l), lane l
+  uint32_t shX[P::VERIFY ? 32 : 1];              // round shifts x^(8 W 64 r)
   uint32_t crcdone;
 };
 
@@ -1983,108 +1987,85 @@ __device__ __forceinline__ void pipe_copy(const PipeBuf<P>& B, const TileArgs& a
 // ---------------------------------------------------------------------------------
 // fused CRC-32C verify (VERIFY kernels): the checksum Reader::block asserts
 // before it decodes a block (src/reader.rs:159-164, crate crc32c 0.4), computed from the tile
-// already staged in LDS by the waves that otherwise idle there: the look-back wave after its
-// look-back and the two loader waves after issuing their DMA.  64-byte chunks counted from
-// each block's END (chunk k is shifted by x^(512 k), a table lookup + one GF(2) multiply),
-// slicing-by-4 over 16 words, 4 chunks in flight per lane; contributions are XORed into a
-// per-block LDS accumulator; the last of the three waves to finish a tile finalises it.
+// already staged in LDS by the COPY waves once their copy is done (they have the issue slots;
+// round 2 ran it on the look-back and loader waves, which sit on the pipeline's critical path:
+// 0.59 ms vs 0.148 for the decode alone, and ablating the CRC loop gave back 0.41 ms of it).
+//   * a block's windows are 72 bytes counted from its END (window k = block bytes
+//     [L - 72 (k + 1), L - 72 k)); bytes before the block start read as zero (leading zeros
+//     leave a zero-init CRC unchanged) and the 0xFFFFFFFF init is folded into bytes 0..3;
+//   * lane l takes windows k = l + 64 r: raw CRC by slicing-by-4 over 18 words (LDS tables),
+//     shifted into place by x^(576 k) = K_l * X^r with K_l = x^(576 l) and X^r = x^(576 64 r)
+//     held in registers from the kernel start (a GF(2) multiply each, none for r = 0);
+//   * the wave XOR-reduces; copy wave w takes blocks w, w + NC, ... (or, with fewer blocks than
+//     copy waves, one of g = NC / nb waves per block takes rounds r = s (mod g)); partials go
+//     into a per-block LDS accumulator; the last copy wave to finish a tile finalises it.
+// Copy wave 0 loads the stored checksums (the u32 before each content) at the start of its
+// share, so their latency hides behind the window work.
 // ---------------------------------------------------------------------------------
 template <class P>
-constexpr int kCrcWaves = 1 + P::LOADW;   // the look-back wave + the loader waves
-
-template <class P>
 __device__ __forceinline__ uint32_t crc_word4(const PipeLds<P>& S, uint32_t c, uint32_t w) {
-  c ^= w;   // slicing-by-4 (measured 0.62 ms vs 0.74 ms byte-at-a-time in this kernel, cfg2)
+  c ^= w;   // slicing-by-4 (the LDS budget of PipeSmallV leaves room for 4 tables, not 8)
   return S.crcT[3][c & 0xffu] ^ S.crcT[2][(c >> 8) & 0xffu] ^ S.crcT[1][(c >> 16) & 0xffu] ^ S.crcT[0][c >> 24];
 }
 
-// Always inlined: under register pressure the compiler outlined one call site (PipeLargeV's
-// look-back wave) and the out-of-line call is what faulted ("the spill fault");
-// MTBLX_CRC_NOINLINE (diagnostic builds only) forces the call.
+// Always inlined: under register pressure the compiler outlined a call of the round-2 CRC
+// routine (PipeLargeV's look-back wave) and the out-of-line call is what faulted (DESIGN.md §4,
+// "the spill fault"); MTBLX_CRC_NOINLINE (diagnostic builds only) forces the call.
 #ifdef MTBLX_CRC_NOINLINE
 #define MTBLX_PIPE_CRC_INLINE __attribute__((noinline))
 #else
 #define MTBLX_PIPE_CRC_INLINE __forceinline__
 #endif
 // MTBLX_ABL_CRC (diagnostic ablation builds only; results are wrong by construction):
-// bit 0 skips the chunk loop, bit 1 the stored-checksum reads of the finalisation, bit 2 the
-// whole pipe_crc
+// bit 0 skips the window loop, bit 1 the stored-checksum reads, bit 2 the whole CRC
 #ifndef MTBLX_ABL_CRC
 #define MTBLX_ABL_CRC 0
 #endif
+#ifndef MTBLX_CRC_WIN
+#define MTBLX_CRC_WIN 72     // window bytes (36: 0.375 ms, 72: 0.340 on cfg2 -- LDS lookups, not chains, bound it)
+#endif
+#ifndef MTBLX_CRC_INFLIGHT
+#define MTBLX_CRC_INFLIGHT 1 // window rounds in flight per lane (2: 0.416 ms at 72 B windows)
+#endif
+#ifndef MTBLX_CRC_UNROLL
+#define MTBLX_CRC_UNROLL 9   // window steps unrolled
+#endif
+#ifndef MTBLX_CRC_EARLY
+#define MTBLX_CRC_EARLY 0    // 1: before the copy (the tile is staged; the copy waits on the look-back)
+#endif
+constexpr uint32_t kCrcWinB = MTBLX_CRC_WIN;
+constexpr uint32_t kCrcRounds = (65664u + 64u * kCrcWinB - 1u) / (64u * kCrcWinB);   // rounds of the largest block
+
+// raw CRC (init 0) of the window whose first byte is at stage address A (block position p0);
+// positions < 0 are zero, the init is folded into positions 0..3
 template <class P>
-__device__ MTBLX_PIPE_CRC_INLINE void pipe_crc(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, int cw, int lane, uint32_t par) {
-  if constexpr ((MTBLX_ABL_CRC & 4) != 0) return;
+__device__ __forceinline__ uint32_t lds_window_raw(const PipeLds<P>& S, const uint32_t* st32, int32_t A, int32_t p0) {
+  const int32_t q = A >> 2;                       // floor
+  const uint32_t sft = (uint32_t)(A & 3) * 8u;
+  uint32_t d0 = q >= 0 ? st32[q] : 0u;
+  uint32_t c = 0;
+#pragma unroll MTBLX_CRC_UNROLL
+  for (int m = 0; m < (int)kCrcWinB / 4; ++m) {
+    const int32_t qa = q + m + 1;
+    const uint32_t d1 = qa >= 0 ? st32[qa] : 0u;
+    uint32_t w = __builtin_amdgcn_alignbit(d1, d0, sft);
+    d0 = d1;
+    const int32_t pos = p0 + 4 * m;               // block position of the word's first byte
+    if (pos < 4) {
+      const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8u * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+      const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8u * (uint32_t)pos);
+      w = (w & keep) ^ fold;
+    }
+    c = crc_word4(S, c, w);
+  }
+  return c;
+}
+
+// the finalisation of tile B's checksums: crc[] / crc_bad[] of its blocks (lanes < nb)
+template <class P>
+__device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, int lane,
+                                               uint32_t par) {
   const uint32_t nb = B.nb, b0 = B.b0;
-  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(B.stage);
-  const uint32_t gl = (uint32_t)cw * kWave + (uint32_t)lane;
-  // chunks of staged blocks of >= 4 bytes, numbered across the tile
-  uint32_t total = 0;
-  if constexpr ((MTBLX_ABL_CRC & 1) == 0)
-  for (uint32_t j = 0; j < nb; ++j) {
-    const uint32_t L = B.blen[j];
-    total += (B.boff[j] < kOutOfBounds && L >= 4u) ? (L + 63u) / 64u : 0u;
-  }
-  // per-lane chunk prefix of the tile's blocks (lane j < nb holds the first chunk of block j)
-  uint32_t mych = 0, myL = 0, mybo = 0;
-  if (lane < (int)nb) {
-    myL = B.blen[lane];
-    mybo = B.boff[lane];
-    mych = (mybo < kOutOfBounds && myL >= 4u) ? (myL + 63u) / 64u : 0u;
-  }
-  const uint32_t incl = wave_incl_scan(mych), excl = incl - mych;
-  constexpr int kCh = 2;   // chunks in flight per lane (register budget: 128 VGPRs at 16 waves/CU)
-  for (uint32_t base = 0; base < total; base += kCh * kCrcWaves<P> * kWave) {
-    uint32_t c[kCh], d0[kCh], jk[kCh], sft[kCh];   // jk = block << 16 | chunk
-    int32_t q[kCh], p0[kCh];   // first dword index; block position of the window's first byte
-#pragma unroll
-    for (int i = 0; i < kCh; ++i) {
-      const uint32_t ch = base + (uint32_t)i * kCrcWaves<P> * kWave + gl;
-      uint32_t j0 = 0;
-      for (uint32_t j = 1; j < nb; ++j) j0 += ((uint32_t)__shfl((int)excl, (int)j, kWave) <= ch) ? 1u : 0u;
-      const uint32_t e0 = (uint32_t)__shfl((int)excl, (int)j0, kWave);
-      const uint32_t L = (uint32_t)__shfl((int)myL, (int)j0, kWave), bo = (uint32_t)__shfl((int)mybo, (int)j0, kWave);
-      const bool on = ch < total;
-      const uint32_t k0 = on ? ch - e0 : 0xFFFFu;
-      jk[i] = j0 << 16 | k0;
-      // window [L - 64 (k0 + 1), L - 64 k0): bytes before the block start read as 0 (leading
-      // zeros leave a zero-init CRC unchanged), so every chunk is 16 word steps
-      p0[i] = on ? (int32_t)L - 64 * (int32_t)k0 - 64 : (1 << 20);   // off: never masked, result dropped
-      const int32_t A = on ? (int32_t)bo + p0[i] : 0;               // stage address (< 0 possible)
-      q[i] = A >> 2;                                                // floor
-      sft[i] = (uint32_t)(A & 3) * 8u;
-      d0[i] = q[i] >= 0 ? st32[q[i]] : 0u;
-      c[i] = 0;
-    }
-#pragma unroll 2
-    for (int m = 0; m < 16; ++m) {
-#pragma unroll
-      for (int i = 0; i < kCh; ++i) {
-        const int32_t pos = p0[i] + 4 * m;           // block position of the word's first byte
-        const int32_t qa = q[i] + m + 1;
-        const uint32_t d1 = qa >= 0 ? st32[qa] : 0u;
-        uint32_t w = __builtin_amdgcn_alignbit(d1, d0[i], sft[i]);
-        d0[i] = d1;
-        if (pos < 4) {   // leading zeros (pos < 0) and the 0xFFFFFFFF init folded into bytes 0..3
-          const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8u * (uint32_t)(-pos)) : 0xFFFFFFFFu);
-          const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8u * (uint32_t)pos);
-          w = (w & keep) ^ fold;
-        }
-        c[i] = crc_word4(S, c[i], w);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < kCh; ++i) {
-      const uint32_t k0 = jk[i] & 0xFFFFu;
-      if (k0 != 0xFFFFu) atomicXor(&S.cacc[par][jk[i] >> 16], mtblx_crc::dmultmodp(mtblx_crc::xpow512(k0), c[i]));
-    }
-  }
-  // the last CRC wave of this tile finalises it
-  uint32_t old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(&S.crcdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-  old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-  if (old % kCrcWaves<P> != kCrcWaves<P> - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   uint32_t crc = 0, L = 0, o = kNotStaged;
   if (lane < (int)nb) {
     L = B.blen[lane];
@@ -2110,17 +2091,105 @@ __device__ MTBLX_PIPE_CRC_INLINE void pipe_crc(const PipeBuf<P>& B, const TileAr
     if (a.crc) a.crc[b] = crc;
     if (a.crc_bad) {
       uint8_t bad = 0;
-      const uint64_t off = a.blk_off[b];
-      if (o == kOutOfBounds) {
-        bad = 1;   // the reference's slice of the block panics before its checksum
-      } else if (a.crc_framed && off >= 4 && (MTBLX_ABL_CRC & 2) == 0) {
-        const uint8_t* d = a.data + off;
-        const uint32_t stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
-        bad = stored != crc;
-      }
+      if (o == kOutOfBounds) bad = 1;   // the reference's slice of the block panics before its checksum
+      else if (a.crc_framed && S.cfr[par][lane]) bad = S.cst[par][lane] != crc;
       a.crc_bad[b] = bad;
     }
   }
+}
+
+// copy wave cw (of NC) after its copy of tile B: its share of the windows, then the count; the
+// last of the NC waves finalises the tile
+template <class P>
+__device__ MTBLX_PIPE_CRC_INLINE void pipe_crc_copy(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, uint32_t cw,
+                                                    int lane, uint32_t par) {
+  if constexpr ((MTBLX_ABL_CRC & 4) != 0) return;
+  constexpr uint32_t NC = (uint32_t)P::NCOPY;
+  constexpr int kIn = MTBLX_CRC_INFLIGHT;
+  const uint32_t nb = B.nb;
+  // copy wave 0: the stored checksums (framed batches), loaded now, written to LDS at the end
+  uint32_t stored = 0, framed = 0;
+  if (cw == 0 && lane < (int)nb && a.crc_framed && (MTBLX_ABL_CRC & 2) == 0) {
+    const uint64_t off = a.blk_off[B.b0 + lane];
+    if (off >= 4) {
+      const uint8_t* d = a.data + off;
+      stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
+      framed = 1;
+    }
+  }
+  const uint32_t* st32 = reinterpret_cast<const uint32_t*>(B.stage);
+  const uint32_t g = nb >= NC ? 1u : NC / nb;           // waves per block
+  const uint32_t jstep = nb >= NC ? NC : nb;            // (nb < NC: one block per wave, then done)
+  if constexpr ((MTBLX_ABL_CRC & 1) == 0)
+  for (uint32_t j = nb >= NC ? cw : cw / g; j < nb; j += jstep) {
+    const uint32_t s = nb >= NC ? 0u : cw % g;
+    const uint32_t L = B.blen[j], bo = B.boff[j];
+    if (bo >= kOutOfBounds || L < 4u) continue;         // finalisation: from HBM / byte-wise
+    const uint32_t nwin = (L + kCrcWinB - 1) / kCrcWinB, nr = (nwin + 63u) / 64u;
+    uint32_t acc = 0;
+    if constexpr (kIn == 1) {
+      for (uint32_t r = s; r < nr; r += g) {
+        const uint32_t k = (uint32_t)lane + 64u * r;
+        uint32_t c = 0;
+        if (k < nwin) {
+          const int32_t p0 = (int32_t)L - (int32_t)(kCrcWinB * (k + 1u));
+          c = lds_window_raw(S, st32, (int32_t)bo + p0, p0);
+        }
+        acc ^= r ? mtblx_crc::dmultmodp(S.shX[r], c) : c;
+      }
+    } else
+    for (uint32_t r0 = s; r0 < nr; r0 += g * kIn) {
+      // rounds r0, r0 + g, ... (kIn of them) side by side: independent chains
+      uint32_t c[kIn], d0[kIn];
+      int32_t Aw[kIn], p0[kIn];
+#pragma unroll
+      for (int i = 0; i < kIn; ++i) {
+        const uint32_t k = (uint32_t)lane + 64u * (r0 + (uint32_t)i * g);
+        const bool on = r0 + (uint32_t)i * g < nr && k < nwin;
+        p0[i] = on ? (int32_t)L - (int32_t)(kCrcWinB * (k + 1u)) : (1 << 20);   // off: never masked, dropped
+        Aw[i] = on ? (int32_t)bo + p0[i] : 0;
+        d0[i] = Aw[i] >= 0 ? st32[Aw[i] >> 2] : 0u;
+        c[i] = 0;
+      }
+#pragma unroll MTBLX_CRC_UNROLL
+      for (int m = 0; m < (int)kCrcWinB / 4; ++m) {
+#pragma unroll
+        for (int i = 0; i < kIn; ++i) {
+          const int32_t qa = (Aw[i] >> 2) + m + 1;
+          const uint32_t d1 = qa >= 0 ? st32[qa] : 0u;
+          uint32_t w = __builtin_amdgcn_alignbit(d1, d0[i], (uint32_t)(Aw[i] & 3) * 8u);
+          d0[i] = d1;
+          const int32_t pos = p0[i] + 4 * m;           // block position of the word's first byte
+          if (pos < 4) {
+            const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8u * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+            const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8u * (uint32_t)pos);
+            w = (w & keep) ^ fold;
+          }
+          c[i] = crc_word4(S, c[i], w);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kIn; ++i) {
+        const uint32_t r = r0 + (uint32_t)i * g;
+        if (r >= nr || p0[i] == (1 << 20)) continue;
+        acc ^= r ? mtblx_crc::dmultmodp(S.shX[r], c[i]) : c[i];
+      }
+    }
+    acc = mtblx_crc::dmultmodp(S.shK[lane], acc);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o, kWave);
+    if (lane == 0) __hip_atomic_fetch_xor(&S.cacc[par][j], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (cw == 0 && lane < (int)nb) {
+    S.cst[par][lane] = stored;
+    S.cfr[par][lane] = framed;
+  }
+  uint32_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(&S.crcdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+  if (old % NC != NC - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  pipe_crc_final(B, a, S, lane, par);
 }
 
 #ifdef MTBLX_LARGE_SERIAL
@@ -2179,6 +2248,9 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   if constexpr (P::VERIFY) {
     for (int i = tid; i < 4 * 256; i += kPipeThreads) S.crcT[i >> 8][i & 255] = mtblx_crc::kTab.slice[i >> 8][i & 255];
     for (int i = tid; i < 2 * P::MAXBLK; i += kPipeThreads) S.cacc[i / P::MAXBLK][i % P::MAXBLK] = 0;
+    // the copy waves' window / round shift constants (read after the barrier before the loop)
+    if (tid < 64) S.shK[tid] = mtblx_crc::xpow8((uint64_t)kCrcWinB * (uint32_t)tid);
+    else if (tid < 64 + (int)kCrcRounds) S.shX[tid - 64] = mtblx_crc::xpow8((uint64_t)kCrcWinB * 64u * (uint32_t)(tid - 64));
   }
 
   uint64_t tinc[3] = {0, 0, 0};           // wave 1
@@ -2239,7 +2311,6 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           load_info(it + 2);
         }
         ST.hit(4);
-        if constexpr (P::VERIFY) pipe_crc(C, a, S, 1 + (int)part, lane, it & 1u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+1 (read next phase)
         ST.hit(6);
       } else if (wv == 1) {
@@ -2247,10 +2318,11 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         pipe_lookback_issue(a, tc, G, lbv, lane);
         pipe_lookback(C, a, tc, G, tinc, lbv, lane, &S.ready, it + 1);
         ST.hit(1);
-        if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, it & 1u);
       } else {
         wait_flag(a, &S.pub, it + 1);
+        if constexpr (P::VERIFY && MTBLX_CRC_EARLY) pipe_crc_copy(C, a, S, (uint32_t)(wv - P::COPY0), lane, it & 1u);
         pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, it + 1, ST, S.cmk[wv]);
+        if constexpr (P::VERIFY && !MTBLX_CRC_EARLY) pipe_crc_copy(C, a, S, (uint32_t)(wv - P::COPY0), lane, it & 1u);
         ST.hit(7);
       }
       raw_barrier();
@@ -2350,9 +2422,6 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         load_info(k2 + 1);
       }
       ST.hit(4);
-      if constexpr (P::VERIFY) {
-        if (it >= 0) pipe_crc(S.buf[(uint32_t)it % P::NBUF], a, S, 1 + (int)part, lane, (uint32_t)it & 1u);
-      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // retire the DMA of tile it+2 (read next phase)
       ST.hit(6);
     } else if (it >= 0) {
@@ -2363,8 +2432,6 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         if (it + 1 == (int)nloc) TLW(8);         // look-back of the last tile done
         else if (it + 2 == (int)nloc) TLW(11);   // ... of the second-to-last
         ST.hit(1);
-        // CRC of tile it while lbv is dead (its words were consumed above): lower register pressure
-        if constexpr (P::VERIFY) pipe_crc(C, a, S, 0, lane, (uint32_t)it & 1u);
         if (k1 < nloc) {
           // the other workgroups publish A(tile it+1's predecessors) about when this
           // workgroup's wave 0 publishes A(tile it+1): issue the look-back loads after that
@@ -2378,10 +2445,12 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
         }
         ST.hit(1);
       } else {
+        if constexpr (P::VERIFY && MTBLX_CRC_EARLY) pipe_crc_copy(C, a, S, (uint32_t)(wv - P::COPY0), lane, (uint32_t)it & 1u);
         pipe_copy(C, a, wv - P::COPY0, lane, &S.ready, (uint32_t)it + 1, ST, S.cmk[wv], kRows);
         if (wv == P::COPY0 && it + 1 == (int)nloc) TLW(9);   // first copy wave: last tile's stores issued
         if (wv == P::COPY0 + P::NCOPY - 1 && it + 1 == (int)nloc) TLW(10);
         if (lane == 0) __hip_atomic_fetch_add(&S.cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (P::VERIFY && !MTBLX_CRC_EARLY) pipe_crc_copy(C, a, S, (uint32_t)(wv - P::COPY0), lane, (uint32_t)it & 1u);
         ST.hit(7);
       }
     }

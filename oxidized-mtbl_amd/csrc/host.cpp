@@ -79,12 +79,13 @@ struct BlockBuilder {
   std::vector<uint8_t> last_key;
   std::vector<uint64_t> restarts{0};
   size_t counter = 0;
+  bool finished = false;
   explicit BlockBuilder(size_t iv) : interval(iv) { buf.reserve(1 << 16); }
-  void reset() { buf.clear(); last_key.clear(); restarts.assign(1, 0); counter = 0; }
+  void reset() { buf.clear(); last_key.clear(); restarts.assign(1, 0); counter = 0; finished = false; }
   bool empty() const { return buf.empty(); }
   size_t estimate() const { return buf.size() + restarts.size() * (buf.size() > 0xFFFFFFFFull ? 8 : 4) + 4; }
   bool add(const uint8_t* k, size_t kl, const uint8_t* v, size_t vl) {
-    if (!(counter <= interval)) return false;  // assert (:50)
+    if (!(counter <= interval) || finished) return false;  // asserts (:50-51)
     size_t shared = 0;
     if (counter < interval) {
       size_t m = std::min(last_key.size(), kl);
@@ -114,8 +115,9 @@ struct BlockBuilder {
     }
     wr32(t, (uint32_t)restarts.size());
     buf.insert(buf.end(), t, t + 4);
-    out.swap(buf);
+    out.swap(buf);   // mem::replace: the builder keeps an empty buffer until reset()
     buf.clear();
+    finished = true;
   }
 };
 
@@ -161,7 +163,6 @@ struct mtblx_writer {
   uint64_t meta[9] = {0};  // footer order, src/metadata.rs:61-79
   uint32_t compression = 0;
   uint32_t level = 0;        // WriterBuilder::compression_level (DEFAULT_COMPRESSION_LEVEL = 0)
-  bool failed = false;       // a compressor error: Err(Error::Io) from insert / into_inner
   BlockBuilder data, index;
   std::vector<uint8_t> last_key;
   uint64_t last_offset = 0, pending_offset = 0;
@@ -180,15 +181,15 @@ struct mtblx_writer {
   }
   // write_block (:203-237): data blocks are compressed with the file's compression type
   // (:214), the index block never (into_inner passes CompressionType::None, :165-173); the
-  // checksum covers the STORED bytes (:217-218)
-  uint64_t write_block(BlockBuilder& b, bool is_data) {
+  // checksum covers the STORED bytes (:217-218).  A compressor Err (Lz4 / Lz4hc: "unsupported",
+  // src/compression.rs:70-81; a codec failure) returns at the `?` of :214: nothing is written
+  // and the block is not reset, so the writer stays as it was (MTBLX_E_IO).
+  int write_block(BlockBuilder& b, bool is_data, uint64_t& written) {
     b.finish(scratch);
     const std::vector<uint8_t>* stored = &scratch;
     if (is_data && compression != 0) {   // compress (src/compression.rs:70-81), codecs_host.cpp
-      if (mtblx_compress_vec(compression, level, scratch.data(), scratch.size(), zbuf) != MTBLX_CODEC_OK) {
-        failed = true;   // the crate returns the io::Error from insert / into_inner
-        zbuf.clear();
-      }
+      if (mtblx_compress_vec(compression, level, scratch.data(), scratch.size(), zbuf) != MTBLX_CODEC_OK)
+        return MTBLX_E_IO;
       stored = &zbuf;
     }
     uint8_t hdr[14];
@@ -202,25 +203,30 @@ struct mtblx_writer {
       cur_nrec = 0;
     }
     out.insert(out.end(), stored->begin(), stored->end());
-    uint64_t written = ll + 4 + stored->size();
+    written = ll + 4 + stored->size();
     last_offset = pending_offset;
     pending_offset += written;
     b.reset();
-    return written;
+    return MTBLX_OK;
   }
-  bool flush() {  // (:183-200)
-    if (data.empty()) return true;
-    if (pending_index_entry) return false;
-    meta[5] += write_block(data, true);
+  int flush() {  // (:183-200): MTBLX_OK, MTBLX_E_IO (Err), MTBLX_E_FORMAT (the assert panics)
+    if (data.empty()) return MTBLX_OK;
+    if (pending_index_entry) return MTBLX_E_FORMAT;
+    uint64_t written = 0;
+    const int r = write_block(data, true, written);
+    if (r != MTBLX_OK) return r;
+    meta[5] += written;
     meta[4] += 1;
     pending_index_entry = true;
-    return true;
+    return MTBLX_OK;
   }
 };
 
 extern "C" mtblx_writer* mtblx_writer_new(uint64_t block_size, uint64_t restart_interval, uint32_t compression) {
-  // None, Snappy, Zlib, Zstd (Lz4 / Lz4hc: the crate's compress returns Err "unsupported")
-  if (!(compression <= 2 || compression == 5) || !mtblx_codec_available(compression)) return nullptr;
+  // CompressionType 0..5.  Lz4 / Lz4hc build a writer whose first data-block flush returns Err
+  // "unsupported" (src/compression.rs:70-81): MTBLX_E_IO from insert / finish.  Zstd needs
+  // libzstd.so.1 on this host (the crate bundles it): NULL without it.
+  if (compression > 5 || (compression == 5 && !mtblx_codec_available(compression))) return nullptr;
   return new mtblx_writer(block_size, restart_interval, compression);
 }
 
@@ -239,7 +245,9 @@ extern "C" int mtblx_writer_insert(mtblx_writer* w, const uint8_t* k, uint64_t k
     return MTBLX_E_FORMAT;
   }
   if (w->data.estimate() + 15 + kl + vl >= w->meta[1]) {  // (:125-130)
-    if (!w->flush()) { w->poisoned = true; return MTBLX_E_FORMAT; }
+    const int r = w->flush();
+    if (r == MTBLX_E_IO) return r;   // Err: this record is not inserted, the writer is unchanged
+    if (r != MTBLX_OK) { w->poisoned = true; return r; }
   }
   if (w->pending_index_entry) {  // (:132-138)
     if (!shortest_separator(w->last_key, k, kl)) { w->poisoned = true; return MTBLX_E_FORMAT; }
@@ -252,7 +260,9 @@ extern "C" int mtblx_writer_insert(mtblx_writer* w, const uint8_t* k, uint64_t k
   w->meta[3] += 1;
   w->meta[7] += kl;
   w->meta[8] += vl;
-  if (!w->data.add(k, kl, v, vl)) { w->poisoned = true; return MTBLX_E_FORMAT; }
+  // BlockBuilder::add's asserts (:50-51) -- `!finished` fires on the insert after a flush whose
+  // compressor returned Err (the builder's buffer was moved out and never reset): a panic
+  if (!w->data.add(k, kl, v, vl)) { w->poisoned = true; return MTBLX_E_INVAL; }
   w->cur_nrec += 1;
   return MTBLX_OK;
 }
@@ -271,7 +281,8 @@ extern "C" int mtblx_writer_insert_batch(mtblx_writer* w, const uint8_t* keys, c
 
 extern "C" int mtblx_writer_finish(mtblx_writer* w, uint8_t** out, uint64_t* out_len) {  // into_inner (:155-181)
   if (!w || w->poisoned || !out || !out_len) return MTBLX_E_INVAL;
-  if (!w->flush() || w->failed) return MTBLX_E_FORMAT;
+  const int r = w->flush();
+  if (r != MTBLX_OK) return r;
   if (w->pending_index_entry) {
     uint8_t enc[10];
     uint32_t el = venc64(enc, w->last_offset);
@@ -279,7 +290,9 @@ extern "C" int mtblx_writer_finish(mtblx_writer* w, uint8_t** out, uint64_t* out
     w->pending_index_entry = false;
   }
   w->meta[0] = w->pending_offset;
-  w->meta[6] += w->write_block(w->index, false);
+  uint64_t written = 0;
+  w->write_block(w->index, false, written);   // CompressionType::None: cannot fail
+  w->meta[6] += written;
   uint8_t md[512];
   memset(md, 0, sizeof(md));
   for (int i = 0; i < 9; ++i) wr64(md + 8 * i, w->meta[i]);

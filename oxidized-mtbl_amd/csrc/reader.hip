@@ -457,8 +457,9 @@ __device__ int wave_cmp(const uint8_t* K, uint64_t kl, const uint8_t* t, uint64_
   return kl < tl ? -1 : (kl > tl ? 1 : 0);
 }
 
-// parse_next_key (src/block.rs:119-143): R_OK / R_END / R_PANIC / R_TOOLONG
-__device__ int s_parse(const Blk& b, SIt& it, uint8_t* K, int lane) {
+// parse_next_key (src/block.rs:119-143): R_OK / R_END / R_PANIC / R_TOOLONG (key past klim,
+// the key buffer's size)
+__device__ __forceinline__ int s_parse(const Blk& b, SIt& it, uint8_t* K, uint64_t klim, int lane) {
   it.current = it.has_next ? it.next : 0;
   if (it.current >= b.R) { it.current = b.R; return R_END; }
   uint32_t sh, ns, vl;
@@ -473,9 +474,9 @@ __device__ int s_parse(const Blk& b, SIt& it, uint8_t* K, int lane) {
     if (c < 8) c = 8;
     it.kcap = c;
   }
-  if (m + ns > kSeekKey) return R_TOOLONG;
+  if (m + ns > klim) return R_TOOLONG;
   for (uint32_t j = (uint32_t)lane; j < ns; j += 64) K[m + j] = b.d[p + j];
-  __syncthreads();   // one-wave workgroup: orders the LDS writes before other lanes read K
+  __syncthreads();   // one-wave workgroup: orders the key writes (LDS or global) before other lanes read K
   it.klen = m + ns;
   it.has_next = true;
   it.next = p + ns + vl;
@@ -488,7 +489,8 @@ __device__ int s_parse(const Blk& b, SIt& it, uint8_t* K, int lane) {
 // BlockIter::seek (src/block.rs:154-194) with the key materialised.  early: the binary search
 // returned on a restart entry with shared != 0 -- the iterator is left as it was (the caller
 // keeps its previous state; this matters for the live index iterator, src/reader.rs:303)
-__device__ int s_seek(const Blk& b, SIt& it, uint8_t* K, const uint8_t* t, uint64_t tl, int lane, bool& early) {
+__device__ __forceinline__ int s_seek(const Blk& b, SIt& it, uint8_t* K, uint64_t klim, const uint8_t* t, uint64_t tl,
+                                      int lane, bool& early) {
   uint32_t left = 0, right = b.n - 1;
   early = false;
   while (left < right) {
@@ -505,21 +507,27 @@ __device__ int s_seek(const Blk& b, SIt& it, uint8_t* K, const uint8_t* t, uint6
   it.has_next = true;
   it.next = restart_point(b, left);
   for (;;) {
-    const int r = s_parse(b, it, K, lane);
+    const int r = s_parse(b, it, K, klim, lane);
     if (r != R_OK) return r == R_END ? R_OK : r;
     if (wave_cmp(K, it.klen, t, tl, lane) >= 0) return R_OK;
     if (it.next == it.current) return R_LOOP;
   }
 }
 
+// GK: the key lives in the caller's buffer (kbuf + q * kbuf_cap) instead of LDS -- keys longer
+// than 64 KiB (mtblx_block_seek_batch_kbuf)
+template <bool GK>
 __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const uint8_t* qkeys, const uint64_t* qend,
                                                    uint32_t nq, mtblx_block_seek* qs, uint8_t* okeys,
                                                    uint64_t keys_cap, uint8_t* ovals, uint64_t vals_cap,
-                                                   uint64_t* oke, uint64_t* ove, uint64_t* okcap, uint64_t rec_cap) {
+                                                   uint64_t* oke, uint64_t* ove, uint64_t* okcap, uint64_t rec_cap,
+                                                   uint8_t* kbuf, uint64_t kbuf_cap) {
   __shared__ uint8_t stage[kSeekStage];
-  __shared__ uint8_t K[kSeekKey];
+  __shared__ uint8_t Klds[GK ? 1 : kSeekKey];
   const int lane = threadIdx.x;
+  const uint64_t klim = GK ? kbuf_cap : kSeekKey;
   for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    uint8_t* K = GK ? kbuf + (uint64_t)q * kbuf_cap : Klds;
     mtblx_block_seek Q = qs[q];
     const uint64_t k0 = q ? qend[q - 1] : 0;
     const uint8_t* t = qkeys + k0;
@@ -554,10 +562,10 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
         it.klen = 0;
         it.has_next = true;
         it.next = restart_point(b, 0);
-        r = s_parse(b, it, K, lane);
+        r = s_parse(b, it, K, klim, lane);
         if (r == R_END) r = R_OK;
       } else if (Q.first == 2) {                                   // resume: next() from a held state
-        if (tl > kSeekKey) {
+        if (tl > klim) {
           r = R_TOOLONG;
         } else {
           for (uint64_t j = (uint64_t)lane; j < tl; j += 64) K[j] = t[j];
@@ -565,11 +573,11 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
           it.klen = tl;
           it.has_next = true;
           it.next = Q.resume_off;
-          r = s_parse(b, it, K, lane);
+          r = s_parse(b, it, K, klim, lane);
           if (r == R_END) r = R_OK;
         }
       } else {
-        r = s_seek(b, it, K, t, tl, lane, early);
+        r = s_seek(b, it, K, klim, t, tl, lane, early);
       }
       Q.early = early ? 1 : 0;
       if (r != R_OK) {
@@ -593,8 +601,19 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
           if (it.vlen >= 4096) {   // big values (blocks >= 4 GiB hold values of GiBs): 16 B per lane
             typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
             const uint64_t nv = it.vlen / 16;
-            for (uint64_t c = (uint64_t)lane; c < nv; c += 64)
-              *reinterpret_cast<v4u*>(vd + Q.val_bytes + 16 * c) = *reinterpret_cast<const v4u*>(d + it.voff + 16 * c);
+            const uint8_t* vs = d + it.voff;
+            uint8_t* vo = vd + Q.val_bytes;
+            // kU loads in flight per lane (one wave moves GiBs: latency-bound otherwise)
+            constexpr uint32_t kU = 16;
+            uint64_t c = (uint64_t)lane;
+            for (; c + (kU - 1) * 64 < nv; c += kU * 64) {
+              v4u x[kU];
+#pragma unroll
+              for (uint32_t u = 0; u < kU; ++u) x[u] = *reinterpret_cast<const v4u*>(vs + 16 * (c + 64 * u));
+#pragma unroll
+              for (uint32_t u = 0; u < kU; ++u) *reinterpret_cast<v4u*>(vo + 16 * (c + 64 * u)) = x[u];
+            }
+            for (; c < nv; c += 64) *reinterpret_cast<v4u*>(vo + 16 * c) = *reinterpret_cast<const v4u*>(vs + 16 * c);
             j0 = 16 * nv;
           }
           for (uint64_t j = j0 + (uint64_t)lane; j < it.vlen; j += 64) vd[Q.val_bytes + j] = d[it.voff + j];
@@ -608,7 +627,7 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
         Q.key_bytes = kb;
         Q.val_bytes = vb;
         if (it.has_next && it.next == it.current) { Q.end = MTBLX_EMIT_LOOP; break; }
-        r = s_parse(b, it, K, lane);                               // BlockIter::next
+        r = s_parse(b, it, K, klim, lane);                         // BlockIter::next
         if (r == R_PANIC) { Q.end = MTBLX_EMIT_PANIC; break; }
         if (r == R_TOOLONG) { Q.status = MTBLX_SEEK_UNSUPPORTED; break; }
       }
@@ -793,9 +812,24 @@ extern "C" int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, 
                                       uint64_t* kcap_out, uint64_t rec_cap, void* stream) {
   if (nq == 0) return MTBLX_OK;
   if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out) return MTBLX_E_INVAL;
-  hipLaunchKernelGGL(mtblx_rd::k_block_seek, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
+  hipLaunchKernelGGL(mtblx_rd::k_block_seek<false>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
-                     vals_cap, key_end_out, val_end_out, kcap_out, rec_cap);
+                     vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, nullptr, 0);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end,
+                                           uint32_t nq, mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap,
+                                           uint8_t* out_vals, uint64_t vals_cap, uint64_t* key_end_out,
+                                           uint64_t* val_end_out, uint64_t* kcap_out, uint64_t rec_cap,
+                                           uint8_t* key_buf, uint64_t key_buf_cap, void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out || !key_buf ||
+      key_buf_cap == 0)
+    return MTBLX_E_INVAL;
+  hipLaunchKernelGGL(mtblx_rd::k_block_seek<true>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
+                     vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, key_buf, key_buf_cap);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
 

@@ -17,7 +17,7 @@ u32p = C.POINTER(C.c_uint32)
 u64p = C.POINTER(C.c_uint64)
 i32p = C.POINTER(C.c_int32)
 
-MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT, MTBLX_E_TIMEOUT = 0, -1, -2, -3, -4, -5
+MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT, MTBLX_E_TIMEOUT, MTBLX_E_IO = 0, -1, -2, -3, -4, -5, -6
 ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW, ST_DECOMPRESS = range(7)
 SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL = range(3)
 CODEC_OK, CODEC_CORRUPT, CODEC_UNSUPPORTED = range(3)
@@ -38,7 +38,8 @@ EXPORTS = [
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
     "mtblx_codec_available", "mtblx_decompress", "mtblx_compress", "mtblx_decompress_blocks", "mtblx_writer_set_level",
-    "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_entry_offsets", "mtblx_key_filter",
+    "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_block_seek_batch_kbuf", "mtblx_entry_offsets",
+    "mtblx_key_filter",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
 
@@ -202,6 +203,9 @@ def lib() -> C.CDLL:
                                              C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_uint64, C.c_void_p]
         L.mtblx_block_seek_batch.restype = C.c_int
+        L.mtblx_block_seek_batch_kbuf.argtypes = L.mtblx_block_seek_batch.argtypes[:-1] + [C.c_void_p, C.c_uint64,
+                                                                                          C.c_void_p]
+        L.mtblx_block_seek_batch_kbuf.restype = C.c_int
         L.mtblx_entry_offsets.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                            C.c_void_p]
         L.mtblx_entry_offsets.restype = C.c_int

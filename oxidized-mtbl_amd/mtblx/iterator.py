@@ -111,22 +111,30 @@ def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 <
     keys_cap, vals_cap = 2 * ln + 64, ln + 16
     if small_caps:
         rec_cap, keys_cap, vals_cap = min(rec_cap, 1 << 16), min(keys_cap, 1 << 20), min(vals_cap, 1 << 20)
-    for _ in range(3):
+    kbuf = None   # the iterator's key: 64 KiB of LDS, or (a longer key) a device buffer
+    for _ in range(4):
         qt = torch.frombuffer(bytearray(bytes(q)), dtype=torch.uint8).to(dev)
         okeys = torch.empty(max(keys_cap, 1), dtype=torch.uint8, device=dev)
         ovals = torch.empty(max(vals_cap, 1), dtype=torch.uint8, device=dev)
         oke = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev)
         ove = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev)
         okc = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev)
-        rc = _lib.lib().mtblx_block_seek_batch(C.c_void_p(data.data_ptr()), C.c_void_p(kb.data_ptr()),
-                                               C.c_void_p(ke.data_ptr()), 1, C.c_void_p(qt.data_ptr()),
-                                               C.c_void_p(okeys.data_ptr()), keys_cap, C.c_void_p(ovals.data_ptr()),
-                                               vals_cap, C.c_void_p(oke.data_ptr()), C.c_void_p(ove.data_ptr()),
-                                               C.c_void_p(okc.data_ptr()), rec_cap,
-                                               C.c_void_p(codec._stream_handle(None)))
+        args = [C.c_void_p(data.data_ptr()), C.c_void_p(kb.data_ptr()), C.c_void_p(ke.data_ptr()), 1,
+                C.c_void_p(qt.data_ptr()), C.c_void_p(okeys.data_ptr()), keys_cap, C.c_void_p(ovals.data_ptr()),
+                vals_cap, C.c_void_p(oke.data_ptr()), C.c_void_p(ove.data_ptr()), C.c_void_p(okc.data_ptr()), rec_cap]
+        if kbuf is None:
+            rc = _lib.lib().mtblx_block_seek_batch(*args, C.c_void_p(codec._stream_handle(None)))
+        else:
+            rc = _lib.lib().mtblx_block_seek_batch_kbuf(*args, C.c_void_p(kbuf.data_ptr()), kbuf.numel(),
+                                                        C.c_void_p(codec._stream_handle(None)))
         if rc != 0:
             raise RuntimeError(f"mtblx_block_seek_batch failed: {rc}")
         res = _lib.BlockSeek.from_buffer_copy(qt.cpu().numpy().tobytes())
+        if res.status == _lib.SEEK_UNSUPPORTED and kbuf is None:
+            # a key past 64 KiB: again with the key in device memory, sized for any key this
+            # iterator can build (the held key plus every suffix in the block)
+            kbuf = torch.empty(len(key or b"") + ln + 64, dtype=torch.uint8, device=dev)
+            continue
         if res.end != _lib.EMIT_OVERFLOW:
             n = int(res.nrec)
             return Emitted(res, okeys[: int(res.key_bytes)], ovals[: int(res.val_bytes)], oke[:n], ove[:n], okc[:n])
@@ -209,7 +217,7 @@ def bulk(r, kind: str, key: bytes, key2: bytes = b""):
     if head.status == _lib.SEEK_LOOP:
         return empty(END_LOOP)
     if head.status == _lib.SEEK_UNSUPPORTED:
-        raise NotImplementedError("emitting seek: block >= 4 GiB or key > 64 KiB")
+        raise RuntimeError("emitting seek: key buffer too small")
     parts = [(head.keys, head.vals, head.key_end, head.val_end, head.nrec)]
     end, err = END_NONE, "None"
     stop = key_filter(head.keys, head.key_end, head.nrec, typ, k)
@@ -438,7 +446,7 @@ class ReaderIntoIter:
         if em.status == _lib.SEEK_LOOP:
             raise ReferenceLoop("index seek")
         if em.status == _lib.SEEK_UNSUPPORTED:
-            raise NotImplementedError("emitting seek: index key > 64 KiB")
+            raise RuntimeError("emitting seek: key buffer too small")
         if em.early:                 # returned on a corrupt restart entry: the old position stays
             return
         self.ix = _IxList(em, self.r._chain_ordinal(em.entry) if em.nrec else None)
@@ -468,7 +476,7 @@ class ReaderIntoIter:
         if em.status == _lib.SEEK_PANIC:
             raise ReferencePanic("index block: next entry")
         if em.status == _lib.SEEK_UNSUPPORTED:
-            raise NotImplementedError("emitting seek: index key > 64 KiB")
+            raise RuntimeError("emitting seek: key buffer too small")
         self.ix = _IxList(em, None if ix.ord0 is None else ix.ord0 + len(ix.recs))
         self._vchunk = None
         return self.ix.valid()
@@ -509,7 +517,7 @@ class ReaderIntoIter:
         if em.status == _lib.SEEK_LOOP:
             raise ReferenceLoop("BlockIter::seek")
         if em.status == _lib.SEEK_UNSUPPORTED:
-            raise NotImplementedError("emitting seek: block >= 4 GiB or key > 64 KiB")
+            raise RuntimeError("emitting seek: key buffer too small")
         bi = _Bi(content, em.host_records(), em.end, em.kcaps.cpu().numpy().tolist(), em.kcap_end)
         if em.has_val:   # BlockIter::val of the last parsed entry (Reader::get's Err quirk)
             d, o, _ = content

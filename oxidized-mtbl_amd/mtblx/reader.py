@@ -215,9 +215,9 @@ class Reader:
         L.mtblx_free(dst)
         zerr = zst[:nb].copy()
         zerr[~ok] = 0
-        if (dlen[:nb] > 0xFFFFFFFF).any():
-            raise NotImplementedError("decompressed block >= 4 GiB")
-        return buf, doff[:nb].copy(), dlen[:nb].astype(np.uint32), zerr
+        # u64 lengths: a content >= 4 GiB is not decoded by the batched call (u32 lengths) but by
+        # the emitting block seek on its bytes in the uploaded buffer (_big_content)
+        return buf, doff[:nb].copy(), dlen[:nb].copy(), zerr
 
     def iter(self) -> Scan:
         """ReaderIntoIter (mode Iter) to the end: the records yielded and how it ends."""
@@ -246,7 +246,7 @@ class Reader:
         ReaderIntoIter::new, whose Err is an Err at open and whose emptiness does not end it).
         Blocks >= 4 GiB are decoded one by one (_big_block) and spliced in.
         -> (parts [(keys, vals, key_end, val_end, nrec)], end, err, stopped)"""
-        dst, bad, zerr, data, _ = self._decode_range(i0, i1)
+        dst, bad, zerr, data, (base, boff, blen) = self._decode_range(i0, i1)
         n = i1 - i0
         bst = data.status[:n].cpu().numpy()
         bnr = data.nrec[:n].cpu().numpy().astype(np.int64)
@@ -258,10 +258,14 @@ class Reader:
 
         i = 0
         while i < n:
-            if dst[i] == _lib.DIR_UNSUPPORTED:   # content >= 4 GiB (u64 restart array)
+            # content >= 4 GiB (u64 restart array): stored that big (DIR_UNSUPPORTED: framed,
+            # checked and decompressed by _big_block), or decompressed that big (_big_content)
+            big_dec = dst[i] == _lib.DIR_OK and not bad[i] and not zerr[i] and int(blen[i]) > 0xFFFFFFFF
+            if dst[i] == _lib.DIR_UNSUPPORTED or big_dec:
                 parts.append(self._slice(data, seg, i, 0))
                 seg = i + 1
-                kind, em = self._big_block(i0 + i)
+                kind, em = (self._big_content((base, int(boff[i]), int(blen[i]))) if big_dec
+                            else self._big_block(i0 + i))
                 if kind == "panic":
                     end, stopped = END_PANIC, True
                     break
@@ -290,8 +294,8 @@ class Reader:
             if st == _lib.ST_INVALID_BLOCK:
                 end, err, stopped = errend(i), "InvalidBlock", True
                 break
-            if st == _lib.ST_UNSUPPORTED:
-                raise NotImplementedError("decompressed block >= 4 GiB")
+            if st == _lib.ST_UNSUPPORTED:     # the batch carries u32 lengths: cannot happen
+                raise RuntimeError("batched decode: block >= 4 GiB")
             if st == _lib.ST_OK and bnr[i] == 0 and not (first_exempt and i == 0):
                 stopped = True                         # an empty block ends the iteration (:362-371)
                 break
@@ -370,18 +374,27 @@ class Reader:
         """Reader::block + Block::init + the scan for a block >= 4 GiB (u64 restart array,
         src/block.rs:25-42): decoded on the device by the emitting block seek (seek_to_first).
         -> ("ok", Emitted) | ("panic", None) | ("loop", None) | (error name, None)"""
-        return self._big_block_value(self._index_records()[i][1])
+        return self._big_block_value(self._index_records()[i][1])[:2]
 
     def _big_block_value(self, value: bytes):
-        from . import iterator
-        if self.compression != 0:
-            raise NotImplementedError("compressed block >= 4 GiB")
         off, start, size, stored = self._big_frame_value(value)
         if start > self.len or size > self.len - start:
-            return "panic", None
+            return "panic", None, None
         if self.verify and self._crc_big(start, size) != stored:
-            return "panic", None                       # assert_eq of the checksum (src/reader.rs:163)
-        em = iterator.block_seek((self.file, start, size), None, 0, small_caps=True)
+            return "panic", None, None                 # assert_eq of the checksum (src/reader.rs:163)
+        if self.compression == 0:
+            content = (self.file, start, size)
+        else:
+            try:                                       # src/reader.rs:166-170 (host, any size)
+                content = self._decompressed(start, size)
+            except MtblError:
+                return "Io", None, None
+        return self._big_content(content) + (content,)
+
+    def _big_content(self, content):
+        """Block::init + the scan of a content >= 4 GiB (tensor, off, len) on the device"""
+        from . import iterator
+        em = iterator.block_seek(content, None, 0, small_caps=True)
         if em.status == _lib.SEEK_ERR:
             return "InvalidBlock", None
         if em.status == _lib.SEEK_PANIC:
@@ -389,7 +402,7 @@ class Reader:
         if em.status == _lib.SEEK_LOOP:
             return "loop", None
         if em.status == _lib.SEEK_UNSUPPORTED:
-            raise NotImplementedError("a key > 64 KiB in a block >= 4 GiB")
+            raise RuntimeError("emitting seek: key buffer too small")
         return "ok", em
 
     # ------------------------------------------------------------------ point queries
@@ -565,12 +578,12 @@ class Reader:
         content (tensor, off, len) BlockIter reads; raises the reference's panics / Err"""
         off, ln, st = self._frame_values([value])
         s = int(st[0].item())
-        if s == _lib.DIR_UNSUPPORTED:                   # content >= 4 GiB
-            if self.compression != 0:
-                raise NotImplementedError("compressed block >= 4 GiB")
+        if s == _lib.DIR_UNSUPPORTED:                   # stored content >= 4 GiB
             _, start, size, stored = self._big_frame_value(value)
             if self.verify and self._crc_big(start, size) != stored:
                 raise ReferencePanic("Reader::block: checksum")
+            if self.compression != 0:
+                return self._decompressed(start, size)
             return self.file, start, size
         if s != _lib.DIR_OK:
             raise ReferencePanic("Reader::block: framing")
@@ -591,8 +604,8 @@ class Reader:
         if self.compression == 0:
             if s.block_status == _lib.SEEK_ERR:
                 raise MtblError(6)
-            if s.block_status == _lib.SEEK_UNSUPPORTED:
-                raise NotImplementedError("block >= 4 GiB")
+            if s.block_status == _lib.SEEK_UNSUPPORTED:   # frame_block handles any size
+                raise RuntimeError("index seek: unexpected block status")
             return self.file, int(s.data_off), int(s.data_len)
         # compressed: Block::init runs on the decompressed content (mtblx_block_seek_batch);
         # block_status's ERR / UNSUPPORTED judged the compressed bytes and do not apply
@@ -634,7 +647,8 @@ class Reader:
         bad = bad.cpu().numpy() if bad is not None else np.zeros(n, np.uint8)
         if self.compression != 0:
             buf, uoff, uln, zerr = self._host_stage(off, ln, st)
-            batch = codec.DeviceBatch.from_host(buf, uoff, uln, device=self.file.device)
+            small = np.where(uln > 0xFFFFFFFF, 0, uln).astype(np.uint32)   # >= 4 GiB: _big_content
+            batch = codec.DeviceBatch.from_host(buf, uoff, small, device=self.file.device)
             where = (batch.data, uoff.astype(np.int64), uln.astype(np.int64))
         else:
             zerr = np.zeros(n, np.int32)
@@ -665,16 +679,19 @@ class Reader:
         out = []
         for i in range(len(values)):
             content = (base, int(boff[i]), int(blen[i]))
-            if dst[i] == _lib.DIR_UNSUPPORTED:   # content >= 4 GiB
-                kind, em = self._big_block_value(values[i])
+            big_dec = dst[i] == _lib.DIR_OK and not bad[i] and not zerr[i] and int(blen[i]) > 0xFFFFFFFF
+            if dst[i] == _lib.DIR_UNSUPPORTED or big_dec:   # content >= 4 GiB
+                if big_dec:
+                    kind, em = self._big_content(content)
+                else:
+                    kind, em, content = self._big_block_value(values[i])
                 if kind == "ok":
-                    fr = self._big_frame_value(values[i])
-                    out.append(((self.file, fr[1], fr[2]), em.host_records(), em.end))
+                    out.append((content, em.host_records(), em.end))
                 elif kind in ("panic", "loop"):
                     out.append(ReferencePanic("Reader::block / BlockIter") if kind == "panic"
                                else ReferenceLoop("BlockIter::next"))
                 else:
-                    out.append(MtblError(6))
+                    out.append(MtblError(7 if kind == "Io" else 6))
                 continue
             if dst[i] != _lib.DIR_OK or bad[i]:
                 out.append(ReferencePanic("Reader::block"))
@@ -685,8 +702,8 @@ class Reader:
             s = int(h.status[i])
             if s == _lib.ST_INVALID_BLOCK:
                 out.append(MtblError(6))
-            elif s == _lib.ST_UNSUPPORTED:
-                out.append(NotImplementedError("block >= 4 GiB"))
+            elif s == _lib.ST_UNSUPPORTED:   # the batch carries u32 lengths: cannot happen
+                out.append(RuntimeError("batched decode: block >= 4 GiB"))
             else:
                 end = {_lib.ST_CORRUPT: _lib.EMIT_PANIC, _lib.ST_LOOP: _lib.EMIT_LOOP}.get(s, _lib.EMIT_END)
                 out.append((content, h.records(i), end))

@@ -27,8 +27,24 @@ class CompressionType:
     Zstd = 5
 
 
-class OutOfOrderKey(RuntimeError):
-    """the reference panics with "out-of-order key" (src/writer.rs:121)"""
+class WriterPanic(RuntimeError):
+    """Where the reference's Writer panics: an assert in BlockBuilder::add (src/block_builder.rs:
+    50-51) -- the insert after a flush whose compressor returned Err -- or use after a panic."""
+
+
+class OutOfOrderKey(WriterPanic):
+    """panic!("out-of-order key") (src/writer.rs:119-123)."""
+
+
+class WriterIoError(OSError):
+    """Err(io::Error) from Writer::insert / into_inner: the data block's compressor failed
+    (Lz4 / Lz4hc: "unsupported", src/compression.rs:70-81).  Nothing was written."""
+
+
+def _io_message(compression: int) -> str:
+    # the crate's message for Lz4 / Lz4hc (it says "decompression" in compress(), sic)
+    return {3: "unsupported Lz4 decompression", 4: "unsupported Lz4hc decompression"}.get(
+        compression, f"compression {compression} failed")
 
 
 class WriterBuilder:
@@ -66,9 +82,10 @@ class Writer:
         L = _lib.lib()
         self._w = L.mtblx_writer_new(int(block_size), int(restart_interval), int(compression))
         if not self._w:
-            # Lz4 / Lz4hc: the crate's compress returns Err "unsupported" (src/compression.rs:70-81)
-            raise NotImplementedError(f"compression {compression}: None, Snappy, Zlib and Zstd only "
-                                      "(Zstd needs libzstd.so.1 on this host)")
+            # Zstd without libzstd.so.1 on this host (the crate bundles its own); Lz4 / Lz4hc build
+            # a writer whose data-block flushes return Err (WriterIoError), as the crate's do
+            raise ValueError(f"compression {compression}: unknown, or Zstd without libzstd.so.1 on this host")
+        self._compression = int(compression)
         L.mtblx_writer_set_level(self._w, int(level))
         self.block_dir = None
 
@@ -86,10 +103,18 @@ class Writer:
         kb = (C.c_uint8 * max(1, len(k))).from_buffer_copy(k or b"\0")
         vb = (C.c_uint8 * max(1, len(v))).from_buffer_copy(v or b"\0")
         rc = _lib.lib().mtblx_writer_insert(self._w, kb, len(k), vb, len(v))
+        self._check(rc, "mtblx_writer_insert")
+
+    def _check(self, rc: int, what: str) -> None:
         if rc == _lib.MTBLX_E_FORMAT:
             raise OutOfOrderKey("out-of-order key")
+        if rc == _lib.MTBLX_E_IO:
+            raise WriterIoError(_io_message(self._compression))
+        if rc == _lib.MTBLX_E_INVAL:
+            raise WriterPanic("BlockBuilder::add: assertion failed (a block left finished by a failed flush), "
+                              "or the writer already panicked")
         if rc != 0:
-            raise RuntimeError(f"mtblx_writer_insert: {rc}")
+            raise RuntimeError(f"{what}: {rc}")
 
     def insert_batch(self, keys: np.ndarray, key_end: np.ndarray, vals: np.ndarray, val_end: np.ndarray) -> None:
         """Bulk insert of n records given as concatenated bytes + u64 end offsets."""
@@ -104,10 +129,7 @@ class Writer:
         rc = _lib.lib().mtblx_writer_insert_batch(self._w, keys.ctypes.data_as(_lib.u8p), ke.ctypes.data_as(_lib.u64p),
                                                   vals.ctypes.data_as(_lib.u8p), ve.ctypes.data_as(_lib.u64p),
                                                   ke.size)
-        if rc == _lib.MTBLX_E_FORMAT:
-            raise OutOfOrderKey("out-of-order key")
-        if rc != 0:
-            raise RuntimeError(f"mtblx_writer_insert_batch: {rc}")
+        self._check(rc, "mtblx_writer_insert_batch")
 
     def into_inner(self) -> bytes:
         """Writer::into_inner: the finished .mtbl bytes.  Also records the data-block directory."""
@@ -115,8 +137,7 @@ class Writer:
         out = _lib.u8p()
         n = C.c_uint64(0)
         rc = L.mtblx_writer_finish(self._w, C.byref(out), C.byref(n))
-        if rc != 0:
-            raise RuntimeError(f"mtblx_writer_finish: {rc}")
+        self._check(rc, "mtblx_writer_finish")
         arr = np.empty(n.value, np.uint8)   # (ctypes.string_at takes a C int size: no files >= 2 GiB)
         C.memmove(arr.ctypes.data, out, n.value)
         L.mtblx_free(out)
@@ -138,8 +159,7 @@ class Writer:
         out = _lib.u8p()
         n = C.c_uint64(0)
         rc = L.mtblx_writer_finish(self._w, C.byref(out), C.byref(n))
-        if rc != 0:
-            raise RuntimeError(f"mtblx_writer_finish: {rc}")
+        self._check(rc, "mtblx_writer_finish")
         arr = np.empty(n.value, np.uint8)
         C.memmove(arr.ctypes.data, out, n.value)
         L.mtblx_free(out)

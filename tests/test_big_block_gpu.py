@@ -71,3 +71,62 @@ def test_block_over_4gib(oracle):
     e2 = oracle.file_scan(bytes(d2), "iter", verify=True)
     s2 = reader.ReaderBuilder().verify_checksums(True).read(bytes(d2)).iter()
     assert s2.end == e2["end"] == reader.END_PANIC and s2.nrec == len(e2["records"]) == 0
+
+
+def test_compressed_blocks_over_4gib(oracle):
+    """Zstd (CompressionType::Zstd, src/compression.rs:140-156): a block whose DECOMPRESSED content
+    is >= 4 GiB (patterned values: stored small) and a block whose STORED content is >= 4 GiB
+    (random values: zstd stores them raw), each Block::init'ed on its u64 restart array
+    (src/block.rs:25-42) -- decompressed on the host (Reader::block, src/reader.rs:166-170) and
+    decoded on the device by the emitting block seek -- against the oracle's restatement."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if torch.cuda.get_device_properties(0).total_memory < (64 << 30):
+        pytest.skip("needs ~64 GiB of device memory")
+    import time
+    from mtblx import _lib, reader
+    from mtblx.writer import Writer
+    if not _lib.lib().mtblx_codec_available(5):
+        pytest.skip("no libzstd.so.1")
+    t0 = time.time()
+
+    def note(msg):
+        print(f"[{time.time() - t0:6.1f}s] {msg}", flush=True)
+
+    vlen = (1 << 31) + 4099
+    pat = np.tile(np.arange(256, dtype=np.uint8), vlen // 256 + 1)[:vlen]
+    rng = np.random.default_rng(7)
+    recs = [(b"a0", b"x"), (b"b", pat.tobytes()), (b"c", (pat * np.uint8(3)).tobytes()), (b"d", b"small"),
+            (b"e", rng.integers(0, 256, vlen, dtype=np.uint8).tobytes()),
+            (b"f", rng.integers(0, 256, vlen, dtype=np.uint8).tobytes()), (b"g", b"tail")]
+    del pat
+    w = Writer(4_400_000_000, 16, 5, 1)
+    for k, v in recs:
+        w.insert(k, v)
+    data = w.into_inner()
+    note(f"file written: {len(data)} bytes")
+    exp = oracle.file_scan(data, "iter", verify=True)
+    note("oracle scan done")
+    assert [k for k, _ in exp["records"]] == [k for k, _ in recs]
+    r = reader.ReaderBuilder().verify_checksums(True).read(data)
+    _, ln, st = r._framing()
+    sts = st.cpu().numpy().tolist()
+    assert sts[0] == 0 and sts[1] == 2, sts    # block 0 stored small (decompressed >= 4 GiB); block 1 stored >= 4 GiB
+    s = r.iter()
+    assert (s.end, exp["end"]) == (reader.END_NONE, 0)
+    got = s.records()
+    assert got == exp["records"]
+    note("device Reader bit-exact")
+    del got, s
+    torch.cuda.empty_cache()
+    # Reader::get and the stateful iterator into both blocks (compressed files: seek-based)
+    assert r.get(b"d") == b"small" and r.get(b"a1") is None
+    it = r.into_iter("from", b"c")
+    k1, _ = it.next()
+    assert k1 == b"c"
+    it.seek(b"e")
+    nxt = it.next()
+    exp2 = oracle.iter_script(data, "from", b"c", b"", [1, ("seek", b"e"), 1], verify=True)
+    assert nxt == exp2["records"][1]
+    note("get / seek ok")

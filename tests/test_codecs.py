@@ -183,3 +183,40 @@ def test_device_reader_and_pipe(oracle, comp, tmp_path):
         r = subprocess.run([dump, str(p)], capture_output=True, timeout=120)
         assert r.returncode == 0
         assert r.stdout == b"".join(b'"' + k + b'" "' + v + b'"\n' for k, v in recs)
+
+
+@pytest.mark.parametrize("comp", [3, 4])
+def test_writer_lz4_err_semantics(oracle, comp):
+    """WriterBuilder with Lz4 / Lz4hc (src/writer.rs:112-237, src/compression.rs:70-81): inserts
+    succeed until the first data-block flush, whose compress() returns Err "unsupported ...":
+    that insert returns the Err and its record is not added.  The data BlockBuilder's buffer was
+    moved out by finish() and never reset, so the next insert panics on `assert!(!finished)`
+    (src/block_builder.rs:51), while into_inner still succeeds -- the flush sees an empty block --
+    and writes the index and a footer whose counts include the lost block's records.  An Lz4
+    writer that never flushes a data block writes an ordinary empty file."""
+    from mtblx.writer import Writer, WriterIoError, WriterPanic
+    f = Writer(1024, 16, comp).into_inner()
+    s = oracle.file_scan(f, "iter")
+    assert s["end"] == 0 and s["records"] == []
+    assert int.from_bytes(f[-512 + 16: -512 + 24], "little") == comp
+
+    recs = [(b"k%04d" % i, b"v" * 60) for i in range(40)]
+    w = Writer(1024, 16, comp)
+    n = 0
+    with pytest.raises(WriterIoError, match="unsupported Lz4"):
+        for k, v in recs:
+            w.insert(k, v)
+            n += 1
+    assert 0 < n < len(recs)                       # the Err came from the first flush
+    with pytest.raises(WriterPanic):
+        w.insert(recs[n + 1][0], recs[n + 1][1])   # assert!(!self.finished) in BlockBuilder::add
+    w2 = Writer(1024, 16, comp)
+    for k, v in recs[:n]:
+        w2.insert(k, v)
+    with pytest.raises(WriterIoError):
+        w2.insert(*recs[n])
+    out = w2.into_inner()                          # flush: the data block is empty -> Ok
+    meta = [int.from_bytes(out[-512 + 8 * i: -512 + 8 * i + 8], "little") for i in range(9)]
+    assert meta[2] == comp and meta[3] == n and meta[4] == 0    # count_entries n, no data block
+    s = oracle.file_scan(out, "iter")
+    assert s["records"] == []

@@ -211,7 +211,7 @@ def test_crc32c_blocks_vs_oracle(oracle):
     data, off, ln = synth.cfg2_file(3000)
     rng = np.random.default_rng(8)
     # varied block sizes including < 64 B and 64 KiB contents (unframed)
-    extra = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in (0, 1, 3, 4, 5, 63, 64, 65, 1000, 65000)]
+    extra = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in (0, 1, 3, 4, 5, 63, 64, 65, 1000, 65000, 300000)]
     xd, xo, xl = corpus.pack(extra, rng=rng, lead=3)
     for d_, o_, l_, framed in ((data, off, ln, True), (xd, xo, xl, False)):
         batch = codec.DeviceBatch.from_host(d_, o_, l_)
@@ -258,6 +258,11 @@ def test_fused_verify_decode(oracle):
     cases.append((d, o, l, False, []))
     d, o, l = synth.cfg2_file(200, block_size=65536)
     cases.append((d, o, l, True, []))
+    for bs in (16384, 32768):   # PipeSmall tiles of fewer blocks than copy waves: window rounds split
+        d, o, l = synth.cfg2_file(150, block_size=bs)
+        d = d.copy()
+        d[int(o[3]) - 2] ^= 0x40
+        cases.append((d, o, l, True, [3]))
     big = [oracle.build_block(corpus.random_records(rng, 1400, 8, 60, 40, 60)) for _ in range(3)]
     assert max(len(b) for b in big) > 70000
     d, o, l = corpus.pack(big, rng=rng)

@@ -360,3 +360,41 @@ def test_compressed_get_matches_oracle(oracle):
         exp = oracle.file_scan(data, "get", k)
         got = r.get(k)
         assert ([got] if got is not None else []) == [v for _, v in exp["records"]], k
+
+
+def _long_key_records(rng, n=40):
+    """keys of 66-200 KiB sharing long prefixes (entries carry shared of 60+ KiB), small values"""
+    base = rng.integers(0, 256, 210_000, dtype=np.uint8).tobytes()
+    keys = set()
+    while len(keys) < n:
+        kl = int(rng.integers(66_000, 200_000))
+        p = int(rng.integers(60_000, kl))
+        keys.add(base[:p] + rng.integers(0, 256, kl - p, dtype=np.uint8).tobytes())
+    return [(k, bytes([i & 0xFF]) * int(rng.integers(0, 40))) for i, k in enumerate(sorted(keys))]
+
+
+def test_keys_over_64kib(oracle):
+    """keys longer than the emitting seek's 64 KiB LDS key (mtblx_block_seek_batch reports
+    them; mtblx_block_seek_batch_kbuf carries the key in device memory): iter_from / prefix /
+    range, the stateful iterator with seeks, Reader::get, and -- with a damaged index read with
+    verification off -- the live index iterator over separators of 60+ KiB"""
+    rd = _mods()
+    rng = np.random.default_rng(64)
+    recs = _long_key_records(rng)
+    data, _ = _write(recs, 600_000, 2)          # several records per block, several blocks
+    assert _bulk_check(oracle, data, True, rng, recs) > 0
+    r = rd.Reader(data)
+    for k in _probe_keys(rng, recs, 10):
+        exp = oracle.file_scan(data, "get", k)
+        got = r.get(k)
+        assert got == (exp["records"][0][1] if exp["records"] and exp["records"][0][0] == k else None)
+    for t in range(6):
+        keys = _probe_keys(rng, recs, 6)
+        ops = [("seek", keys[int(rng.integers(0, len(keys)))]) if rng.random() < 0.5 else int(rng.choice([1, 3, 30]))
+               for _ in range(6)]
+        _script_check(oracle, data, True, "from", keys[t % len(keys)], b"", ops)
+    for kind in ("restart", "shared"):
+        bad = _corrupt_index(data, rng, kind)
+        keys = _probe_keys(rng, recs, 6)
+        ops = [("seek", keys[1]), 3, ("seek", keys[2]), 5, ("seek", keys[0]), 40]
+        _script_check(oracle, bad, False, "iter", b"", b"", ops)

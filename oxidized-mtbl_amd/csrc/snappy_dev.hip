@@ -29,6 +29,8 @@
 //    lane with aligned dword stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "mtblx.h"
 #include "mtblx_host.h"
@@ -426,6 +428,7 @@ constexpr int NCH = BUF / 16;           // 16-byte chunks of a buffer
 constexpr int NPL = (NCH + G - 1) / G;  // chunks per lane
 constexpr int WG_PER_CU = 8;
 constexpr int32_t kDefer = 0x7fffffff;  // internal status: the block goes to k_snappy_deferred
+constexpr int32_t kLanes = 0x7ffffffe;  // internal status: a compressible block, left to k_snappy_lanes
 
 struct alignas(16) Blk {
   uint8_t b[BUF + 16];   // 16 B slack: 8-byte header reads and 4-byte writes past the end
@@ -465,7 +468,8 @@ __device__ __forceinline__ uint32_t umod(uint32_t j, uint32_t off, float rcp) {
 __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, const uint64_t* src_off,
                                                         const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
                                                         const uint64_t* dst_off, const uint32_t* dst_len,
-                                                        uint32_t max_out, int32_t* status, uint32_t* dec_len) {
+                                                        uint32_t max_out, int32_t* status, uint32_t* dec_len,
+                                                        uint32_t lanes_x) {
   __shared__ Blk S[NG];
   const int lane = threadIdx.x, g = lane >> 4, l = lane & 15;
   uint8_t* base = S[g].b;
@@ -541,6 +545,7 @@ __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, cons
       if (!fits) st = kDefer;
       else if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
       else if (want > cur.cap) st = MTBLX_SNAPPY_TOO_SMALL;
+      else if (lanes_x && want > (uint64_t)lanes_x * n) st = kLanes;   // expands > lanes_x times
       else if (want > min(max_out, (uint32_t)OUT)) st = kDefer;
       W = (uint32_t)want;
     }
@@ -628,7 +633,7 @@ __global__ void __launch_bounds__(kWave) k_snappy_quads(const uint8_t* src, cons
     }
     if (on && l == 0) {
       status[b] = st;
-      if (dec_len && st != kDefer) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
+      if (dec_len && st != kDefer && st != kLanes) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
     }
     if (qn >= nquad) break;   // wave-uniform
     q = qn;
@@ -662,6 +667,220 @@ __global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, c
   }
 }
 }  // namespace quad
+
+// ---- Compressible blocks (round 3): one LANE per block, the output streamed to HBM ----
+//
+// The quad kernel is bound by blocks in flight per CU (LDS holds each block's whole output) and
+// by ~1000 cycles of dependent latency per element.  On compressible streams (~13 B per element)
+// that is 173 GB/s.  Here every lane decodes its own block with no LDS at all: the element
+// header comes from a 16-byte register window of the stored bytes, the element is written to
+// the block's HBM slot in 16-byte stores, and a copy reads its source back from the bytes this
+// lane already wrote (a thread's own stores are seen by its later loads).  Throughput is then
+// every block of the batch in flight at once, one element per memory round trip each.
+//   overlapping copies (off < 16 <= L or off < L): the first 16 bytes are the off-byte period
+//   built in registers (doubling: p |= p << 8v, v = off, 2 off, ...); chunk j >= 16 then reads
+//   the 16 bytes at j - off2, off2 = off * ceil(16 / off) in [16, 16 + off): already written (or
+//   the period's bytes before the element, which equal it).
+//   a 16-byte store past the element is overwritten by the next element before any copy can read
+//   it (copies read only produced bytes); near the end of the slot (dst_len) stores are exact.
+// Checks and statuses are the quad kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.
+namespace lanes {
+typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef unsigned __int128 u128;
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ u128 to128(const v4u x) {
+  return (u128)x.x | ((u128)x.y << 32) | ((u128)x.z << 64) | ((u128)x.w << 96);
+}
+__device__ __forceinline__ v4u from128(u128 x) {
+  return v4u{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+}
+// stored bytes [p, p + 16) of s[0, n) (zero past n): one unaligned load inside, bytes at the end
+__device__ __forceinline__ u128 ld16(const uint8_t* s, uint64_t n, uint64_t p) {
+  if (p + 16u <= n) return to128(*reinterpret_cast<const v4u*>(s + p));
+  u128 w = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (p + k < n) w |= (u128)s[p + k] << (8 * k);
+  return w;
+}
+// 16 bytes to dg[o, o + 16), or only dg[o, end) when the slot (cap bytes) ends before o + 16
+__device__ __forceinline__ void st16(uint8_t* dg, uint64_t o, u128 v, uint64_t end, uint64_t cap) {
+  if (o + 16u <= cap) {
+    *reinterpret_cast<v4u*>(dg + o) = from128(v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (o + k < end) dg[o + k] = (uint8_t)(v >> (8 * k));
+  }
+}
+
+// RING: each lane also keeps the last 256 output bytes of its block in LDS (a ring of 64 words,
+// word k of lane t at ring[k][t]: one bank per lane, conflict-free), so a copy whose offset is at
+// most kRingOff reads its source from LDS instead of re-reading HBM bytes this lane just stored
+// (a store -> load round trip through the L2 per element).  Words are appended whole: the
+// output's last partial word is kept in a register (`carry`) and merged into the next append.
+constexpr int kRingWords = 64;
+constexpr uint32_t kRingOff = 240;
+
+__device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t r) {   // ((hi:lo) >> 8r), r < 4
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r));
+}
+// append cnt (1..16) bytes of v at output position d
+__device__ __forceinline__ void ring_put(uint32_t (*R)[kThreads], int t, uint32_t& carry, uint64_t d, u128 v, uint32_t cnt) {
+  const uint32_t r = (uint32_t)d & 3u, q = (uint32_t)(d >> 2);
+  const uint32_t v0 = (uint32_t)v, v1 = (uint32_t)(v >> 32), v2 = (uint32_t)(v >> 64), v3 = (uint32_t)(v >> 96);
+  uint32_t w[5];
+  w[0] = (carry & ((1u << (8 * r)) - 1u)) | (v0 << (8 * r));
+  w[1] = alignb(v1, v0, 4u - r);
+  w[2] = alignb(v2, v1, 4u - r);
+  w[3] = alignb(v3, v2, 4u - r);
+  w[4] = r ? v3 >> (32u - 8u * r) : 0u;
+  if (r == 0u) {
+    w[1] = v1;
+    w[2] = v2;
+    w[3] = v3;
+  }
+  const uint32_t e = r + cnt, nw = (e + 3u) >> 2;
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if ((uint32_t)k < nw) R[(q + k) & (kRingWords - 1)][t] = w[k];
+  const uint32_t c = e >> 2;
+  carry = c == 0u ? w[0] : c == 1u ? w[1] : c == 2u ? w[2] : c == 3u ? w[3] : w[4];
+}
+// output bytes [x, x + 16) (x >= d - 255; bytes at or past d are whatever the ring holds)
+__device__ __forceinline__ u128 ring_get(const uint32_t (*R)[kThreads], int t, uint64_t x) {
+  const uint32_t r = (uint32_t)x & 3u, q = (uint32_t)(x >> 2);
+  uint32_t w[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) w[k] = R[(q + k) & (kRingWords - 1)][t];
+  return (u128)alignb(w[1], w[0], r) | ((u128)alignb(w[2], w[1], r) << 32) | ((u128)alignb(w[3], w[2], r) << 64) |
+         ((u128)alignb(w[4], w[3], r) << 96);
+}
+
+template <bool RING>
+__global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, const uint64_t* src_off,
+                                                           const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                           const uint64_t* dst_off, const uint32_t* dst_len,
+                                                           int32_t* status, uint32_t* dec_len, int only_marked) {
+  __shared__ uint32_t ring[RING ? kRingWords : 1][kThreads];
+  const int t = threadIdx.x;
+  const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
+  if (b >= nblk) return;
+  if (only_marked && status[b] != quad::kLanes) return;
+  const uint8_t* s = src + src_off[b];
+  const uint64_t n = src_len[b];
+  uint8_t* dg = dst + dst_off[b];
+  const uint64_t cap = dst_len[b];
+  // preamble
+  uint64_t want = 0, pos = 0;
+  bool term = false;
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+    const uint32_t byte = s[i];
+    want |= (uint64_t)(byte & 0x7fu) << (7 * i);
+    if (!(byte & 0x80u)) {
+      term = true;
+      pos = i + 1;
+      break;
+    }
+  }
+  int32_t st = MTBLX_SNAPPY_OK;
+  if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * n) st = MTBLX_SNAPPY_CORRUPT;
+  else if (want > cap) st = MTBLX_SNAPPY_TOO_SMALL;
+  const uint64_t W = st == MTBLX_SNAPPY_OK ? want : 0;
+  uint64_t d = 0;
+  uint32_t carry = 0;
+  u128 win = 0;
+  uint64_t wp = ~0ull;   // stream position of the window's byte 0 (none yet)
+  while (st == MTBLX_SNAPPY_OK && pos < n) {
+    if (wp == ~0ull || pos + 5u > wp + 16u) {   // tag + up to 4 bytes must be in the window
+      win = ld16(s, n, pos);
+      wp = pos;
+    }
+    const uint64_t h = (uint64_t)(win >> (8 * (uint32_t)(pos - wp)));
+    const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+    const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2;
+    const uint64_t avail = n - pos - 1u;
+    const uint32_t raw = (lo >> 8) | (hi << 24);   // the 4 bytes after the tag
+    const bool lg = t2 >= 60u;
+    const uint32_t nb = t2 - 59u;
+    const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * (nb & 3u))) - 1u);
+    const uint64_t llit = lg ? (uint64_t)ext + 1u : t2 + 1u, hlit = lg ? 1u + nb : 1u;
+    const bool lbad = lg && (avail < nb || ext == 0xFFFFFFFFu);
+    const uint32_t lc = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
+    const uint32_t off = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
+    const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
+    const bool lit = kind == 0u;
+    const uint64_t L = lit ? llit : lc, sp = pos + (lit ? hlit : need + 1u);
+    bool bad = lit ? (lbad || n - sp < L) : (avail < need || off == 0u || off > d);
+    bad = bad || W - d < L;
+    if (bad) {
+      st = MTBLX_SNAPPY_CORRUPT;
+      break;
+    }
+    const uint64_t end = d + L;
+    const bool rg = RING && !lit && off <= kRingOff;   // the source from the LDS ring
+    // The first 16 bytes: ONE load for every element kind, so the lanes of a wave (different
+    // blocks, different element kinds) do not serialise one memory round trip per kind.
+    const bool ov = !lit && off < 16u && off < L;   // overlapping short copy: the off-byte period
+    u128 v0;
+    if (rg) v0 = ring_get(ring, t, d - off);
+    else if (lit && sp + 16u > n) v0 = ld16(s, n, sp);   // the last stored bytes (once per block)
+    else v0 = to128(*reinterpret_cast<const v4u*>(lit ? s + sp : dg + d - off));
+    if (ov) {
+      v0 &= ((u128)1 << (8 * off)) - 1;
+      uint32_t v = off;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (v < 16u) v0 |= v0 << (8 * v);
+        v = v < 16u ? 2u * v : v;
+      }
+    }
+    st16(dg, d, v0, end, cap);
+    if (RING) ring_put(ring, t, carry, d, v0, L < 16u ? (uint32_t)L : 16u);
+    if (lit) {   // the stored bytes after a short literal hold the next header
+      win = v0;
+      wp = sp;
+    }
+    if (L > 16u) {
+      if (!RING && (lit || off >= L || off >= 64u)) {
+        // sources independent of this element's stores: four 16-byte loads in flight per step
+        const uint8_t* cs = dg + d - off;
+        for (uint64_t j = 16; j < L; j += 64) {
+          u128 v[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint64_t q = j + 16u * k;
+            v[k] = 0;
+            if (q < L) v[k] = lit ? ld16(s, n, sp + q) : to128(*reinterpret_cast<const v4u*>(cs + q));
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (j + 16u * k < L) st16(dg, d + j + 16u * k, v[k], end, cap);
+        }
+      } else {
+        // chunk j reads [d + j - off2, +16), all before d + j: written by chunk j - 16 or earlier,
+        // or (overlapping copies, off2 = off * ceil(16 / off) < 16 + off) the period's bytes
+        // before the element, which equal it
+        const uint32_t off2 = ov ? off * ((16u + off - 1u) / off) : off;
+        for (uint64_t j = 16; j < L; j += 16) {
+          u128 v;
+          if (lit) v = ld16(s, n, sp + j);
+          else if (rg) v = ring_get(ring, t, d + j - off2);
+          else v = to128(*reinterpret_cast<const v4u*>(dg + d + j - off2));
+          st16(dg, d + j, v, end, cap);
+          if (RING) ring_put(ring, t, carry, d + j, v, L - j < 16u ? (uint32_t)(L - j) : 16u);
+        }
+      }
+    }
+    pos = lit ? sp + L : sp;
+    d = end;
+  }
+  if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
+  status[b] = st;
+  if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? (uint32_t)W : 0u;
+}
+}  // namespace lanes
 
 // ---- directory: preamble lengths, 16-byte aligned exclusive prefix ----
 constexpr int kDirThreads = 256, kDirPer = 8, kDirSpan = kDirThreads * kDirPer;
@@ -802,10 +1021,25 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   if (nblk == 0) return MTBLX_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !dst_len || !status) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
+  // MTBLX_SNAPPY_KERNEL (read once): "auto" (default: blocks expanding > 2x go to
+  // k_snappy_lanes, the rest to the quad / one-wave kernels), "lanes" (every block), "quads"
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("MTBLX_SNAPPY_KERNEL");
+    mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "lanesg")) ? 3 : (e && !strcmp(e, "quads")) ? 1 : 0;
+  }
+  const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(lanes::kThreads);
+  if (mode == 2 || mode == 3) {
+    hipLaunchKernelGGL(mode == 2 ? lanes::k_snappy_lanes<true> : lanes::k_snappy_lanes<false>, glanes, tlanes, 0, s, src,
+                       src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len, 0);
+  } else if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
+    const uint32_t lanes_x = mode == 0 ? 2u : 0u;
     hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
-                       dec_len);
+                       dec_len, lanes_x);
+    if (lanes_x)
+      hipLaunchKernelGGL(lanes::k_snappy_lanes<true>, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
+                         dst_len, status, dec_len, 1);
     hipLaunchKernelGGL(quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
                        src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   } else {

@@ -1,6 +1,7 @@
-"""A/B of the CRC-32C kernels (MTBLX_CRC_KERNEL 0 / 1 / 2) over the cfg2 bench batch: each
-variant in its own child process (the choice is read once per process), HIP events around
-50 launches after a 40 ms preload, two alternations; also decode + verify (two launches)."""
+"""Timing of the CRC-32C kernel over the cfg2 bench batch: each run in its own child process
+(argv names runs; MTBLX_CRC_KERNEL is passed through for A/B builds), HIP events around 50
+launches after a 200 ms preload, two alternations; also decode + verify (two launches).
+Round 3 measured kernels 0-7 with it (profiles/r03/crc_ab.txt); only kernel 0 remains."""
 import json
 import os
 import subprocess

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--compressible", action="store_true", help="cfg1-style repeated values instead")
+    ap.add_argument("--tile", type=int, default=1, help="the generated file's blocks this many times over")
     a = ap.parse_args()
     t0 = time.time()
     w = Writer(4096, 16, 1)
@@ -36,6 +37,10 @@ def main():
                        np.arange(1, n + 1, dtype=np.uint64) * np.uint64(vl))
         z = w.into_inner_np()
     zoff, zln = w.block_dir
+    if a.tile > 1:   # bench.py compressible_snappy's 100 000-block batch: the file tiled
+        zoff = np.concatenate([zoff.astype(np.uint64) + np.uint64(i * z.size) for i in range(a.tile)])
+        zln = np.tile(zln, a.tile)
+        z = np.tile(z, a.tile)
     print(f"generated {zoff.size} blocks, {int(zln.sum()) / 2**20:.1f} MiB stored in {time.time() - t0:.1f}s",
           flush=True)
     zb = codec.SnappyBatch.from_host(z, zoff, zln)

@@ -152,3 +152,39 @@ def test_cfg3_roundtrip_sample(oracle):
         rr = [(keys[(ke_h[r - 1] if r else 0): ke_h[r]].tobytes(), vals[(ve_h[r - 1] if r else 0): ve_h[r]].tobytes())
               for r in range(r0, r1)]
         assert ho[bo[j]: bo[j] + bl[j]].tobytes() == oracle.build_block(rr, 16)
+
+
+def test_block_shapes_vs_writer(oracle):
+    """k_encode at the edges of its paths: ~1000 and > 1024 entries per 64 KiB block, blocks
+    over the LDS buffer (assembled in place in HBM), lengths around 76 KiB, interval-1 blocks
+    of tiny entries, entry edges at every phase of 16 bytes -- byte for byte against the
+    product Writer; the oracle reads every block back."""
+    enc = _enc()
+    rng = np.random.default_rng(64)
+    cases = [
+        (65536, 16, 9000, 0, 4, 0, 4),          # ~6 B entries: > 1024 per 64 KiB block
+        (65536, 16, 3000, 0, 12, 0, 60),        # ~1000 entries per block: straddles the limit
+        (131072, 4, 300, 0, 40, 0, 1500),       # 128 KiB blocks: in place in HBM
+        (77000, 16, 400, 1, 30, 0, 900),        # block lengths around 76 KiB
+        (1024, 1, 500, 0, 3, 0, 2),             # every entry a restart, blocks far under 16 B chunks
+        (4096, 16, 2000, 0, 17, 15, 17),        # entry edges at every phase of the 16-byte chunks
+    ]
+    for bs, iv, n, kmin, kmax, vmin, vmax in cases:
+        recs = corpus.random_records(rng, n, kmin, kmax, vmin, vmax)
+        data, off, ln, nrec = _writer_file(recs, bs, iv)
+        d = enc.DeviceRecords.from_list(recs)
+        e = enc.encode_blocks(d, enc.plan(d, bs, iv), iv, framed=True)
+        total = int(e.totals[0].item())
+        assert int(e.totals[1].item()) == 0 and (e.status.cpu().numpy() == 0).all(), (bs, iv)
+        idx_off = int(np.frombuffer(data[-512:-504], np.uint64)[0])
+        assert total == idx_off, (bs, iv)
+        assert e.out[:total].cpu().numpy().tobytes() == data[:idx_off], (bs, iv)
+        orc = oracle.decode_blocks(e.out[:total].cpu().numpy(), off, ln)
+        assert (orc.status == 0).all() and int(orc.nrec.sum()) == n
+    # single records: empty key and value (the smallest block), one byte each
+    for recs in ([(b"", b"")], [(b"k", b"v")], [(b"", b"x" * 70000)]):
+        d = enc.DeviceRecords.from_list(recs)
+        data, off, ln, _ = _writer_file(recs, 4096, 16)
+        e = enc.encode_blocks(d, enc.plan(d, 4096, 16), 16, framed=True)
+        total = int(e.totals[0].item())
+        assert e.out[:total].cpu().numpy().tobytes() == data[:total]

@@ -57,14 +57,6 @@ __device__ __forceinline__ uint32_t vlen64(uint64_t v) {
   while (v >= 128) { v >>= 7; ++n; }
   return n;
 }
-// varint_encode32 / varint_encode64 (src/varint.rs:12-42, :63-76): LEB128
-__device__ __forceinline__ uint32_t venc(uint8_t* p, uint64_t v) {
-  uint32_t i = 0;
-  while (v >= 128) { p[i++] = (uint8_t)(v | 128); v >>= 7; }
-  p[i++] = (uint8_t)v;
-  return i;
-}
-
 struct Recs {
   const uint8_t* keys;
   const uint64_t* key_end;
@@ -375,13 +367,35 @@ __device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, 
   return e;
 }
 
-// write entry e at dst (header varints, key suffix, value): src/block_builder.rs:69-77
+// varint32 bytes of v packed little-endian in a register (<= 5 bytes), *len = their count
+// (src/varint.rs:12-42)
+__device__ __forceinline__ uint64_t vpack(uint64_t v, uint32_t& len) {
+  uint64_t w = 0;
+  uint32_t i = 0;
+  while (v >= 128) {
+    w |= ((v & 127u) | 128u) << (8 * i);
+    v >>= 7;
+    ++i;
+  }
+  len = i + 1;
+  return w | (v << (8 * i));
+}
+
+// write entry e at dst (header varints, key suffix, value): src/block_builder.rs:69-77.  The
+// header bytes are computed in registers (byte k of varint32(v): 7 bits of v, continuation bit
+// unless last): a byte array here was dynamically indexed, i.e. lived in scratch.
+__device__ __forceinline__ void put_varint(uint8_t* p, uint32_t v, uint32_t len) {
+#pragma unroll
+  for (uint32_t k = 0; k < 5; ++k)
+    if (k < len) p[k] = (uint8_t)(((v >> (7 * k)) & 0x7fu) | (k + 1 < len ? 0x80u : 0u));
+}
 __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent& e) {
-  uint8_t h[15];
-  uint32_t n = venc(h, e.sh);
-  n += venc(h + n, e.kl - e.sh);
-  n += venc(h + n, e.vl);
-  for (uint32_t k = 0; k < n; ++k) dst[k] = h[k];
+  const uint32_t sh = (uint32_t)e.sh, ks = (uint32_t)(e.kl - e.sh), vl = (uint32_t)e.vl;   // < 4 GiB (k_plan)
+  const uint32_t l0 = vlen32(sh), l1 = vlen32(ks), l2 = vlen32(vl);
+  put_varint(dst, sh, l0);
+  put_varint(dst + l0, ks, l1);
+  put_varint(dst + l0 + l1, vl, l2);
+  const uint32_t n = l0 + l1 + l2;
   copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys);
   copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl, R.vals);
 }
@@ -528,9 +542,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       const uint32_t crc = wg_crc32c(S, src, L);
       ESTAMP(6);   // CRC-32C
       if (tid == 0) {
-        uint8_t h[10];
-        const uint32_t hl = venc(h, L);
-        for (uint32_t k = 0; k < hl; ++k) a.out[pre + k] = h[k];
+        uint32_t hl;   // varint64(L) | crc32c (write_block, src/writer.rs:203-237)
+        const uint64_t hw = vpack(L, hl);   // L < 2^35: 5 bytes at most
+#pragma unroll
+        for (uint32_t k = 0; k < 5; ++k)
+          if (k < hl) a.out[pre + k] = (uint8_t)(hw >> (8 * k));
         put32(a.out + pre + hl, crc);
       }
     }

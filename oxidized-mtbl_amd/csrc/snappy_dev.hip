@@ -671,76 +671,70 @@ __global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, c
 // ---- Compressible blocks (round 3): one LANE per block, the output streamed to HBM ----
 //
 // The quad kernel is bound by blocks in flight per CU (LDS holds each block's whole output) and
-// by ~1000 cycles of dependent latency per element.  On compressible streams (~13 B per element)
-// that is 173 GB/s.  Here every lane decodes its own block with no LDS at all: the element
-// header comes from a 16-byte register window of the stored bytes, the element is written to
-// the block's HBM slot in 16-byte stores, and a copy reads its source back from the bytes this
-// lane already wrote (a thread's own stores are seen by its later loads).  Throughput is then
-// every block of the batch in flight at once, one element per memory round trip each.
-//   overlapping copies (off < 16 <= L or off < L): the first 16 bytes are the off-byte period
-//   built in registers (doubling: p |= p << 8v, v = off, 2 off, ...); chunk j >= 16 then reads
-//   the 16 bytes at j - off2, off2 = off * ceil(16 / off) in [16, 16 + off): already written (or
-//   the period's bytes before the element, which equal it).
-//   a 16-byte store past the element is overwritten by the next element before any copy can read
-//   it (copies read only produced bytes); near the end of the slot (dst_len) stores are exact.
-// Checks and statuses are the quad kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.
+// by ~1000 cycles of dependent latency per element: on compressible streams (~13 B per element)
+// that is 172 GB/s over 100 000 blocks.  Here every lane decodes its own block, so one vector
+// instruction advances 64 blocks and every block of the batch is in flight at once:
+//  - the element header comes from a 32-byte register window of the stored bytes, advanced 16
+//    bytes at a time with the next 16 loaded ahead;
+//  - every element's bytes go to the block's HBM slot in 16-byte stores, and into a 256-byte
+//    per-lane ring in LDS (64 words, word k of lane t at ring[k][t]: one bank per lane), from
+//    which copies with offsets up to kRingOff read their source -- no store -> load round trip
+//    through the L2 per element; longer offsets re-read the slot in HBM (a thread sees its own
+//    stores);
+//  - an overlapping copy (off < 16, off < L) starts with the off-byte period built by two byte
+//    permutes per word from a per-offset selector table; its chunk j >= 16 then reads the 16
+//    bytes at j - off2, off2 = off * ceil(16 / off) in [16, 16 + off): bytes already written, or
+//    the period's bytes before the element, which equal it;
+//  - a 16-byte store past the element is overwritten by the next element before any copy can
+//    read it (copies read produced bytes only); at the end of the slot (dst_len) stores are exact.
+// All state is 32-bit (a block and its output are < 4 GiB).  Checks and statuses are the quad
+// kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.
 namespace lanes {
 typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
-typedef unsigned __int128 u128;
 constexpr int kThreads = 256;
-
-__device__ __forceinline__ u128 to128(const v4u x) {
-  return (u128)x.x | ((u128)x.y << 32) | ((u128)x.z << 64) | ((u128)x.w << 96);
-}
-__device__ __forceinline__ v4u from128(u128 x) {
-  return v4u{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
-}
-// stored bytes [p, p + 16) of s[0, n) (zero past n): one unaligned load inside, bytes at the end
-__device__ __forceinline__ u128 ld16(const uint8_t* s, uint64_t n, uint64_t p) {
-  if (p + 16u <= n) return to128(*reinterpret_cast<const v4u*>(s + p));
-  u128 w = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k)
-    if (p + k < n) w |= (u128)s[p + k] << (8 * k);
-  return w;
-}
-// 16 bytes to dg[o, o + 16), or only dg[o, end) when the slot (cap bytes) ends before o + 16
-__device__ __forceinline__ void st16(uint8_t* dg, uint64_t o, u128 v, uint64_t end, uint64_t cap) {
-  if (o + 16u <= cap) {
-    *reinterpret_cast<v4u*>(dg + o) = from128(v);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (o + k < end) dg[o + k] = (uint8_t)(v >> (8 * k));
-  }
-}
-
-// RING: each lane also keeps the last 256 output bytes of its block in LDS (a ring of 64 words,
-// word k of lane t at ring[k][t]: one bank per lane, conflict-free), so a copy whose offset is at
-// most kRingOff reads its source from LDS instead of re-reading HBM bytes this lane just stored
-// (a store -> load round trip through the L2 per element).  Words are appended whole: the
-// output's last partial word is kept in a register (`carry`) and merged into the next append.
 constexpr int kRingWords = 64;
 constexpr uint32_t kRingOff = 240;
 
+struct Q4 {
+  uint32_t w[4];
+};
+__device__ __forceinline__ Q4 q4(const v4u x) { return Q4{{x.x, x.y, x.z, x.w}}; }
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t r) {   // ((hi:lo) >> 8r), r < 4
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r));
+  return __builtin_amdgcn_alignbyte(hi, lo, r);
 }
-// append cnt (1..16) bytes of v at output position d
-__device__ __forceinline__ void ring_put(uint32_t (*R)[kThreads], int t, uint32_t& carry, uint64_t d, u128 v, uint32_t cnt) {
-  const uint32_t r = (uint32_t)d & 3u, q = (uint32_t)(d >> 2);
-  const uint32_t v0 = (uint32_t)v, v1 = (uint32_t)(v >> 32), v2 = (uint32_t)(v >> 64), v3 = (uint32_t)(v >> 96);
-  uint32_t w[5];
-  w[0] = (carry & ((1u << (8 * r)) - 1u)) | (v0 << (8 * r));
-  w[1] = alignb(v1, v0, 4u - r);
-  w[2] = alignb(v2, v1, 4u - r);
-  w[3] = alignb(v3, v2, 4u - r);
-  w[4] = r ? v3 >> (32u - 8u * r) : 0u;
-  if (r == 0u) {
-    w[1] = v1;
-    w[2] = v2;
-    w[3] = v3;
+// stored bytes [p, p + 16) of s[0, n) (zero past n): one unaligned load inside, bytes at the end
+__device__ __forceinline__ Q4 ld16(const uint8_t* s, uint32_t n, uint32_t p) {
+  if ((uint64_t)p + 16u <= n) return q4(*reinterpret_cast<const v4u*>(s + p));
+  Q4 q{{0u, 0u, 0u, 0u}};
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if ((uint64_t)p + k < n) q.w[k >> 2] |= (uint32_t)s[p + k] << (8 * (k & 3));
+  return q;
+}
+// 16 bytes to dg[o, o + 16), or only dg[o, end) when the slot (cap bytes) ends before o + 16
+__device__ __forceinline__ void st16(uint8_t* dg, uint32_t o, const Q4& v, uint32_t end, uint32_t cap) {
+#ifdef MTBLX_SNAP_ABL_NOSTORE   // timing ablation only (wrong output): no HBM stores
+  return;
+#endif
+  if ((uint64_t)o + 16u <= cap) {
+    *reinterpret_cast<v4u*>(dg + o) = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if ((uint64_t)o + k < end) dg[o + k] = (uint8_t)(v.w[k >> 2] >> (8 * (k & 3)));
   }
+}
+// ring: append cnt (1..16) bytes of v at output position d (the output's last partial word is
+// `carry`, merged into the first word written)
+__device__ __forceinline__ void ring_put(uint32_t (*R)[kThreads], int t, uint32_t& carry, uint32_t d, const Q4& v,
+                                         uint32_t cnt) {
+  const uint32_t r = d & 3u, q = d >> 2;
+  uint32_t w[5];
+  w[0] = (carry & ((1u << (8 * r)) - 1u)) | (v.w[0] << (8 * r));
+  w[1] = r ? alignb(v.w[1], v.w[0], 4u - r) : v.w[1];
+  w[2] = r ? alignb(v.w[2], v.w[1], 4u - r) : v.w[2];
+  w[3] = r ? alignb(v.w[3], v.w[2], 4u - r) : v.w[3];
+  w[4] = r ? v.w[3] >> (32u - 8u * r) : 0u;
   const uint32_t e = r + cnt, nw = (e + 3u) >> 2;
 #pragma unroll
   for (int k = 0; k < 5; ++k)
@@ -748,32 +742,50 @@ __device__ __forceinline__ void ring_put(uint32_t (*R)[kThreads], int t, uint32_
   const uint32_t c = e >> 2;
   carry = c == 0u ? w[0] : c == 1u ? w[1] : c == 2u ? w[2] : c == 3u ? w[3] : w[4];
 }
-// output bytes [x, x + 16) (x >= d - 255; bytes at or past d are whatever the ring holds)
-__device__ __forceinline__ u128 ring_get(const uint32_t (*R)[kThreads], int t, uint64_t x) {
-  const uint32_t r = (uint32_t)x & 3u, q = (uint32_t)(x >> 2);
+// ring: output bytes [x, x + 16) (x >= d - 255; bytes at or past d are whatever the ring holds)
+__device__ __forceinline__ Q4 ring_get(const uint32_t (*R)[kThreads], int t, uint32_t x) {
+  const uint32_t r = x & 3u, q = x >> 2;
   uint32_t w[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) w[k] = R[(q + k) & (kRingWords - 1)][t];
-  return (u128)alignb(w[1], w[0], r) | ((u128)alignb(w[2], w[1], r) << 32) | ((u128)alignb(w[3], w[2], r) << 64) |
-         ((u128)alignb(w[4], w[3], r) << 96);
+  return Q4{{alignb(w[1], w[0], r), alignb(w[2], w[1], r), alignb(w[3], w[2], r), alignb(w[4], w[3], r)}};
 }
 
-template <bool RING>
 __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, const uint64_t* src_off,
                                                            const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
                                                            const uint64_t* dst_off, const uint32_t* dst_len,
                                                            int32_t* status, uint32_t* dec_len, int only_marked) {
-  __shared__ uint32_t ring[RING ? kRingWords : 1][kThreads];
+  __shared__ uint32_t ring[kRingWords][kThreads];
+  // period selectors: for offset o < 16 and output word i, byte j = source byte (4 i + j) mod o:
+  // psel[o][i] = {v_perm selector over source bytes 0..7, over bytes 8..15, mask of the latter}
+  __shared__ uint32_t psel[16][4][3];
   const int t = threadIdx.x;
+  if (t < 64) {
+    const uint32_t o = (uint32_t)t >> 2, i = (uint32_t)t & 3u;
+    uint32_t lo = 0, hi = 0, mk = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t m = o ? (4u * i + j) % o : 0u;
+      if (m < 8u) lo |= m << (8 * j);
+      else {
+        hi |= (m - 8u) << (8 * j);
+        mk |= 0xFFu << (8 * j);
+      }
+    }
+    psel[o][i][0] = lo;
+    psel[o][i][1] = hi;
+    psel[o][i][2] = mk;
+  }
+  __syncthreads();
   const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
   if (b >= nblk) return;
   if (only_marked && status[b] != quad::kLanes) return;
   const uint8_t* s = src + src_off[b];
-  const uint64_t n = src_len[b];
+  const uint32_t n = src_len[b];
   uint8_t* dg = dst + dst_off[b];
-  const uint64_t cap = dst_len[b];
+  const uint32_t cap = dst_len[b];
   // preamble
-  uint64_t want = 0, pos = 0;
+  uint64_t want = 0;
+  uint32_t pos = 0;
   bool term = false;
   for (uint32_t i = 0; i < 5 && i < n; ++i) {
     const uint32_t byte = s[i];
@@ -785,92 +797,78 @@ __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, c
     }
   }
   int32_t st = MTBLX_SNAPPY_OK;
-  if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * n) st = MTBLX_SNAPPY_CORRUPT;
+  if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
   else if (want > cap) st = MTBLX_SNAPPY_TOO_SMALL;
-  const uint64_t W = st == MTBLX_SNAPPY_OK ? want : 0;
-  uint64_t d = 0;
-  uint32_t carry = 0;
-  u128 win = 0;
-  uint64_t wp = ~0ull;   // stream position of the window's byte 0 (none yet)
+  const uint32_t W = st == MTBLX_SNAPPY_OK ? (uint32_t)want : 0u;
+  uint32_t d = 0, carry = 0;
+  // the window: stored bytes [wp, wp + 32) in w[0..7]; w[4..7] may still be in flight
+  uint32_t wp = pos;
+  Q4 lo4 = ld16(s, n, wp), hi4 = ld16(s, n, wp + 16u);
   while (st == MTBLX_SNAPPY_OK && pos < n) {
-    if (wp == ~0ull || pos + 5u > wp + 16u) {   // tag + up to 4 bytes must be in the window
-      win = ld16(s, n, pos);
-      wp = pos;
+    if (pos - wp >= 16u) {
+      if (pos - wp < 32u) {   // advance 16 bytes, load the next 16 ahead
+        lo4 = hi4;
+        wp += 16u;
+        hi4 = ld16(s, n, wp + 16u);
+      } else {                // a long literal jumped past the window
+        wp = pos;
+        lo4 = ld16(s, n, wp);
+        hi4 = ld16(s, n, wp + 16u);
+      }
     }
-    const uint64_t h = (uint64_t)(win >> (8 * (uint32_t)(pos - wp)));
-    const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+    const uint32_t k = pos - wp, kq = k >> 2, kr = k & 3u;   // tag + 4 bytes at window byte k < 16
+    uint32_t a = lo4.w[0], bb = lo4.w[1], c = lo4.w[2];
+    if (kq == 1u) { a = lo4.w[1]; bb = lo4.w[2]; c = lo4.w[3]; }
+    if (kq == 2u) { a = lo4.w[2]; bb = lo4.w[3]; c = hi4.w[0]; }
+    if (kq == 3u) { a = lo4.w[3]; bb = hi4.w[0]; c = hi4.w[1]; }
+    const uint32_t lo = alignb(bb, a, kr), hi = alignb(c, bb, kr);
     const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2;
-    const uint64_t avail = n - pos - 1u;
-    const uint32_t raw = (lo >> 8) | (hi << 24);   // the 4 bytes after the tag
+    const uint32_t avail = n - pos - 1u;
+    const uint32_t raw = alignb(hi, lo, 1u);   // the 4 bytes after the tag
     const bool lg = t2 >= 60u;
     const uint32_t nb = t2 - 59u;
     const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * (nb & 3u))) - 1u);
-    const uint64_t llit = lg ? (uint64_t)ext + 1u : t2 + 1u, hlit = lg ? 1u + nb : 1u;
-    const bool lbad = lg && (avail < nb || ext == 0xFFFFFFFFu);
     const uint32_t lc = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
     const uint32_t off = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
     const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
     const bool lit = kind == 0u;
-    const uint64_t L = lit ? llit : lc, sp = pos + (lit ? hlit : need + 1u);
-    bool bad = lit ? (lbad || n - sp < L) : (avail < need || off == 0u || off > d);
+    const uint32_t L = lit ? (lg ? ext + 1u : t2 + 1u) : lc;   // ext + 1 wraps only when ext == ~0: bad below
+    const uint32_t sp = pos + (lit ? (lg ? 1u + nb : 1u) : need + 1u);
+    bool bad = lit ? ((lg && (avail < nb || ext == 0xFFFFFFFFu)) || n - sp < L) : (avail < need || off == 0u || off > d);
     bad = bad || W - d < L;
     if (bad) {
       st = MTBLX_SNAPPY_CORRUPT;
       break;
     }
-    const uint64_t end = d + L;
-    const bool rg = RING && !lit && off <= kRingOff;   // the source from the LDS ring
-    // The first 16 bytes: ONE load for every element kind, so the lanes of a wave (different
-    // blocks, different element kinds) do not serialise one memory round trip per kind.
-    const bool ov = !lit && off < 16u && off < L;   // overlapping short copy: the off-byte period
-    u128 v0;
-    if (rg) v0 = ring_get(ring, t, d - off);
-    else if (lit && sp + 16u > n) v0 = ld16(s, n, sp);   // the last stored bytes (once per block)
-    else v0 = to128(*reinterpret_cast<const v4u*>(lit ? s + sp : dg + d - off));
+    const uint32_t end = d + L;
+    const bool rg = !lit && off <= kRingOff;           // copy source in the LDS ring
+    const bool ov = !lit && off < 16u && off < L;      // overlapping short copy: the period
+    Q4 v;
+    if (rg) v = ring_get(ring, t, d - off);
+    else v = lit ? ld16(s, n, sp) : q4(*reinterpret_cast<const v4u*>(dg + d - off));
     if (ov) {
-      v0 &= ((u128)1 << (8 * off)) - 1;
-      uint32_t v = off;
+      const uint32_t o = off;
+      Q4 p;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (v < 16u) v0 |= v0 << (8 * v);
-        v = v < 16u ? 2u * v : v;
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t pl = __builtin_amdgcn_perm(v.w[1], v.w[0], psel[o][i][0]);
+        const uint32_t ph = __builtin_amdgcn_perm(v.w[3], v.w[2], psel[o][i][1]);
+        const uint32_t mk = psel[o][i][2];
+        p.w[i] = (pl & ~mk) | (ph & mk);
       }
+      v = p;
     }
-    st16(dg, d, v0, end, cap);
-    if (RING) ring_put(ring, t, carry, d, v0, L < 16u ? (uint32_t)L : 16u);
-    if (lit) {   // the stored bytes after a short literal hold the next header
-      win = v0;
-      wp = sp;
-    }
+    st16(dg, d, v, end, cap);
+    ring_put(ring, t, carry, d, v, L < 16u ? L : 16u);
     if (L > 16u) {
-      if (!RING && (lit || off >= L || off >= 64u)) {
-        // sources independent of this element's stores: four 16-byte loads in flight per step
-        const uint8_t* cs = dg + d - off;
-        for (uint64_t j = 16; j < L; j += 64) {
-          u128 v[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint64_t q = j + 16u * k;
-            v[k] = 0;
-            if (q < L) v[k] = lit ? ld16(s, n, sp + q) : to128(*reinterpret_cast<const v4u*>(cs + q));
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (j + 16u * k < L) st16(dg, d + j + 16u * k, v[k], end, cap);
-        }
-      } else {
-        // chunk j reads [d + j - off2, +16), all before d + j: written by chunk j - 16 or earlier,
-        // or (overlapping copies, off2 = off * ceil(16 / off) < 16 + off) the period's bytes
-        // before the element, which equal it
-        const uint32_t off2 = ov ? off * ((16u + off - 1u) / off) : off;
-        for (uint64_t j = 16; j < L; j += 16) {
-          u128 v;
-          if (lit) v = ld16(s, n, sp + j);
-          else if (rg) v = ring_get(ring, t, d + j - off2);
-          else v = to128(*reinterpret_cast<const v4u*>(dg + d + j - off2));
-          st16(dg, d + j, v, end, cap);
-          if (RING) ring_put(ring, t, carry, d + j, v, L - j < 16u ? (uint32_t)(L - j) : 16u);
-        }
+      const uint32_t off2 = ov ? off * ((16u + off - 1u) / off) : off;
+      for (uint32_t j = 16; j < L; j += 16) {
+        Q4 x;
+        if (lit) x = ld16(s, n, sp + j);
+        else if (rg) x = ring_get(ring, t, d + j - off2);
+        else x = q4(*reinterpret_cast<const v4u*>(dg + d + j - off2));
+        st16(dg, d + j, x, end, cap);
+        ring_put(ring, t, carry, d + j, x, L - j < 16u ? L - j : 16u);
       }
     }
     pos = lit ? sp + L : sp;
@@ -878,7 +876,7 @@ __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, c
   }
   if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
   status[b] = st;
-  if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? (uint32_t)W : 0u;
+  if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
 }
 }  // namespace lanes
 
@@ -1026,19 +1024,19 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("MTBLX_SNAPPY_KERNEL");
-    mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "lanesg")) ? 3 : (e && !strcmp(e, "quads")) ? 1 : 0;
+    mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : 0;
   }
   const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(lanes::kThreads);
-  if (mode == 2 || mode == 3) {
-    hipLaunchKernelGGL(mode == 2 ? lanes::k_snappy_lanes<true> : lanes::k_snappy_lanes<false>, glanes, tlanes, 0, s, src,
-                       src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len, 0);
+  if (mode == 2) {
+    hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
+                       status, dec_len, 0);
   } else if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
     const uint32_t lanes_x = mode == 0 ? 2u : 0u;
     hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len, lanes_x);
     if (lanes_x)
-      hipLaunchKernelGGL(lanes::k_snappy_lanes<true>, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
+      hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
                          dst_len, status, dec_len, 1);
     hipLaunchKernelGGL(quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
                        src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);

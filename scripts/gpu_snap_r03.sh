@@ -18,8 +18,8 @@ step() {  # name timeout cmd...
 T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
 step t_auto 400 $T tests/test_snappy_gpu.py tests/test_pipe_gpu.py
 step t_lanes 400 env MTBLX_SNAPPY_KERNEL=lanes $T tests/test_snappy_gpu.py
-step t_lanesg 400 env MTBLX_SNAPPY_KERNEL=lanesg $T tests/test_snappy_gpu.py
-for m in ${MODES:-quads lanes lanesg auto}; do
+
+for m in ${MODES:-quads lanes auto}; do
   step p_comp_$m 300 env MTBLX_SNAPPY_KERNEL=$m python scripts/snappy_probe.py --compressible --blocks 100000 --tile 4
   step p_rand_$m 300 env MTBLX_SNAPPY_KERNEL=$m python scripts/snappy_probe.py --blocks 100000
 done

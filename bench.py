@@ -281,7 +281,8 @@ def compressible_snappy(s, nrec=2_000_000):
     """cfg5 on data snappy actually compresses: cfg1-style records (a 10-digit
     key, the key repeated 1-8 times as the value), written by the product Writer with
     CompressionType::Snappy into 4 KiB blocks (~4.5x), decompressed on the device
-    (k_snappy_quads) and decoded, device-resident.  Checked: every block decompresses, and the
+    (mtblx_snappy_decompress_dev: its blocks expand > 2x, so k_snappy_lanes takes them) and
+    decoded, device-resident.  Checked: every block decompresses, and the
     decode yields every record written."""
     from mtblx import codec, synth
     from mtblx.writer import Writer
@@ -336,7 +337,8 @@ def compressible_snappy(s, nrec=2_000_000):
         raise RuntimeError("compressible cfg5: decode after device decompression failed")
     stored = int(zln.sum(dtype=np.uint64))
     return {"records": n, "blocks": int(zb.nblk), "file_repeats": rep, "stored_bytes": stored, "decompressed_bytes": out_bytes,
-            "ratio": round(out_bytes / stored, 2), "kernel": "k_snappy_quads",
+            "ratio": round(out_bytes / stored, 2),
+            "kernel": "k_snappy_lanes (blocks expanding > 2x; MTBLX_SNAPPY_KERNEL=" + os.environ.get("MTBLX_SNAPPY_KERNEL", "auto") + ")",
             "device_decompress_ms": round(dz_ms, 4),
             "device_decompress_GB_per_s_out": round(out_bytes / (dz_ms * 1e-3) / 1e9, 1),
             "device_decompress_plus_decode_GiB_per_s": round(out_bytes / (both_ms * 1e-3) / 2**30, 1)}

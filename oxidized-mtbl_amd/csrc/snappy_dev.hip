@@ -751,17 +751,56 @@ __device__ __forceinline__ Q4 ring_get(const uint32_t (*R)[kThreads], int t, uin
   return Q4{{alignb(w[1], w[0], r), alignb(w[2], w[1], r), alignb(w[3], w[2], r), alignb(w[4], w[3], r)}};
 }
 
-__global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, const uint64_t* src_off,
-                                                           const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
-                                                           const uint64_t* dst_off, const uint32_t* dst_len,
-                                                           int32_t* status, uint32_t* dec_len, int only_marked) {
+// v3: the HBM stores move to WRITER waves.  A vector-memory wait is in issue order over loads and
+// stores alike, so every header / literal load a decoding lane waited for also waited for all the
+// 16-byte stores it had issued before (an ablation without stores ran 1.63 -> 1.04 ms).  Here the
+// workgroup is 256 decoding lanes + 256 writer lanes, lane t + 256 writing lane t's block: the
+// decoder appends to its LDS ring and publishes its position (dpos); the writer copies whole
+// 16-byte chunks [fpos, dpos) from the ring to HBM and publishes fpos (issued) and fvis (stores
+// completed).  The decoder never overwrites ring words the writer has not taken (it waits on
+// fpos), and a copy whose source is beyond the ring (off > kRingOff) waits for fvis and reads HBM
+// with device-coherent loads.  LDS operations of one wave execute in order, so a position read
+// from dpos / fpos covers every ring write / read issued before it.  Short literals come from the
+// register window (48 bytes: two in use, the third loaded 16 bytes ahead).
+constexpr uint32_t kRun = 0xFFFFFFFFu;   // dend while the decoder runs
+constexpr uint64_t kSpinTicks = 2ull * 100000000ull;   // 2 s of s_memrealtime: only a bug waits that long
+
+struct LaneSync {
+  uint32_t dpos[kThreads], fpos[kThreads], fvis[kThreads], dend[kThreads];
+};
+
+__device__ __forceinline__ uint32_t vld(const uint32_t* p) { return *reinterpret_cast<const volatile uint32_t*>(p); }
+__device__ __forceinline__ void vst(uint32_t* p, uint32_t v) { *reinterpret_cast<volatile uint32_t*>(p) = v; }
+
+// 16 bytes at window byte k (k + 16 <= 32) of the window words w[0..7]
+__device__ __forceinline__ Q4 win16(const uint32_t (&w)[8], uint32_t k) {
+  const uint32_t q = k >> 2, r = k & 3u;
+  uint32_t x[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (q + i == (uint32_t)j) v = w[j];
+    x[i] = v;
+  }
+  return Q4{{alignb(x[1], x[0], r), alignb(x[2], x[1], r), alignb(x[3], x[2], r), alignb(x[4], x[3], r)}};
+}
+
+__global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* src, const uint64_t* src_off,
+                                                               const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                               const uint64_t* dst_off, const uint32_t* dst_len,
+                                                               int32_t* status, uint32_t* dec_len, int only_marked) {
   __shared__ uint32_t ring[kRingWords][kThreads];
+  __shared__ LaneSync Y;
   // period selectors: for offset o < 16 and output word i, byte j = source byte (4 i + j) mod o:
   // psel[o][i] = {v_perm selector over source bytes 0..7, over bytes 8..15, mask of the latter}
   __shared__ uint32_t psel[16][4][3];
-  const int t = threadIdx.x;
-  if (t < 64) {
-    const uint32_t o = (uint32_t)t >> 2, i = (uint32_t)t & 3u;
+  const int tid = threadIdx.x, t = tid & (kThreads - 1);
+  const bool writer = tid >= kThreads;
+  const uint32_t b = blockIdx.x * kThreads + (uint32_t)t;
+  if (tid < 64) {
+    const uint32_t o = (uint32_t)tid >> 2, i = (uint32_t)tid & 3u;
     uint32_t lo = 0, hi = 0, mk = 0;
     for (uint32_t j = 0; j < 4; ++j) {
       const uint32_t m = o ? (4u * i + j) % o : 0u;
@@ -775,19 +814,64 @@ __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, c
     psel[o][i][1] = hi;
     psel[o][i][2] = mk;
   }
+  if (!writer) {   // the lane's block, decided once (the decoder rewrites status[b] at its end)
+    const bool act = b < nblk && (!only_marked || status[b] == quad::kLanes);
+    Y.dpos[t] = 0;
+    Y.fpos[t] = 0;
+    Y.fvis[t] = 0;
+    Y.dend[t] = act ? kRun : 0u;
+  }
   __syncthreads();
-  const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
   if (b >= nblk) return;
-  if (only_marked && status[b] != quad::kLanes) return;
+  uint8_t* dg = b < nblk ? dst + dst_off[b] : dst;
+
+  if (writer) {   // ---- writer lane: ring -> HBM ----
+    uint32_t f = 0;
+    uint64_t t0 = 0;
+    uint32_t spins = 0;
+    for (;;) {
+      const uint32_t de = vld(&Y.dend[t]);
+      const uint32_t dp = de != kRun ? de : vld(&Y.dpos[t]);
+      bool moved = false;
+      while (f + 16u <= dp) {
+        const uint32_t q = f >> 2;
+        const v4u x = v4u{ring[q & (kRingWords - 1)][t], ring[(q + 1) & (kRingWords - 1)][t],
+                          ring[(q + 2) & (kRingWords - 1)][t], ring[(q + 3) & (kRingWords - 1)][t]};
+        *reinterpret_cast<v4u*>(dg + f) = x;
+        f += 16u;
+        moved = true;
+      }
+      if (de != kRun) {   // the decoder is done: the last partial chunk, byte by byte
+        for (uint32_t p = f; p < de; ++p)
+          dg[p] = (uint8_t)(ring[(p >> 2) & (kRingWords - 1)][t] >> (8 * (p & 3u)));
+        break;
+      }
+      if (moved) {
+        vst(&Y.fpos[t], f);
+        __builtin_amdgcn_s_waitcnt(0);   // stores performed (vmcnt / lgkmcnt 0): far copies may read them
+        vst(&Y.fvis[t], f);
+        t0 = 0;
+      } else {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 63u) == 0u) {
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (t0 == 0) t0 = now;
+          if (now - t0 > kSpinTicks) break;   // the decoder is gone (a bug): do not hang the GPU
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- decoder lane ----
+  if (vld(&Y.dend[t]) == 0u) return;
   const uint8_t* s = src + src_off[b];
   const uint32_t n = src_len[b];
-  uint8_t* dg = dst + dst_off[b];
   const uint32_t cap = dst_len[b];
-  // preamble
   uint64_t want = 0;
   uint32_t pos = 0;
   bool term = false;
-  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {   // preamble
     const uint32_t byte = s[i];
     want |= (uint64_t)(byte & 0x7fu) << (7 * i);
     if (!(byte & 0x80u)) {
@@ -801,26 +885,64 @@ __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, c
   else if (want > cap) st = MTBLX_SNAPPY_TOO_SMALL;
   const uint32_t W = st == MTBLX_SNAPPY_OK ? (uint32_t)want : 0u;
   uint32_t d = 0, carry = 0;
-  // the window: stored bytes [wp, wp + 32) in w[0..7]; w[4..7] may still be in flight
+  bool hang = false;
+  // wait until the writer has taken the ring words an append at x overwrites
+  auto room = [&](uint32_t x) {
+    const uint32_t need = 4u * (x >> 2) + 20u;
+    if (need <= 256u || vld(&Y.fpos[t]) + 256u >= need) return;
+    uint64_t t0 = 0;
+    uint32_t spins = 0;
+    while (vld(&Y.fpos[t]) + 256u < need) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 63u) == 0u) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) t0 = now;
+        if (now - t0 > kSpinTicks) { hang = true; return; }
+      }
+    }
+  };
+  // output bytes [x, x + 16) from HBM once the writer's stores cover [x, lim): device-coherent loads
+  auto far16 = [&](uint32_t x, uint32_t lim) {
+    uint64_t t0 = 0;
+    uint32_t spins = 0;
+    while (vld(&Y.fvis[t]) < lim && !hang) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 63u) == 0u) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) t0 = now;
+        if (now - t0 > kSpinTicks) hang = true;
+      }
+    }
+    const uint8_t* p = dg + x;
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = __hip_atomic_load(a + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return Q4{{alignb(w[1], w[0], r), alignb(w[2], w[1], r), alignb(w[3], w[2], r), alignb(w[4], w[3], r)}};
+  };
+  // the window: stored bytes [wp, wp + 48) in c0 c1 c2 (c2 loaded 16 bytes ahead)
   uint32_t wp = pos;
-  Q4 lo4 = ld16(s, n, wp), hi4 = ld16(s, n, wp + 16u);
-  while (st == MTBLX_SNAPPY_OK && pos < n) {
+  Q4 c0 = ld16(s, n, wp), c1 = ld16(s, n, wp + 16u), c2 = ld16(s, n, wp + 32u);
+  while (st == MTBLX_SNAPPY_OK && pos < n && !hang) {
     if (pos - wp >= 16u) {
-      if (pos - wp < 32u) {   // advance 16 bytes, load the next 16 ahead
-        lo4 = hi4;
+      if (pos - wp < 32u) {   // advance 16 bytes, load the next 16 two steps ahead
+        c0 = c1;
+        c1 = c2;
         wp += 16u;
-        hi4 = ld16(s, n, wp + 16u);
+        c2 = ld16(s, n, wp + 32u);
       } else {                // a long literal jumped past the window
         wp = pos;
-        lo4 = ld16(s, n, wp);
-        hi4 = ld16(s, n, wp + 16u);
+        c0 = ld16(s, n, wp);
+        c1 = ld16(s, n, wp + 16u);
+        c2 = ld16(s, n, wp + 32u);
       }
     }
     const uint32_t k = pos - wp, kq = k >> 2, kr = k & 3u;   // tag + 4 bytes at window byte k < 16
-    uint32_t a = lo4.w[0], bb = lo4.w[1], c = lo4.w[2];
-    if (kq == 1u) { a = lo4.w[1]; bb = lo4.w[2]; c = lo4.w[3]; }
-    if (kq == 2u) { a = lo4.w[2]; bb = lo4.w[3]; c = hi4.w[0]; }
-    if (kq == 3u) { a = lo4.w[3]; bb = hi4.w[0]; c = hi4.w[1]; }
+    uint32_t a = c0.w[0], bb = c0.w[1], c = c0.w[2];
+    if (kq == 1u) { a = c0.w[1]; bb = c0.w[2]; c = c0.w[3]; }
+    if (kq == 2u) { a = c0.w[2]; bb = c0.w[3]; c = c1.w[0]; }
+    if (kq == 3u) { a = c0.w[3]; bb = c1.w[0]; c = c1.w[1]; }
     const uint32_t lo = alignb(bb, a, kr), hi = alignb(c, bb, kr);
     const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2;
     const uint32_t avail = n - pos - 1u;
@@ -841,24 +963,38 @@ __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, c
       break;
     }
     const uint32_t end = d + L;
-    const bool rg = !lit && off <= kRingOff;           // copy source in the LDS ring
-    const bool ov = !lit && off < 16u && off < L;      // overlapping short copy: the period
+    const bool rg = !lit && off <= kRingOff;        // copy source in the LDS ring
+    const bool ov = !lit && off < 16u && off < L;   // overlapping short copy: the period
+    const uint32_t lk = sp - wp;                    // a literal's window byte
     Q4 v;
-    if (rg) v = ring_get(ring, t, d - off);
-    else v = lit ? ld16(s, n, sp) : q4(*reinterpret_cast<const v4u*>(dg + d - off));
+    if (lit) {
+      if (lk + (L < 16u ? L : 16u) <= 32u) {   // inside c0 c1 (c2 may still be in flight: not read)
+        const bool h = lk >= 16u;
+        const uint32_t w8[8] = {h ? c1.w[0] : c0.w[0], h ? c1.w[1] : c0.w[1], h ? c1.w[2] : c0.w[2],
+                                h ? c1.w[3] : c0.w[3], h ? 0u : c1.w[0],    h ? 0u : c1.w[1],
+                                h ? 0u : c1.w[2],      h ? 0u : c1.w[3]};
+        v = win16(w8, lk & 15u);   // bytes past the literal are not used
+      } else {
+        v = ld16(s, n, sp);
+      }
+    } else if (rg) {
+      v = ring_get(ring, t, d - off);
+    } else {
+      v = far16(d - off, d - off + 16u);
+    }
     if (ov) {
       const uint32_t o = off;
-      Q4 p;
+      Q4 pp;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t pl = __builtin_amdgcn_perm(v.w[1], v.w[0], psel[o][i][0]);
         const uint32_t ph = __builtin_amdgcn_perm(v.w[3], v.w[2], psel[o][i][1]);
         const uint32_t mk = psel[o][i][2];
-        p.w[i] = (pl & ~mk) | (ph & mk);
+        pp.w[i] = (pl & ~mk) | (ph & mk);
       }
-      v = p;
+      v = pp;
     }
-    st16(dg, d, v, end, cap);
+    room(d);
     ring_put(ring, t, carry, d, v, L < 16u ? L : 16u);
     if (L > 16u) {
       const uint32_t off2 = ov ? off * ((16u + off - 1u) / off) : off;
@@ -866,15 +1002,25 @@ __global__ void __launch_bounds__(kThreads) k_snappy_lanes(const uint8_t* src, c
         Q4 x;
         if (lit) x = ld16(s, n, sp + j);
         else if (rg) x = ring_get(ring, t, d + j - off2);
-        else x = q4(*reinterpret_cast<const v4u*>(dg + d + j - off2));
-        st16(dg, d + j, x, end, cap);
+        else x = far16(d + j - off2, d + j - off2 + 16u);
+        // bytes [0, d + j) are final: publish them, or a long literal would wait for room
+        // the writer cannot make
+        __asm__ volatile("" ::: "memory");
+        vst(&Y.dpos[t], d + j);
+        room(d + j);
         ring_put(ring, t, carry, d + j, x, L - j < 16u ? L - j : 16u);
       }
     }
+    // no fence: a workgroup release would also wait for the window's loads in flight; LDS
+    // operations of a wave execute in order, so the ring writes land before this one
+    __asm__ volatile("" ::: "memory");
+    vst(&Y.dpos[t], end);
     pos = lit ? sp + L : sp;
     d = end;
   }
+  if (hang) st = MTBLX_SNAPPY_CORRUPT;
   if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
+  vst(&Y.dend[t], st == MTBLX_SNAPPY_OK ? d : 0u);
   status[b] = st;
   if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
 }
@@ -1026,7 +1172,7 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
     const char* e = getenv("MTBLX_SNAPPY_KERNEL");
     mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : 0;
   }
-  const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(lanes::kThreads);
+  const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(2 * lanes::kThreads);
   if (mode == 2) {
     hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
                        status, dec_len, 0);

@@ -763,6 +763,9 @@ __device__ __forceinline__ Q4 ring_get(const uint32_t (*R)[kThreads], int t, uin
 // from dpos / fpos covers every ring write / read issued before it.  Short literals come from the
 // register window (48 bytes: two in use, the third loaded 16 bytes ahead).
 constexpr uint32_t kRun = 0xFFFFFFFFu;   // dend while the decoder runs
+#ifndef MTBLX_SNAP_WSLEEP
+#define MTBLX_SNAP_WSLEEP 8   // writer's idle sleep, x 64 cycles
+#endif
 constexpr uint64_t kSpinTicks = 2ull * 100000000ull;   // 2 s of s_memrealtime: only a bug waits that long
 
 struct LaneSync {
@@ -852,8 +855,10 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
         vst(&Y.fvis[t], f);
         t0 = 0;
       } else {
-        __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 63u) == 0u) {
+        // idle: sleep (64 x MTBLX_SNAP_WSLEEP cycles) -- 2, 8 and 20 measured within 1 %: the
+        // decoding lanes, not the writers' issue slots, bound the kernel
+        __builtin_amdgcn_s_sleep(MTBLX_SNAP_WSLEEP);
+        if ((++spins & 15u) == 0u) {
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (t0 == 0) t0 = now;
           if (now - t0 > kSpinTicks) break;   // the decoder is gone (a bug): do not hang the GPU
@@ -921,68 +926,87 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     for (int k = 0; k < 5; ++k) w[k] = __hip_atomic_load(a + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return Q4{{alignb(w[1], w[0], r), alignb(w[2], w[1], r), alignb(w[3], w[2], r), alignb(w[4], w[3], r)}};
   };
+  // The loop emits ONE chunk (up to 16 bytes) per iteration: the next chunk of the current
+  // element, or -- once it is done -- the first chunk of the next one.  An element-per-iteration
+  // loop with an inner loop over its chunks made every lane of a wave pay for the wave's longest
+  // element in every iteration (~520 vector + ~490 scalar instructions per element, SQ counters).
   // the window: stored bytes [wp, wp + 48) in c0 c1 c2 (c2 loaded 16 bytes ahead)
   uint32_t wp = pos;
   Q4 c0 = ld16(s, n, wp), c1 = ld16(s, n, wp + 16u), c2 = ld16(s, n, wp + 32u);
-  while (st == MTBLX_SNAPPY_OK && pos < n && !hang) {
-    if (pos - wp >= 16u) {
-      if (pos - wp < 32u) {   // advance 16 bytes, load the next 16 two steps ahead
-        c0 = c1;
-        c1 = c2;
-        wp += 16u;
-        c2 = ld16(s, n, wp + 32u);
-      } else {                // a long literal jumped past the window
-        wp = pos;
-        c0 = ld16(s, n, wp);
-        c1 = ld16(s, n, wp + 16u);
-        c2 = ld16(s, n, wp + 32u);
+  uint32_t rem = 0;    // bytes of the current element still to emit
+  bool elit = false;   // the current element is a literal: next bytes at stream position es
+  uint32_t es = 0;     // literal: stream position; copy: source distance (d - source)
+  bool fin = st != MTBLX_SNAPPY_OK || pos >= n;
+  while (__ballot(!fin)) {
+    if (fin) continue;
+    bool first = false, ov = false;
+    uint32_t off = 0;
+    if (rem == 0u) {   // ---- decode the next element ----
+      if (pos - wp >= 16u) {
+        if (pos - wp < 32u) {   // advance 16 bytes, load the next 16 two steps ahead
+          c0 = c1;
+          c1 = c2;
+          wp += 16u;
+          c2 = ld16(s, n, wp + 32u);
+        } else {                // a long literal jumped past the window
+          wp = pos;
+          c0 = ld16(s, n, wp);
+          c1 = ld16(s, n, wp + 16u);
+          c2 = ld16(s, n, wp + 32u);
+        }
       }
+      const uint32_t k = pos - wp, kq = k >> 2, kr = k & 3u;   // tag + 4 bytes at window byte k < 16
+      uint32_t a = c0.w[0], bb = c0.w[1], c = c0.w[2];
+      if (kq == 1u) { a = c0.w[1]; bb = c0.w[2]; c = c0.w[3]; }
+      if (kq == 2u) { a = c0.w[2]; bb = c0.w[3]; c = c1.w[0]; }
+      if (kq == 3u) { a = c0.w[3]; bb = c1.w[0]; c = c1.w[1]; }
+      const uint32_t lo = alignb(bb, a, kr), hi = alignb(c, bb, kr);
+      const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2;
+      const uint32_t avail = n - pos - 1u;
+      const uint32_t raw = alignb(hi, lo, 1u);   // the 4 bytes after the tag
+      const bool lg = t2 >= 60u;
+      const uint32_t nb = t2 - 59u;
+      const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * (nb & 3u))) - 1u);
+      const uint32_t lc = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
+      off = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
+      const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
+      elit = kind == 0u;
+      const uint32_t L = elit ? (lg ? ext + 1u : t2 + 1u) : lc;   // ext + 1 wraps only when ext == ~0: bad
+      const uint32_t sp = pos + (elit ? (lg ? 1u + nb : 1u) : need + 1u);
+      bool bad = elit ? ((lg && (avail < nb || ext == 0xFFFFFFFFu)) || n - sp < L) : (avail < need || off == 0u || off > d);
+      bad = bad || W - d < L;
+      if (bad) {
+        st = MTBLX_SNAPPY_CORRUPT;
+        fin = true;
+        continue;
+      }
+      rem = L;
+      first = true;
+      ov = !elit && off < 16u && off < L;   // overlapping short copy: the period
+      es = elit ? sp : off;
+      pos = elit ? sp + L : sp;
     }
-    const uint32_t k = pos - wp, kq = k >> 2, kr = k & 3u;   // tag + 4 bytes at window byte k < 16
-    uint32_t a = c0.w[0], bb = c0.w[1], c = c0.w[2];
-    if (kq == 1u) { a = c0.w[1]; bb = c0.w[2]; c = c0.w[3]; }
-    if (kq == 2u) { a = c0.w[2]; bb = c0.w[3]; c = c1.w[0]; }
-    if (kq == 3u) { a = c0.w[3]; bb = c1.w[0]; c = c1.w[1]; }
-    const uint32_t lo = alignb(bb, a, kr), hi = alignb(c, bb, kr);
-    const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2;
-    const uint32_t avail = n - pos - 1u;
-    const uint32_t raw = alignb(hi, lo, 1u);   // the 4 bytes after the tag
-    const bool lg = t2 >= 60u;
-    const uint32_t nb = t2 - 59u;
-    const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * (nb & 3u))) - 1u);
-    const uint32_t lc = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
-    const uint32_t off = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
-    const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
-    const bool lit = kind == 0u;
-    const uint32_t L = lit ? (lg ? ext + 1u : t2 + 1u) : lc;   // ext + 1 wraps only when ext == ~0: bad below
-    const uint32_t sp = pos + (lit ? (lg ? 1u + nb : 1u) : need + 1u);
-    bool bad = lit ? ((lg && (avail < nb || ext == 0xFFFFFFFFu)) || n - sp < L) : (avail < need || off == 0u || off > d);
-    bad = bad || W - d < L;
-    if (bad) {
-      st = MTBLX_SNAPPY_CORRUPT;
-      break;
-    }
-    const uint32_t end = d + L;
-    const bool rg = !lit && off <= kRingOff;        // copy source in the LDS ring
-    const bool ov = !lit && off < 16u && off < L;   // overlapping short copy: the period
-    const uint32_t lk = sp - wp;                    // a literal's window byte
+    // ---- one chunk ----
+    const uint32_t cnt = rem < 16u ? rem : 16u;
     Q4 v;
-    if (lit) {
-      if (lk + (L < 16u ? L : 16u) <= 32u) {   // inside c0 c1 (c2 may still be in flight: not read)
+    if (elit) {
+      const uint32_t lk = es - wp;   // the literal's window byte (es >= wp while it is in the window)
+      if (es >= wp && lk + cnt <= 32u) {   // inside c0 c1 (c2 may still be in flight: not read)
         const bool h = lk >= 16u;
         const uint32_t w8[8] = {h ? c1.w[0] : c0.w[0], h ? c1.w[1] : c0.w[1], h ? c1.w[2] : c0.w[2],
                                 h ? c1.w[3] : c0.w[3], h ? 0u : c1.w[0],    h ? 0u : c1.w[1],
                                 h ? 0u : c1.w[2],      h ? 0u : c1.w[3]};
         v = win16(w8, lk & 15u);   // bytes past the literal are not used
       } else {
-        v = ld16(s, n, sp);
+        v = ld16(s, n, es);
       }
-    } else if (rg) {
-      v = ring_get(ring, t, d - off);
+      es += 16u;
+    } else if (es <= kRingOff) {
+      v = ring_get(ring, t, d - es);
     } else {
-      v = far16(d - off, d - off + 16u);
+      v = far16(d - es, d - es + 16u);
     }
-    if (ov) {
+    if (first && ov) {   // the period of an overlapping copy; later chunks read it back at off2
       const uint32_t o = off;
       Q4 pp;
 #pragma unroll
@@ -993,30 +1017,19 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
         pp.w[i] = (pl & ~mk) | (ph & mk);
       }
       v = pp;
+      // chunk j >= 16 reads [d + j - off2, +16), off2 = off * ceil(16 / off) in [16, 16 + off):
+      // bytes written by earlier chunks, or the period's bytes before the element, which equal it
+      es = off * ((16u + off - 1u) / off);
     }
     room(d);
-    ring_put(ring, t, carry, d, v, L < 16u ? L : 16u);
-    if (L > 16u) {
-      const uint32_t off2 = ov ? off * ((16u + off - 1u) / off) : off;
-      for (uint32_t j = 16; j < L; j += 16) {
-        Q4 x;
-        if (lit) x = ld16(s, n, sp + j);
-        else if (rg) x = ring_get(ring, t, d + j - off2);
-        else x = far16(d + j - off2, d + j - off2 + 16u);
-        // bytes [0, d + j) are final: publish them, or a long literal would wait for room
-        // the writer cannot make
-        __asm__ volatile("" ::: "memory");
-        vst(&Y.dpos[t], d + j);
-        room(d + j);
-        ring_put(ring, t, carry, d + j, x, L - j < 16u ? L - j : 16u);
-      }
-    }
+    ring_put(ring, t, carry, d, v, cnt);
+    d += cnt;
+    rem -= cnt;
     // no fence: a workgroup release would also wait for the window's loads in flight; LDS
     // operations of a wave execute in order, so the ring writes land before this one
     __asm__ volatile("" ::: "memory");
-    vst(&Y.dpos[t], end);
-    pos = lit ? sp + L : sp;
-    d = end;
+    vst(&Y.dpos[t], d);
+    if (hang || (rem == 0u && pos >= n)) fin = true;
   }
   if (hang) st = MTBLX_SNAPPY_CORRUPT;
   if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;

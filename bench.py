@@ -336,7 +336,29 @@ def compressible_snappy(s, nrec=2_000_000):
     if out.totals_host() != (nr, kb, vb, 0):
         raise RuntimeError("compressible cfg5: decode after device decompression failed")
     stored = int(zln.sum(dtype=np.uint64))
+    # end to end (pinned file in -> pinned outputs out, mtblx_pipe_decode) with host and with
+    # device decompression: which one MTBLX_PIPE_DEVICE_SNAPPY=auto should pick here
+    from mtblx import pipe
+    hout = pipe.HostOutputs(int(zb.nblk), nr, kb, vb)
+    e2e = {}
+    pipe.register(z)
+    try:
+        for name, mode in (("host_decompress", False), ("device_decompress", True)):
+            pp = pipe.HostPipe(chunk_bytes=64 << 20, max_blocks=1 << 16, threads=16, device_snappy=mode)
+            pp.decode(z, zoff, zln, hout, compression=1)   # warm-up
+            t0 = time.perf_counter()
+            for _ in range(3):
+                pp.decode(z, zoff, zln, hout, compression=1)
+            el = (time.perf_counter() - t0) / 3
+            tot = hout.totals
+            if int(tot[0]) != nr or int(tot[1]) != kb or int(tot[2]) != vb or int(tot[3]) != 0:
+                raise RuntimeError(f"compressible cfg5 end to end ({name}) failed: totals={list(tot)}")
+            e2e[name] = {"GiB_per_s_of_block_bytes": round(out_bytes / el / 2**30, 2), "ms_per_pass": round(el * 1e3, 2)}
+            del pp
+    finally:
+        pipe.unregister(z)
     return {"records": n, "blocks": int(zb.nblk), "file_repeats": rep, "stored_bytes": stored, "decompressed_bytes": out_bytes,
+            "end_to_end": e2e,
             "ratio": round(out_bytes / stored, 2),
             "kernel": "k_snappy_lanes (blocks expanding > 2x; MTBLX_SNAPPY_KERNEL=" + os.environ.get("MTBLX_SNAPPY_KERNEL", "auto") + ")",
             "device_decompress_ms": round(dz_ms, 4),

@@ -38,8 +38,6 @@
 #include "mtblx.h"
 #include "mtblx_host.h"
 
-// MTBLX_PIPE_DEVICE_SNAPPY auto: device decompression when uncompressed / stored <= this
-static constexpr uint64_t kAutoDeviceMaxRatio = 2;
 
 namespace {
 
@@ -170,7 +168,7 @@ struct mtblx_pipe {
   uint64_t chunk_bytes = 64ull << 20;
   uint32_t max_blocks = 1u << 16;
   int dev = 0;
-  int dev_snappy = 2;   // MTBLX_PIPE_DEVICE_SNAPPY: 0 host, 1 device, 2 auto (device for poorly compressed files)
+  int dev_snappy = 2;   // MTBLX_PIPE_DEVICE_SNAPPY: 0 host, 1 device, 2 auto (= the device, measured faster on both)
   hipStream_t s_h2d = nullptr, s_dec = nullptr, s_d2h = nullptr;
   Slot slot[kSlots];
   void* ws = nullptr;
@@ -354,16 +352,12 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     }
   }
   // stored bytes H2D + device decompression (mtblx_snappy_decompress_dev) or host decompression.
-  // auto: the device only where it wins -- a PCIe-bound pipe on poorly compressed blocks (the
-  // stored bytes cross PCIe once, the host stage vanishes); on compressible streams the device
-  // decompressor (~170 GB/s of output) loses to 16 host threads (~110 GB/s of
-  // input), so they stay on the host.
-  bool dz_mode = compression == 1 && p->dev_snappy == 1;
-  if (compression == 1 && p->dev_snappy == 2) {
-    uint64_t su = 0, ss = 0;
-    for (uint32_t b = 0; b < nblk; ++b) { su += ulen[b]; ss += blk_len[b]; }
-    dz_mode = ss > 0 && su <= kAutoDeviceMaxRatio * ss;
-  }
+  // auto = the device: the stored bytes cross PCIe once and the host stage vanishes.  It wins on
+  // poorly compressed blocks (cfg5, ~1x: 28.5-32 vs 27 GiB/s end to end) and, since
+  // k_snappy_lanes (~320 GB/s of output), on compressible ones too (the bench line's 4.58x
+  // stream: 21.1 vs 13.4 GiB/s end to end).  (Round 2's auto kept streams that
+  // expand > 2x on the host, when the device decompressor ran ~170 GB/s.)
+  const bool dz_mode = compression == 1 && p->dev_snappy != 0;
   const bool ranged = compression == 0 || dz_mode;
   std::vector<Chunk> chunks;
   Caps need;

@@ -81,7 +81,7 @@ class HostPipe:
         if not self._p:
             raise RuntimeError("mtblx_pipe_new failed")
         # MTBLX_PIPE_DEVICE_SNAPPY: snappy blocks cross PCIe compressed, decompressed on the device
-        # (True), on the host (False), or "auto": the device only for poorly compressed batches
+        # (True), on the host (False), or "auto" (the device: faster end to end on any snappy stream)
         mode = 2 if device_snappy == "auto" else (1 if device_snappy else 0)
         if _lib.lib().mtblx_pipe_set(self._p, 1, mode) != 0:
             raise RuntimeError("mtblx_pipe_set failed")

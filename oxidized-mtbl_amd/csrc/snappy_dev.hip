@@ -1178,19 +1178,21 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   if (nblk == 0) return MTBLX_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !dst_len || !status) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  // MTBLX_SNAPPY_KERNEL (read once): "auto" (default: blocks expanding > 2x go to
-  // k_snappy_lanes, the rest to the quad / one-wave kernels), "lanes" (every block), "quads"
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("MTBLX_SNAPPY_KERNEL");
-    mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : 0;
-  }
+  constexpr uint32_t kLanesMinBlocks = 49152;
+  // MTBLX_SNAPPY_KERNEL (read per call; tests switch it): "auto" (default: in batches of
+  // >= kLanesMinBlocks, blocks expanding > 2x go to k_snappy_lanes, the rest to the quad /
+  // one-wave kernels), "lanes" (every block), "quads"
+  const char* e = getenv("MTBLX_SNAPPY_KERNEL");
+  const int mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : 0;
   const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(2 * lanes::kThreads);
   if (mode == 2) {
     hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
                        status, dec_len, 0);
   } else if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
-    const uint32_t lanes_x = mode == 0 ? 2u : 0u;
+    // k_snappy_lanes costs about one block's serial decode however many blocks run (all are in
+    // flight), the quads ~0.19 ms per round of 8 192 blocks: the lanes win from ~50 000 blocks
+    // (25 000 compressible blocks: quads 0.66 ms, lanes ~1.0 ms; 100 000: 2.33 vs 1.24 ms)
+    const uint32_t lanes_x = (mode == 0 && nblk >= kLanesMinBlocks) ? 2u : 0u;
     hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len, lanes_x);

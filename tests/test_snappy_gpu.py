@@ -18,6 +18,17 @@ from test_snappy import _inputs, _libsnappy
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["auto", "lanes"], autouse=True)
+def snappy_kernel(request, monkeypatch):
+    """every test under the default routing and with every block on k_snappy_lanes (one lane
+    per block, output streamed to HBM) -- auto sends blocks there only in large batches"""
+    if request.param == "lanes":
+        monkeypatch.setenv("MTBLX_SNAPPY_KERNEL", "lanes")
+    else:
+        monkeypatch.delenv("MTBLX_SNAPPY_KERNEL", raising=False)
+    return request.param
+
+
 def _dev():
     import torch
     if not torch.cuda.is_available():
@@ -265,3 +276,35 @@ def test_snappy_file_device_decompress_then_decode(oracle):
             assert h.status[b] == 1 and h.nrec[b] == 0
         else:
             assert h.status[b] == 0 and h.records(b) == exp.records(b)
+
+
+def test_auto_routing_large_batch(oracle, snappy_kernel):
+    """a batch of 60 000 blocks (>= the 49 152 from which auto routes blocks expanding > 2x to
+    k_snappy_lanes): compressible, random and corrupt streams mixed, so the quad kernel, the
+    lanes kernel (blocks the quads mark) and the deferred pass all run in one call"""
+    if snappy_kernel != "auto":
+        pytest.skip("the routing itself")
+    codec = _dev()
+    from mtblx import pipe, synth
+    rng = np.random.default_rng(21)
+    distinct = [pipe.snappy_compress(x) for x in _compressible(rng) if len(x) <= 4608]
+    recs = list(synth.cfg1_records(4000))
+    for i in range(0, 4000, 50):   # cfg1-style blocks of 50 records (<= 4500 bytes: the quad path)
+        distinct.append(pipe.snappy_compress(b"".join(k + v for k, v in recs[i: i + 50])))
+    distinct += [pipe.snappy_compress(rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()) for n in (100, 3000, 4000)]
+    bad = bytearray(distinct[-5])
+    bad[len(bad) // 2] ^= 0x40
+    distinct.append(bytes(bad))
+    expect = [oracle.snappy_decompress(z) for z in distinct]
+    pick = rng.integers(0, len(distinct), 60_000)
+    streams = [distinct[int(i)] for i in pick]
+    assert max(len(e) for e in expect if e is not None) <= 4608
+    got, st, _ = _device(codec, streams, rng)
+    for j, i in enumerate(pick):
+        e = expect[int(i)]
+        if e is None:
+            assert st[j] == 1, j
+        else:
+            assert st[j] == 0 and got[j] == e, j
+    ratios = [len(e) / max(len(z), 1) for z, e in zip(distinct, expect) if e is not None]
+    assert max(ratios) > 2 and min(ratios) < 2   # both kernels took blocks

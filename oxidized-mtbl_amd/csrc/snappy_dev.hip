@@ -892,12 +892,16 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
   uint32_t d = 0, carry = 0;
   bool hang = false;
   // wait until the writer has taken the ring words an append at x overwrites
+  // (fseen: the writer's position last read -- it only grows, so most chunks need no LDS read)
+  uint32_t fseen = 0;
   auto room = [&](uint32_t x) {
     const uint32_t need = 4u * (x >> 2) + 20u;
-    if (need <= 256u || vld(&Y.fpos[t]) + 256u >= need) return;
+    if (need <= fseen + 256u) return;
+    fseen = vld(&Y.fpos[t]);
+    if (need <= fseen + 256u) return;
     uint64_t t0 = 0;
     uint32_t spins = 0;
-    while (vld(&Y.fpos[t]) + 256u < need) {
+    while ((fseen = vld(&Y.fpos[t])) + 256u < need) {
       __builtin_amdgcn_s_sleep(1);
       if ((++spins & 63u) == 0u) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();

@@ -703,12 +703,34 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t r)
   return __builtin_amdgcn_alignbyte(hi, lo, r);
 }
 // stored bytes [p, p + 16) of s[0, n) (zero past n): one unaligned load inside, bytes at the end
+// Past the end (p + 16 > n) the 16 bytes ENDING at n are loaded -- in bounds whenever n >= 16 --
+// and shifted down by r = p + 16 - n bytes: one load and a funnel shift instead of 16 byte
+// loads (a wave has some lane near its stream's end in most iterations).
 __device__ __forceinline__ Q4 ld16(const uint8_t* s, uint32_t n, uint32_t p) {
   if ((uint64_t)p + 16u <= n) return q4(*reinterpret_cast<const v4u*>(s + p));
   Q4 q{{0u, 0u, 0u, 0u}};
+  if (n >= 16u) {
+    const Q4 x = q4(*reinterpret_cast<const v4u*>(s + n - 16u));
+    const uint32_t r = p >= n ? 16u : p + 16u - n, rq = r >> 2, rb = r & 3u;   // r in [1, 16]
+    uint32_t y[6];
 #pragma unroll
-  for (int k = 0; k < 16; ++k)
-    if ((uint64_t)p + k < n) q.w[k >> 2] |= (uint32_t)s[p + k] << (8 * (k & 3));
+    for (int i = 0; i < 6; ++i) {   // y[i] = x.w[i + rq] (0 past the end)
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((uint32_t)(i + 0) + rq == (uint32_t)j) v = x.w[j];
+      y[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.w[i] = alignb(y[i + 1], y[i], rb);
+    return q;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {   // a stream under 16 bytes: clamped loads, no branches
+    const uint32_t pk = p + (uint32_t)k < n ? p + (uint32_t)k : 0u;
+    const uint32_t v = n ? (uint32_t)s[pk] : 0u;
+    q.w[k >> 2] |= ((uint64_t)p + k < n ? v : 0u) << (8 * (k & 3));
+  }
   return q;
 }
 // 16 bytes to dg[o, o + 16), or only dg[o, end) when the slot (cap bytes) ends before o + 16

@@ -691,9 +691,16 @@ __global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, c
 // kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.
 namespace lanes {
 typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
-constexpr int kThreads = 256;
-constexpr int kRingWords = 64;
-constexpr uint32_t kRingOff = 240;
+#ifndef MTBLX_LANE_THREADS   // decoding lanes per workgroup (as many writer lanes again)
+#define MTBLX_LANE_THREADS 256
+#endif
+#ifndef MTBLX_LANE_RING_WORDS   // per-lane ring, 4-byte words (a power of two)
+#define MTBLX_LANE_RING_WORDS 64
+#endif
+constexpr int kThreads = MTBLX_LANE_THREADS;
+constexpr int kRingWords = MTBLX_LANE_RING_WORDS;
+constexpr uint32_t kRingBytes = 4u * kRingWords;
+constexpr uint32_t kRingOff = kRingBytes - 16u;   // copies reaching back at most this far read the ring
 
 struct Q4 {
   uint32_t w[4];
@@ -918,12 +925,12 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
   uint32_t fseen = 0;
   auto room = [&](uint32_t x) {
     const uint32_t need = 4u * (x >> 2) + 20u;
-    if (need <= fseen + 256u) return;
+    if (need <= fseen + kRingBytes) return;
     fseen = vld(&Y.fpos[t]);
-    if (need <= fseen + 256u) return;
+    if (need <= fseen + kRingBytes) return;
     uint64_t t0 = 0;
     uint32_t spins = 0;
-    while ((fseen = vld(&Y.fpos[t])) + 256u < need) {
+    while ((fseen = vld(&Y.fpos[t])) + kRingBytes < need) {
       __builtin_amdgcn_s_sleep(1);
       if ((++spins & 63u) == 0u) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -933,7 +940,22 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     }
   };
   // output bytes [x, x + 16) from HBM once the writer's stores cover [x, lim): device-coherent loads
-  auto far16 = [&](uint32_t x, uint32_t lim) {
+#ifndef MTBLX_LANE_FAR_CACHED
+#define MTBLX_LANE_FAR_CACHED 1
+#endif
+  auto far16 = [&](uint32_t x) {
+#if MTBLX_LANE_FAR_CACHED
+    // Wait until the writer's completed stores cover every 128-byte line the 16 bytes touch, then
+    // read them with an ordinary (cacheable) load: a line this CU caches was complete when it
+    // was loaded, so no copy of it can be stale.  (Lines shared with a neighbouring block's slot
+    // hold that block's LAST bytes, which are never a copy source: sources lie >= 224 bytes
+    // before the decoding position.)  Device-coherent dword loads here cost a trip to the L2
+    // per dword in ~80 % of the wave's iterations.
+    const uintptr_t base = reinterpret_cast<uintptr_t>(dg);
+    const uint32_t lim = (uint32_t)((((base + x + 15u) | 127u) + 1u) - base);
+#else
+    const uint32_t lim = x + 16u;
+#endif
     uint64_t t0 = 0;
     uint32_t spins = 0;
     while (vld(&Y.fvis[t]) < lim && !hang) {
@@ -944,6 +966,9 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
         if (now - t0 > kSpinTicks) hang = true;
       }
     }
+#if MTBLX_LANE_FAR_CACHED
+    return q4(*reinterpret_cast<const v4u*>(dg + x));
+#else
     const uint8_t* p = dg + x;
     const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
     const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
@@ -951,6 +976,7 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
 #pragma unroll
     for (int k = 0; k < 5; ++k) w[k] = __hip_atomic_load(a + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return Q4{{alignb(w[1], w[0], r), alignb(w[2], w[1], r), alignb(w[3], w[2], r), alignb(w[4], w[3], r)}};
+#endif
   };
   // The loop emits ONE chunk (up to 16 bytes) per iteration: the next chunk of the current
   // element, or -- once it is done -- the first chunk of the next one.  An element-per-iteration
@@ -963,8 +989,27 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
   bool elit = false;   // the current element is a literal: next bytes at stream position es
   uint32_t es = 0;     // literal: stream position; copy: source distance (d - source)
   bool fin = st != MTBLX_SNAPPY_OK || pos >= n;
+#ifdef MTBLX_SNAP_STAMPS
+  // diagnostic: per wave iteration, whether any lane took each path:
+  // [0] iterations [1] decode [2] literal from the window [3] literal from HBM [4] ring copy
+  // [5] far copy [6] overlapping copy [7] full window reload
+  uint32_t dbg_path = 0;
+#define LANE_PATH(k) (dbg_path |= 1u << (k))
+#else
+#define LANE_PATH(k) ((void)0)
+#endif
   while (__ballot(!fin)) {
-    if (fin) continue;
+#ifdef MTBLX_SNAP_STAMPS
+    dbg_path = 0;
+#endif
+    if (fin) {
+#ifdef MTBLX_SNAP_STAMPS
+      goto lane_stamp;
+#else
+      continue;
+#endif
+    }
+    {
     bool first = false, ov = false;
     uint32_t off = 0;
     if (rem == 0u) {   // ---- decode the next element ----
@@ -975,6 +1020,7 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
           wp += 16u;
           c2 = ld16(s, n, wp + 32u);
         } else {                // a long literal jumped past the window
+          LANE_PATH(7);
           wp = pos;
           c0 = ld16(s, n, wp);
           c1 = ld16(s, n, wp + 16u);
@@ -1008,6 +1054,7 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
       }
       rem = L;
       first = true;
+      LANE_PATH(1);
       ov = !elit && off < 16u && off < L;   // overlapping short copy: the period
       es = elit ? sp : off;
       pos = elit ? sp + L : sp;
@@ -1023,16 +1070,21 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
                                 h ? c1.w[3] : c0.w[3], h ? 0u : c1.w[0],    h ? 0u : c1.w[1],
                                 h ? 0u : c1.w[2],      h ? 0u : c1.w[3]};
         v = win16(w8, lk & 15u);   // bytes past the literal are not used
+        LANE_PATH(2);
       } else {
         v = ld16(s, n, es);
+        LANE_PATH(3);
       }
       es += 16u;
     } else if (es <= kRingOff) {
       v = ring_get(ring, t, d - es);
+      LANE_PATH(4);
     } else {
-      v = far16(d - es, d - es + 16u);
+      v = far16(d - es);
+      LANE_PATH(5);
     }
-    if (first && ov) {   // the period of an overlapping copy; later chunks read it back at off2
+    if (first && ov) {
+      LANE_PATH(6);   // the period of an overlapping copy; later chunks read it back at off2
       const uint32_t o = off;
       Q4 pp;
 #pragma unroll
@@ -1056,6 +1108,20 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     __asm__ volatile("" ::: "memory");
     vst(&Y.dpos[t], d);
     if (hang || (rem == 0u && pos >= n)) fin = true;
+    }
+#ifdef MTBLX_SNAP_STAMPS
+  lane_stamp:
+    {
+      uint32_t any = dbg_path;   // OR over the wave's lanes
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) any |= (uint32_t)__shfl_xor((int)any, sh, 64);
+      if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_snap_dbg[0], 1ull);
+        for (int k = 1; k < 8; ++k)
+          if (any & (1u << k)) atomicAdd(&g_snap_dbg[k], 1ull);
+      }
+    }
+#endif
   }
   if (hang) st = MTBLX_SNAPPY_CORRUPT;
   if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;

@@ -76,6 +76,13 @@ def main():
         codec.snappy_decompress_into(zb, lay, dst, st, dl, int(tot[1]), s)
         torch.cuda.synchronize()
         L.mtblx_snap_debug(dbg, 0)
+        if os.environ.get("MTBLX_SNAPPY_KERNEL") == "lanes":   # k_snappy_lanes' per-path counters
+            it = max(int(dbg[0]), 1)
+            names = ["iterations", "decode", "literal(window)", "literal(HBM)", "ring copy", "far copy",
+                     "overlapping copy", "window reload"]
+            print("lanes: wave iterations %d; share of iterations where any lane took: %s" % (
+                it, ", ".join("%s %.3f" % (names[k], dbg[k] / it) for k in range(1, 8))), flush=True)
+            return
         nb = max(int(dbg[5]), 1)
         print("per block: cycles %.0f  in flush %.0f  store %.0f  elements %.1f  flushes %.1f  restages %.2f  steps %.1f"
               % (dbg[0] / nb, dbg[1] / nb, dbg[2] / nb, dbg[3] / nb, dbg[4] / nb, dbg[6] / nb, dbg[7] / nb), flush=True)

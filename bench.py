@@ -263,7 +263,7 @@ def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
             "host_decompress_GiB_per_s_16_threads": round(block_bytes / t_dz / 2**30, 2),
             "device_resident_GiB_per_s": round(block_bytes / (dev_ms * 1e-3) / 2**30, 1)})
         res["cfg5_snappy_device_decompress"] = run(zdata, zoff, zln, 1, "cfg5-dz", {
-            "mode": "MTBLX_PIPE_DEVICE_SNAPPY: stored bytes H2D, k_snappy_blocks + decode on the device",
+            "mode": "MTBLX_PIPE_DEVICE_SNAPPY: stored bytes H2D, mtblx_snappy_decompress_dev + decode on the device",
             "device_resident_decompress_ms": round(dz_ms, 4),
             "device_resident_decompress_GiB_per_s": round(block_bytes / (dz_ms * 1e-3) / 2**30, 1),
             "device_resident_decompress_plus_decode_GiB_per_s": round(block_bytes / (both_ms * 1e-3) / 2**30, 1)},

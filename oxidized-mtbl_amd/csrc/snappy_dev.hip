@@ -1080,7 +1080,11 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
       v = ring_get(ring, t, d - es);
       LANE_PATH(4);
     } else {
+#ifdef MTBLX_LANE_ABL_NOFAR   // timing ablation only (wrong output): far copies read the ring
+      v = ring_get(ring, t, d - 16u);
+#else
       v = far16(d - es);
+#endif
       LANE_PATH(5);
     }
     if (first && ov) {

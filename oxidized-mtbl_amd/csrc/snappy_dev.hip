@@ -14,7 +14,13 @@
 //   a copy's offset is 1 .. bytes produced so far; nothing may run past the input or the
 //   stated length; the output must be exactly the stated length.
 //
-// Design (one wave per block; blocks are independent, so no cross-wave state):
+// Three kernels, chosen per call in mtblx_snappy_decompress_dev (blocks are independent):
+//  - k_snappy_quads: outputs <= 4.5 KiB, four blocks per wave, one LDS buffer per block;
+//  - k_snappy_lanes: in batches of >= 49 152 blocks, the blocks expanding > 2x, one LANE per
+//    block, output streamed to HBM through a per-lane LDS ring and writer waves;
+//  - k_snappy_blocks / k_snappy_deferred: larger outputs and what the quads leave, one wave per
+//    block, as below.
+// One-wave-per-block design:
 //  - the block's stored bytes are staged through an LDS window (coalesced 16-byte loads);
 //    the output is assembled in LDS (Small: <= 4.5 KiB out, 16 waves per CU; Large: <= 65 KiB
 //    out, 2 waves per CU) and streamed to HBM with 16-byte stores; larger outputs are

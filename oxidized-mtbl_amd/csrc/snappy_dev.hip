@@ -680,21 +680,19 @@ __global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, c
 // by ~1000 cycles of dependent latency per element: on compressible streams (~13 B per element)
 // that is 172 GB/s over 100 000 blocks.  Here every lane decodes its own block, so one vector
 // instruction advances 64 blocks and every block of the batch is in flight at once:
-//  - the element header comes from a 32-byte register window of the stored bytes, advanced 16
-//    bytes at a time with the next 16 loaded ahead;
-//  - every element's bytes go to the block's HBM slot in 16-byte stores, and into a 256-byte
-//    per-lane ring in LDS (64 words, word k of lane t at ring[k][t]: one bank per lane), from
-//    which copies with offsets up to kRingOff read their source -- no store -> load round trip
-//    through the L2 per element; longer offsets re-read the slot in HBM (a thread sees its own
-//    stores);
+//  - the element header and short literals come from a 48-byte register window of the stored
+//    bytes (two 16-byte chunks in use, the third loaded 16 bytes ahead);
+//  - the loop emits one chunk (<= 16 bytes) per iteration into a 256-byte per-lane ring in LDS
+//    (64 words, word k of lane t at ring[k][t]: one bank per lane), from which copies with
+//    offsets up to kRingOff read their source;
+//  - writer waves store the ring to the block's HBM slot (see below), and copies from further
+//    back read HBM once those stores are complete;
 //  - an overlapping copy (off < 16, off < L) starts with the off-byte period built by two byte
 //    permutes per word from a per-offset selector table; its chunk j >= 16 then reads the 16
 //    bytes at j - off2, off2 = off * ceil(16 / off) in [16, 16 + off): bytes already written, or
-//    the period's bytes before the element, which equal it;
-//  - a 16-byte store past the element is overwritten by the next element before any copy can
-//    read it (copies read produced bytes only); at the end of the slot (dst_len) stores are exact.
+//    the period's bytes before the element, which equal it.
 // All state is 32-bit (a block and its output are < 4 GiB).  Checks and statuses are the quad
-// kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.
+// kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.  DESIGN.md §4 has the measurements.
 namespace lanes {
 typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
 #ifndef MTBLX_LANE_THREADS   // decoding lanes per workgroup (as many writer lanes again)
@@ -793,8 +791,8 @@ __device__ __forceinline__ Q4 ring_get(const uint32_t (*R)[kThreads], int t, uin
 // decoder appends to its LDS ring and publishes its position (dpos); the writer copies whole
 // 16-byte chunks [fpos, dpos) from the ring to HBM and publishes fpos (issued) and fvis (stores
 // completed).  The decoder never overwrites ring words the writer has not taken (it waits on
-// fpos), and a copy whose source is beyond the ring (off > kRingOff) waits for fvis and reads HBM
-// with device-coherent loads.  LDS operations of one wave execute in order, so a position read
+// fpos), and a copy whose source is beyond the ring (off > kRingOff) waits for fvis to cover its
+// whole lines and reads HBM with a cached load (far16).  LDS operations of one wave execute in order, so a position read
 // from dpos / fpos covers every ring write / read issued before it.  Short literals come from the
 // register window (48 bytes: two in use, the third loaded 16 bytes ahead).
 constexpr uint32_t kRun = 0xFFFFFFFFu;   // dend while the decoder runs

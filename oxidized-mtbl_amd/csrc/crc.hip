@@ -174,7 +174,10 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = (ncu > 0 ? ncu : 256) * 2;   // 32 waves per CU
+#ifndef MTBLX_CRC_WG_PER_CU
+#define MTBLX_CRC_WG_PER_CU 2
+#endif
+    grid = (ncu > 0 ? ncu : 256) * MTBLX_CRC_WG_PER_CU;   // 98 VGPRs: one 1024-thread workgroup resident per CU
   }
   const uint32_t need = (in->nblk + 15u) / 16u;
   const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);

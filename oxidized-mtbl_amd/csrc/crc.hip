@@ -174,10 +174,12 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+// 98 VGPRs: one 1024-thread workgroup is resident per CU, so a grid of one workgroup per CU runs
+// in a single round; 2 per CU measured 0.1256-0.1261 ms against 0.1232 (profiles/r03/final2)
 #ifndef MTBLX_CRC_WG_PER_CU
-#define MTBLX_CRC_WG_PER_CU 2
+#define MTBLX_CRC_WG_PER_CU 1
 #endif
-    grid = (ncu > 0 ? ncu : 256) * MTBLX_CRC_WG_PER_CU;   // 98 VGPRs: one 1024-thread workgroup resident per CU
+    grid = (ncu > 0 ? ncu : 256) * MTBLX_CRC_WG_PER_CU;
   }
   const uint32_t need = (in->nblk + 15u) / 16u;
   const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);

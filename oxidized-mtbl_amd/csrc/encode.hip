@@ -38,6 +38,9 @@ constexpr int kWaves = kThreads / kWave;
 #ifndef MTBLX_ENC_LDS_BLOCK
 #define MTBLX_ENC_LDS_BLOCK (65536 + 1024)
 #endif
+#ifndef MTBLX_ENC_PERSIST   // persistent workgroups (2 per CU) looping over block tickets
+#define MTBLX_ENC_PERSIST 0
+#endif
 #ifndef MTBLX_ENC_WPE   // waves per SIMD the register budget is sized for
 #define MTBLX_ENC_WPE (kThreads / 128)
 #endif
@@ -457,8 +460,20 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   }
   if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
   __syncthreads();
+#if MTBLX_ENC_PERSIST
+  for (;;) {
+#endif
   const uint32_t b = S.sh_u32[0];
   if (b >= a.nblk) return;
+#if MTBLX_ENC_PERSIST
+  // claim the next block now: the ticket's round trip overlaps this block.  Tickets stay in
+  // claim order, so the lowest unfinished block is always being encoded (its look-back waits
+  // only on lower, finished blocks): no circular wait.
+  uint32_t next = 0;
+#if MTBLX_ENC_PERSIST == 1
+  if (tid == 0) next = atomicAdd(a.ticket, 1u);
+#endif
+#endif
   const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
   const uint32_t iv = a.interval;
   ESTAMP(2);   // tables + ticket
@@ -516,6 +531,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 
   // ---- look-back: this block's offset in the output ----
   if (w == 0) {
+#if MTBLX_ENC_PERSIST == 2   // claim the next block here: its round trip overlaps the look-back
+    if (tid == 0) next = atomicAdd(a.ticket, 1u);
+#endif
     bool to = false;
     const uint64_t excl = b == 0 ? 0 : lookback(a, b, lane, to);
     if (lane == 0) {
@@ -574,6 +592,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     if (st != MTBLX_ST_OK) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 1), 1ull);
     if (b == a.nblk - 1) a.totals[0] = pre + F;
   }
+#if MTBLX_ENC_PERSIST
+  __syncthreads();   // every wave is done with this block's LDS
+  if (tid == 0) S.sh_u32[0] = next;
+  __syncthreads();
+  }
+#endif
 }
 
 }  // namespace mtblx_enc
@@ -657,6 +681,17 @@ extern "C" int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk
             totals,
             reinterpret_cast<uint32_t*>(ws),
             reinterpret_cast<uint64_t*>(ws + 256)};
-  hipLaunchKernelGGL(k_encode, dim3(nblk), dim3(kThreads), 0, s, a);
+  uint32_t grid = nblk;
+#if MTBLX_ENC_PERSIST
+  static uint32_t resident = 0;   // 2 workgroups per CU (LDS)
+  if (!resident) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
+  }
+  if (grid > resident) grid = resident;
+#endif
+  hipLaunchKernelGGL(k_encode, dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -228,9 +228,14 @@ struct EncArgs {
   uint64_t* lbw;             // [nblk] look-back words
 };
 
+#ifndef MTBLX_ENC_CRC8   // slicing-by-8 for the block CRC: 16 dependent steps per 128 bytes, not 32
+#define MTBLX_ENC_CRC8 0
+#endif
+constexpr int kSlice = MTBLX_ENC_CRC8 ? 8 : 4;
+
 struct alignas(16) EncLds {
   uint8_t ob[kLdsBlock];
-  uint32_t T[4][256];        // slicing-by-4 CRC-32C tables
+  uint32_t T[kSlice][256];   // slicing-by-4 (-8) CRC-32C tables
   uint16_t shc[kShCache];    // phase A's `shared` of the first entries (0xFFFF: recompute)
   uint64_t red[kWaves];
   uint32_t redf[kWaves];
@@ -307,6 +312,14 @@ __device__ __forceinline__ uint32_t crc_word(const EncLds& S, uint32_t c, uint32
   return S.T[3][c & 0xffu] ^ S.T[2][(c >> 8) & 0xffu] ^ S.T[1][(c >> 16) & 0xffu] ^ S.T[0][c >> 24];
 }
 
+#if MTBLX_ENC_CRC8
+__device__ __forceinline__ uint32_t crc_dword(const EncLds& S, uint32_t c, uint32_t w0, uint32_t w1) {
+  const uint32_t x = c ^ w0;
+  return S.T[7][x & 0xffu] ^ S.T[6][(x >> 8) & 0xffu] ^ S.T[5][(x >> 16) & 0xffu] ^ S.T[4][x >> 24] ^
+         S.T[3][w1 & 0xffu] ^ S.T[2][(w1 >> 8) & 0xffu] ^ S.T[1][(w1 >> 16) & 0xffu] ^ S.T[0][w1 >> 24];
+}
+#endif
+
 __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t acc = 0;
@@ -320,10 +333,15 @@ __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
       uint64_t o = a0;
       for (; o + 16 <= a1; o += 16) {
         const v4u x = *reinterpret_cast<const v4u*>(d + o);
+#if MTBLX_ENC_CRC8
+        c = crc_dword(S, c, o == 0 ? x.x ^ 0xFFFFFFFFu : x.x, x.y);
+        c = crc_dword(S, c, x.z, x.w);
+#else
         c = crc_word(S, c, o == 0 ? x.x ^ 0xFFFFFFFFu : x.x);
         c = crc_word(S, c, x.y);
         c = crc_word(S, c, x.z);
         c = crc_word(S, c, x.w);
+#endif
       }
       for (; o < a1; ++o) {   // tail bytes (byte loads: never past the content)
         uint32_t byte = d[o];
@@ -449,11 +467,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   uint64_t tprev = __builtin_amdgcn_s_memtime();
 #endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < 256; i += kThreads) {   // slicing-by-4 tables from the byte table
+  for (int i = tid; i < 256; i += kThreads) {   // slicing tables from the byte table
     uint32_t t = mtblx_crc::kTab.byte[i];
     S.T[0][i] = t;
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < kSlice; ++k) {
       t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
       S.T[k][i] = t;
     }

@@ -19,6 +19,11 @@
 // content is computed from LDS and the block streams out with 16-byte stores.  Blocks larger
 // than the LDS buffer are assembled in place in HBM after the look-back.
 // All integer/byte work (HBM bound, no MFMA).
+// Round 3 variants, measured on cfg3 (2 x 200 000 blocks, profiles/r03/late, product 914-916
+// GiB/s) and removed: persistent workgroups (2 per CU) claiming the next block's ticket at the
+// block's start 900-901 / at the look-back 905-908 (the block loop raised scratch 48 -> 96-104
+// bytes per lane); the block CRC with slicing-by-8 tables (16 dependent steps per 128 bytes
+// instead of 32; 4 KiB more LDS) 882.  Earlier ones: profiles/r03/encode_gather.txt.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -37,9 +42,6 @@ constexpr int kThreads = MTBLX_ENC_THREADS;   // one workgroup per block, 2 per 
 constexpr int kWaves = kThreads / kWave;
 #ifndef MTBLX_ENC_LDS_BLOCK
 #define MTBLX_ENC_LDS_BLOCK (65536 + 1024)
-#endif
-#ifndef MTBLX_ENC_PERSIST   // persistent workgroups (2 per CU) looping over block tickets
-#define MTBLX_ENC_PERSIST 0
 #endif
 #ifndef MTBLX_ENC_WPE   // waves per SIMD the register budget is sized for
 #define MTBLX_ENC_WPE (kThreads / 128)
@@ -228,14 +230,9 @@ struct EncArgs {
   uint64_t* lbw;             // [nblk] look-back words
 };
 
-#ifndef MTBLX_ENC_CRC8   // slicing-by-8 for the block CRC: 16 dependent steps per 128 bytes, not 32
-#define MTBLX_ENC_CRC8 0
-#endif
-constexpr int kSlice = MTBLX_ENC_CRC8 ? 8 : 4;
-
 struct alignas(16) EncLds {
   uint8_t ob[kLdsBlock];
-  uint32_t T[kSlice][256];   // slicing-by-4 (-8) CRC-32C tables
+  uint32_t T[4][256];        // slicing-by-4 CRC-32C tables
   uint16_t shc[kShCache];    // phase A's `shared` of the first entries (0xFFFF: recompute)
   uint64_t red[kWaves];
   uint32_t redf[kWaves];
@@ -312,14 +309,6 @@ __device__ __forceinline__ uint32_t crc_word(const EncLds& S, uint32_t c, uint32
   return S.T[3][c & 0xffu] ^ S.T[2][(c >> 8) & 0xffu] ^ S.T[1][(c >> 16) & 0xffu] ^ S.T[0][c >> 24];
 }
 
-#if MTBLX_ENC_CRC8
-__device__ __forceinline__ uint32_t crc_dword(const EncLds& S, uint32_t c, uint32_t w0, uint32_t w1) {
-  const uint32_t x = c ^ w0;
-  return S.T[7][x & 0xffu] ^ S.T[6][(x >> 8) & 0xffu] ^ S.T[5][(x >> 16) & 0xffu] ^ S.T[4][x >> 24] ^
-         S.T[3][w1 & 0xffu] ^ S.T[2][(w1 >> 8) & 0xffu] ^ S.T[1][(w1 >> 16) & 0xffu] ^ S.T[0][w1 >> 24];
-}
-#endif
-
 __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t acc = 0;
@@ -333,15 +322,10 @@ __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
       uint64_t o = a0;
       for (; o + 16 <= a1; o += 16) {
         const v4u x = *reinterpret_cast<const v4u*>(d + o);
-#if MTBLX_ENC_CRC8
-        c = crc_dword(S, c, o == 0 ? x.x ^ 0xFFFFFFFFu : x.x, x.y);
-        c = crc_dword(S, c, x.z, x.w);
-#else
         c = crc_word(S, c, o == 0 ? x.x ^ 0xFFFFFFFFu : x.x);
         c = crc_word(S, c, x.y);
         c = crc_word(S, c, x.z);
         c = crc_word(S, c, x.w);
-#endif
       }
       for (; o < a1; ++o) {   // tail bytes (byte loads: never past the content)
         uint32_t byte = d[o];
@@ -467,31 +451,19 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   uint64_t tprev = __builtin_amdgcn_s_memtime();
 #endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < 256; i += kThreads) {   // slicing tables from the byte table
+  for (int i = tid; i < 256; i += kThreads) {   // slicing-by-4 tables from the byte table
     uint32_t t = mtblx_crc::kTab.byte[i];
     S.T[0][i] = t;
 #pragma unroll
-    for (int k = 1; k < kSlice; ++k) {
+    for (int k = 1; k < 4; ++k) {
       t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
       S.T[k][i] = t;
     }
   }
   if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
   __syncthreads();
-#if MTBLX_ENC_PERSIST
-  for (;;) {
-#endif
   const uint32_t b = S.sh_u32[0];
   if (b >= a.nblk) return;
-#if MTBLX_ENC_PERSIST
-  // claim the next block now: the ticket's round trip overlaps this block.  Tickets stay in
-  // claim order, so the lowest unfinished block is always being encoded (its look-back waits
-  // only on lower, finished blocks): no circular wait.
-  uint32_t next = 0;
-#if MTBLX_ENC_PERSIST == 1
-  if (tid == 0) next = atomicAdd(a.ticket, 1u);
-#endif
-#endif
   const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
   const uint32_t iv = a.interval;
   ESTAMP(2);   // tables + ticket
@@ -549,9 +521,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 
   // ---- look-back: this block's offset in the output ----
   if (w == 0) {
-#if MTBLX_ENC_PERSIST == 2   // claim the next block here: its round trip overlaps the look-back
-    if (tid == 0) next = atomicAdd(a.ticket, 1u);
-#endif
     bool to = false;
     const uint64_t excl = b == 0 ? 0 : lookback(a, b, lane, to);
     if (lane == 0) {
@@ -610,12 +579,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     if (st != MTBLX_ST_OK) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 1), 1ull);
     if (b == a.nblk - 1) a.totals[0] = pre + F;
   }
-#if MTBLX_ENC_PERSIST
-  __syncthreads();   // every wave is done with this block's LDS
-  if (tid == 0) S.sh_u32[0] = next;
-  __syncthreads();
-  }
-#endif
 }
 
 }  // namespace mtblx_enc
@@ -699,17 +662,6 @@ extern "C" int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk
             totals,
             reinterpret_cast<uint32_t*>(ws),
             reinterpret_cast<uint64_t*>(ws + 256)};
-  uint32_t grid = nblk;
-#if MTBLX_ENC_PERSIST
-  static uint32_t resident = 0;   // 2 workgroups per CU (LDS)
-  if (!resident) {
-    int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
-  }
-  if (grid > resident) grid = resident;
-#endif
-  hipLaunchKernelGGL(k_encode, dim3(grid), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(k_encode, dim3(nblk), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

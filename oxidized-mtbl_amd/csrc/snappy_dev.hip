@@ -947,6 +947,8 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
 #ifndef MTBLX_LANE_FAR_CACHED
 #define MTBLX_LANE_FAR_CACHED 1
 #endif
+  // (Round 3: a far copy's next chunk -- and a long literal's from HBM -- loaded one iteration
+  // ahead measured 346-348 GB/s against 354-355 (profiles/r03/late/snap_pf); not kept.)
   auto far16 = [&](uint32_t x) {
 #if MTBLX_LANE_FAR_CACHED
     // Wait until the writer's completed stores cover every 128-byte line the 16 bytes touch, then
@@ -993,15 +995,6 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
   bool elit = false;   // the current element is a literal: next bytes at stream position es
   uint32_t es = 0;     // literal: stream position; copy: source distance (d - source)
   bool fin = st != MTBLX_SNAPPY_OK || pos >= n;
-#ifndef MTBLX_LANE_FAR_PF
-#define MTBLX_LANE_FAR_PF 0
-#endif
-#if MTBLX_LANE_FAR_PF
-  // a far copy's next chunk (=2: also a literal's from HBM), loaded one iteration ahead: its
-  // latency overlaps this chunk's emission and the other lanes' work
-  Q4 pf;
-  bool pfv = false;
-#endif
 #ifdef MTBLX_SNAP_STAMPS
   // diagnostic: per wave iteration, whether any lane took each path:
   // [0] iterations [1] decode [2] literal from the window [3] literal from HBM [4] ring copy
@@ -1085,13 +1078,7 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
         v = win16(w8, lk & 15u);   // bytes past the literal are not used
         LANE_PATH(2);
       } else {
-#if MTBLX_LANE_FAR_PF >= 2   // a long literal's later chunks all come from HBM: one ahead too
-        v = pfv ? pf : ld16(s, n, es);
-        pfv = rem > 16u;
-        if (pfv) pf = ld16(s, n, es + 16u);
-#else
         v = ld16(s, n, es);
-#endif
         LANE_PATH(3);
       }
       es += 16u;
@@ -1101,10 +1088,6 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     } else {
 #ifdef MTBLX_LANE_ABL_NOFAR   // timing ablation only (wrong output): far copies read the ring
       v = ring_get(ring, t, d - 16u);
-#elif MTBLX_LANE_FAR_PF
-      v = pfv ? pf : far16(d - es);
-      pfv = rem > 16u;   // the element's next chunk is far too (same distance es > kRingOff)
-      if (pfv) pf = far16(d + 16u - es);
 #else
       v = far16(d - es);
 #endif

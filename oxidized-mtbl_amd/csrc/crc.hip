@@ -17,7 +17,10 @@
 
 namespace mtblx_crc {
 
-constexpr int kCrcThreads = 1024;   // 16 waves per workgroup, 2 workgroups per CU (LDS: 48 KiB each)
+#ifndef MTBLX_CRC_THREADS
+#define MTBLX_CRC_THREADS 1024
+#endif
+constexpr int kCrcThreads = MTBLX_CRC_THREADS;   // 16 waves per workgroup (LDS: 48 KiB each)
 
 // Slicing-by-8 tables: T8[k][i] = CRC of byte i followed by k zero bytes.
 struct Slice8 {
@@ -181,7 +184,8 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
 #endif
     grid = (ncu > 0 ? ncu : 256) * MTBLX_CRC_WG_PER_CU;
   }
-  const uint32_t need = (in->nblk + 15u) / 16u;
+  const uint32_t wpg = mtblx_crc::kCrcThreads / mtblx_crc::kWave;   // waves (blocks in flight) per workgroup
+  const uint32_t need = (in->nblk + wpg - 1u) / wpg;
   const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);
   hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, g, t, 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
                      in->blk_off, in->blk_len, in->nblk, crc, bad, framed);

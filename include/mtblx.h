@@ -45,7 +45,9 @@ extern "C" {
                                  its outputs were discarded (synchronous entry points only)  */
 #define MTBLX_E_IO (-6)       /* the writer's compressor returned Err (Writer::insert / into_inner's
                                  io::Error: Lz4 / Lz4hc "unsupported", src/compression.rs:70-81;
-                                 a codec failure); nothing was written, the writer is unchanged */
+                                 a codec failure); nothing was written, but the records of the
+                                 block being flushed are lost and the next insert fails (the
+                                 reference's BlockBuilder::finish already ran, :85-104)       */
 
 /* ---- per-block status (status[b]) ----
  * Exact correspondence with the reference's behaviour on the same bytes:         */
@@ -189,14 +191,32 @@ int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int veri
               uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
               uint64_t* val_off, uint64_t* val_len, void* stream);
 
+/* The same for a compressed file (Snappy / Zlib / Zstd: the crate's decompress step of
+ * Reader::block, src/reader.rs:166-170).  Framing and the checksum stay on the stored bytes in
+ * `file`; the blocks are scanned in their decompressed form, which the caller provides (the
+ * host codecs, mtblx_decompress_blocks, or the device snappy): a table of ntab blocks sorted by
+ * tab_start = the file offset of the stored content (Reader::block's raw_start), whose content
+ * is dec[tab_doff[i] .. + tab_dlen[i]) when tab_st[i] == 0, and Err(Io) otherwise (the
+ * crate's decompress error; reported like Err(InvalidBlock)).  A stored block missing from the
+ * table is treated as Err(Io).  val_off of FOUND is an offset into `dec`. */
+int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
+                           uint64_t index_off, uint64_t index_len, const uint64_t* tab_start,
+                           const uint64_t* tab_doff, const uint64_t* tab_dlen, const int32_t* tab_st, uint32_t ntab,
+                           const uint8_t* dec, const uint8_t* keys, const uint64_t* key_end, uint32_t nq,
+                           int32_t* status, uint64_t* val_off, uint64_t* val_len, void* stream);
+
 /* ---- seek-based iteration (ReaderIntoIter::new_from / seek, src/reader.rs:256-335) ----
  * Three device primitives; the host drives the iterator state (block_offset quirk, first /
  * valid, index position) exactly as src/reader.rs:219-405 does, and decodes the blocks after
  * the sought one with mtblx_decode_blocks -- only the blocks the iteration touches.
  *
  * (1) index_iter.seek(key) + the landed entry's block_at_index / Reader::block
- *     (src/block.rs:154-194, src/reader.rs:139-186), one wave per query, on a fresh index
- *     iterator.  All fields are outputs. */
+ *     (src/block.rs:154-194, src/reader.rs:139-186), one wave per query, starting from a fresh
+ *     index iterator.  ReaderIntoIter::seek re-seeks its LIVE index iterator (:303); from a
+ *     regular index block (mtblx_entry_offsets) every start lands on the same entry, so the
+ *     drivers use this primitive there, and otherwise seek the index block itself with
+ *     mtblx_block_seek_batch from the live iterator's state and key capacity
+ *     (mtblx/iterator.py, include/mtbl.hpp ReaderIntoIter).  All fields are outputs. */
 #define MTBLX_SEEK_OK 0
 #define MTBLX_SEEK_ERR 1          /* Err(InvalidBlock) from Block::init                       */
 #define MTBLX_SEEK_PANIC 2        /* the reference panics                                     */

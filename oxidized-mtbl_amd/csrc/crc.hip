@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include "crc_dev.h"
+#include "crc_mfma.h"
 #include "mtblx.h"
 
 namespace mtblx_crc {
@@ -154,6 +155,352 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_crc32c_mfma: the same checksum on the matrix cores (crc_mfma.h has the method and the
+// operand layout).  Persistent: wave w takes the contiguous blocks [nblk w / W, nblk (w + 1) / W)
+// one at a time and reads each one contiguously, a STEP of 16 consecutive 128-byte windows (2 KiB) at a time,
+// counted from the block's END (window w = bytes [L - 128 (w + 1), L - 128 w)), so one set of
+// shift matrices serves every block length; bytes before the block start are zero and the
+// 0xFFFFFFFF init is folded into bytes 0..3.  Lane (g = lane >> 4, n = lane & 15) feeds 32 bytes
+// of window n of the step.  The steps reach the lanes through a per-wave LDS ring filled by
+// LDS-DMA kRing - 1 steps ahead, across block boundaries.  Per step: 4 vector instructions per
+// loaded dword (the fp4 bit planes), 16 MFMAs, 17 to pack the stage-2 operand; per 4 steps 2
+// MFMAs; per block a parity extraction, the column shifts and a 16-lane XOR.
+// ---------------------------------------------------------------------------------------------
+static __constant__ MfmaTabs kMfma = MfmaTabs();
+static_assert(MfmaTabs().max_row < 1024, "stage-1 sums must stay below 2^10 for the bit-12 parity");
+
+// MTBLX_CRC_ABL=1 (diagnostic, wrong checksums by construction): the ring without stage 1/2
+#if defined(MTBLX_CRC_ABL) && !defined(MTBLX_DIAG)
+#error "MTBLX_CRC_ABL is an ablation: build it only through a diagnostic target (-DMTBLX_DIAG)"
+#endif
+#ifndef MTBLX_CRC_ABL
+#define MTBLX_CRC_ABL 0
+#endif
+constexpr int kMThreads = 512;                 // 8 waves, one workgroup per CU (160 KiB of LDS)
+constexpr int kMWaves = kMThreads / kWave;
+constexpr int kRing = 8;                       // steps per wave ring (16 KiB)
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ v4f mfma_fp4(v4i a, v4i b, v4f c) {
+  const v8i a8 = {a.x, a.y, a.z, a.w, 0, 0, 0, 0};
+  const v8i b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 4, 4, 0, 0, 0, 0);
+}
+
+// parity of an exact integer-valued sum v (0 <= v < 2^(22 - k)) at bit k: v + 1.5·2^(23-k) keeps
+// v · 2^k in the low mantissa bits
+__device__ __forceinline__ uint32_t par_bits(float v, float magic) { return __float_as_uint(v + magic); }
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (mask & a) | (~mask & b); }
+constexpr float kMag0 = 12582912.0f, kMag4 = 786432.0f, kMag8 = 49152.0f, kMag12 = 3072.0f;
+
+// stage-2 operand dword of one step: parity of C1[h][i] at bit 16 h + 4 i
+__device__ __forceinline__ uint32_t pack_window(v4f lo, v4f hi) {
+  uint32_t x = par_bits(lo.x, kMag0) & 1u;
+  x = bfi(1u << 4, par_bits(lo.y, kMag4), x);
+  x = bfi(1u << 8, par_bits(lo.z, kMag8), x);
+  x = bfi(1u << 12, par_bits(lo.w, kMag12), x);
+  uint32_t y = par_bits(hi.x, kMag0) & 1u;
+  y = bfi(1u << 4, par_bits(hi.y, kMag4), y);
+  y = bfi(1u << 8, par_bits(hi.z, kMag8), y);
+  y = bfi(1u << 12, par_bits(hi.w, kMag12), y);
+  return x | (y << 16);
+}
+
+struct RingSlot {   // one step: its 128 16-byte chunks, lowest address first
+  v4u c[128];
+};
+
+// The block's first bytes: a step's chunks lie at block positions a = sb + 16 k, 16-byte aligned
+// in memory while the block is not.  A chunk wholly before the block is zeroed (its DMA read
+// the block's first aligned chunk instead); the chunk holding byte 0 keeps bytes >= 0 only; the
+// 0xFFFFFFFF init is folded into bytes 0..3 (one or two chunks).  a is in [-2048, 2048) here.
+__device__ __forceinline__ uint32_t head_dword(uint32_t w, int pos) {
+  if (pos >= 4) return w;
+  const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+  const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8 * (uint32_t)pos);
+  return (w & keep) ^ fold;
+}
+__device__ __forceinline__ v4u head_chunk(v4u x, int a) {
+  if (a <= -16) return v4u{0u, 0u, 0u, 0u};
+  if (a >= 4) return x;
+  return v4u{head_dword(x.x, a), head_dword(x.y, a + 4), head_dword(x.z, a + 8), head_dword(x.w, a + 12)};
+}
+// the pad after the block's end: t < 16 zero bytes in the step's last chunk (chunk 127 of step 0)
+__device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
+  const uint32_t k = 16u - t;   // bytes kept
+  const auto m = [&](uint32_t d) {
+    return k >= 4 * d + 4 ? 0xFFFFFFFFu : (k <= 4 * d ? 0u : 0xFFFFFFFFu >> (8 * (4 * d + 4 - k)));
+  };
+  return v4u{y.x & m(0), y.y & m(1), y.z & m(2), y.w & m(3)};
+}
+
+// s_waitcnt vmcnt(2k): a step has landed once at most the 2k DMA instructions of the k steps
+// issued after it are outstanding (other vector-memory operations of the wave only make the
+// wait stricter: the counter retires in issue order)
+__device__ __forceinline__ void wait_ring(uint32_t k) {
+  switch (k) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+  }
+}
+static_assert(kRing == 8, "wait_ring covers kRing - 1 = 7 steps ahead");
+
+// the lane's two chunks of a landed slot.  Inline asm: the compiler treats an LDS read it can see
+// as aliasing every LDS-DMA in flight and waits vmcnt(0) before it, which would drain the ring;
+// wait_ring has already waited for exactly this slot's DMA.
+__device__ __forceinline__ void ring_read(const RingSlot* sl, uint32_t kx, v4u& x, v4u& y) {
+  const uint32_t ax = (uint32_t)(uintptr_t)(const lds_void*)&sl->c[kx];
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x), "=&v"(y)
+               : "v"(ax)
+               : "memory");
+}
+
+// serial CRC-32C of a short block (< 4 bytes), one lane
+__device__ __forceinline__ uint32_t crc_tiny(const uint8_t* d, uint64_t L) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (uint64_t i = 0; i < L; ++i) c = kTab.byte[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+__device__ __forceinline__ void crc_store(const uint8_t* d, uint64_t off, bool oob, uint32_t c, uint32_t b,
+                                          uint32_t* crc_out, uint8_t* bad, int framed) {
+  if (crc_out) crc_out[b] = oob ? 0u : c;
+  if (bad) {
+    if (oob) {
+      bad[b] = 1;   // the window runs past the buffer: the reference's slice panics
+    } else {
+      uint32_t stored = 0;
+      if (framed && off >= 4)
+        stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
+      bad[b] = (framed && off >= 4) ? (uint8_t)(stored != c) : (uint8_t)0;
+    }
+  }
+}
+
+// a block of the stream (wave-uniform values)
+struct MBlk {
+  uint64_t off;     // block offset in the buffer
+  int64_t L;        // content length
+  int64_t Lp;       // L + t: padded to a 16-byte aligned end address
+  uint32_t t;       // pad bytes, < 16
+  uint32_t steps;   // ceil(Lp / 2 KiB)
+  int64_t a0;       // block position of the 16-byte aligned chunk holding byte 0 (in [-15, 0])
+};
+__device__ __forceinline__ MBlk mblk(uint64_t base, uint64_t off, uint64_t L) {
+  MBlk m;
+  m.off = off;
+  m.L = (int64_t)L;
+  m.t = (uint32_t)((16u - ((base + off + L) & 15u)) & 15u);
+  m.Lp = m.L + m.t;
+  m.steps = (uint32_t)((m.Lp + kMStep - 1) / kMStep);
+  m.a0 = -(int64_t)((base + off) & 15u);
+  return m;
+}
+
+__global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __restrict__ data, uint64_t data_len,
+                                                             const uint64_t* __restrict__ blk_off,
+                                                             const uint32_t* __restrict__ blk_len, uint32_t nblk,
+                                                             uint32_t* __restrict__ crc_out, uint8_t* __restrict__ bad,
+                                                             int framed) {
+  __shared__ v4i sA2[8 * 2 * 64];              // 16 KiB: stage-2 operands
+  __shared__ uint32_t sCol[16][8][16];         // 8 KiB: column shifts
+  __shared__ uint32_t sInv[16][8][16];         // 8 KiB: pad removal
+  __shared__ RingSlot sRing[kMWaves][kRing];   // 128 KiB
+  const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {
+    const v4i* a2 = reinterpret_cast<const v4i*>(&kMfma.a2[0][0][0][0]);
+    for (int i = threadIdx.x; i < 8 * 2 * 64; i += kMThreads) sA2[i] = a2[i];
+    for (int i = threadIdx.x; i < 16 * 8 * 16; i += kMThreads) {
+      (&sCol[0][0][0])[i] = (&kMfma.col[0][0][0])[i];
+      (&sInv[0][0][0])[i] = (&kMfma.inv[0][0][0])[i];
+    }
+  }
+  v4i A[8][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    A[t][0] = reinterpret_cast<const v4i*>(&kMfma.a[t][0][0][0])[lane];
+    A[t][1] = reinterpret_cast<const v4i*>(&kMfma.a[t][1][0][0])[lane];
+  }
+  // use A here, so the wait for its loads is placed before the loop: left to its first use
+  // inside the loop, the wait would be a vmcnt(0) in every iteration, draining the ring
+#pragma unroll
+  for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(A[t][0]), "v"(A[t][1]));
+  __syncthreads();
+  RingSlot* ring = sRing[wv];
+  const uint64_t base = (uint64_t)(uintptr_t)data;
+  const uint32_t W = gridDim.x * kMWaves;
+  const uint32_t w0 = blockIdx.x * kMWaves + wv;
+  const uint32_t kx = 120u - 8u * (uint32_t)n + (uint32_t)g;   // the lane's first chunk of a step
+
+  // the wave's blocks w0 + k W, 64 at a time: lane j holds block k = 64 m + j of window m
+  for (uint64_t kb = 0; w0 + kb * W < nblk; kb += kWave) {
+    const uint64_t bi = w0 + (kb + (uint64_t)lane) * W;
+    const bool valid = bi < nblk;
+    uint64_t off = 0, L = 0;
+    if (valid) {
+      off = blk_off[bi];
+      L = blk_len[bi];
+    }
+    const bool oob = valid && off + L > data_len;
+    // the MFMA path: whole 16-byte aligned chunks around the block inside the buffer, L >= 4
+    const bool elig = valid && !oob && L >= 4 && ((base + off) & ~15ull) >= base &&
+                      ((base + off + L + 15u) & ~15ull) <= base + data_len;
+    const uint64_t em = __ballot(elig);
+    uint32_t res = 0;   // lane j: the checksum of block j of the window
+
+    // issue cursor: step is of block ij;   compute cursor: step cs of block cj
+    uint64_t irest = em;
+    uint32_t is = 0, issued = 0, done = 0;
+    MBlk I{};
+    bool ilive = irest != 0;
+    if (ilive) {
+      const int j = __builtin_ctzll(irest);
+      irest &= irest - 1;
+      I = mblk(base, (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32),
+               (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, j));
+    }
+    auto issue = [&]() {
+      RingSlot* sl = ring + (issued % kRing);
+      const int64_t sb = I.Lp - (int64_t)kMStep * (is + 1);      // block position of chunk 0
+      const int64_t px = sb + 16 * lane, py = px + 16 * kWave;
+      // chunks wholly before the block load its first aligned chunk instead (zeroed on read)
+      const uint8_t* p = data + I.off + (px + 16 > 0 ? px : I.a0);
+      const uint8_t* q = data + I.off + (py + 16 > 0 ? py : I.a0);
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)&sl->c[0], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(q, (lds_void*)&sl->c[kWave], 16, 0, 0);
+      ++issued;
+      if (++is == I.steps) {
+        is = 0;
+        ilive = irest != 0;
+        if (ilive) {
+          const int j = __builtin_ctzll(irest);
+          irest &= irest - 1;
+          I = mblk(base, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32),
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, j));
+        }
+      }
+    };
+    while (ilive && issued < (uint32_t)(kRing - 1)) issue();
+
+    uint64_t crest = em;
+    MBlk Cb{};
+    int cj = 0;
+    bool clive = crest != 0;
+    auto cnext = [&]() {
+      clive = crest != 0;
+      if (clive) {
+        cj = __builtin_ctzll(crest);
+        crest &= crest - 1;
+        Cb = mblk(base, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, cj) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), cj) << 32),
+                  (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, cj));
+      }
+    };
+    cnext();
+    uint32_t cs = 0, acc = 0;
+    v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
+    v4i bb = {0, 0, 0, 0};   // stage-2 operand: dword d = step 4 jq + d of the quad (shifted in)
+    while (clive) {
+      if (ilive && issued - done < (uint32_t)kRing) issue();
+      wait_ring(issued - done - 1 < (uint32_t)(kRing - 1) ? issued - done - 1 : (uint32_t)(kRing - 1));
+      v4u x, y;
+      ring_read(ring + (done % kRing), kx, x, y);
+      ++done;
+      const int64_t sb = Cb.Lp - (int64_t)kMStep * (cs + 1);
+      if (cs == 0 && Cb.t != 0 && lane == 48) y = tail_chunk(y, Cb.t);   // lane (g 3, n 0): chunk 127
+      if (sb < 4) {   // the step holds the block's first bytes (sb >= -2047: 32-bit positions)
+        const int a = (int)sb + 16 * (int)kx;
+        x = head_chunk(x, a);
+        y = head_chunk(y, a + 64);
+      }
+#if MTBLX_CRC_ABL == 1
+      acc ^= x.x ^ x.y ^ x.z ^ x.w ^ y.x ^ y.y ^ y.z ^ y.w;
+#else
+      const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      v4f c1a = {0.f, 0.f, 0.f, 0.f}, c1b = c1a;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t v = w[t];
+        const v4i b = {(int)(v & 0x11111111u), (int)(v & 0x22222222u), (int)(v & 0x44444444u),
+                       (int)((v >> 1) & 0x44444444u)};
+        c1a = mfma_fp4(A[t][0], b, c1a);
+        c1b = mfma_fp4(A[t][1], b, c1b);
+      }
+      bb = v4i{bb.y, bb.z, bb.w, (int)pack_window(c1a, c1b)};
+#endif
+      const bool last = cs + 1 == Cb.steps;
+      if ((cs & 3u) == 3u || last) {
+        for (uint32_t r = cs & 3u; r < 3u; ++r) bb = v4i{bb.y, bb.z, bb.w, 0};   // a partial last quad
+        const uint32_t jq = (cs >> 2) & 7u;
+        c2a = mfma_fp4(sA2[(2 * jq) * 64 + lane], bb, c2a);
+        c2b = mfma_fp4(sA2[(2 * jq + 1) * 64 + lane], bb, c2b);
+        bb = v4i{0, 0, 0, 0};
+        if (jq == 7u || last) {   // super-window done: each column's raw CRC, shifted into place
+          uint32_t dv = 0;
+          const uint32_t sh = 4u * (uint32_t)g;
+          dv |= (par_bits(c2a.x, kMag0) & 1u) << (sh + 0);
+          dv |= (par_bits(c2a.y, kMag0) & 1u) << (sh + 1);
+          dv |= (par_bits(c2a.z, kMag0) & 1u) << (sh + 2);
+          dv |= (par_bits(c2a.w, kMag0) & 1u) << (sh + 3);
+          dv |= (par_bits(c2b.x, kMag0) & 1u) << (sh + 16);
+          dv |= (par_bits(c2b.y, kMag0) & 1u) << (sh + 17);
+          dv |= (par_bits(c2b.z, kMag0) & 1u) << (sh + 18);
+          dv |= (par_bits(c2b.w, kMag0) & 1u) << (sh + 19);
+          const uint32_t S = cs >> 5;
+          if (S == 0) acc ^= dv;
+          else if (S < 16) acc ^= mul_nib(dv, kMfma.sw[S]);
+          else acc ^= dmultmodp(xpow8((uint64_t)S * (uint64_t)(kMStep * kMSup)), dv);
+          c2a = v4f{0.f, 0.f, 0.f, 0.f};
+          c2b = c2a;
+        }
+      }
+      if (!last) {
+        ++cs;
+        continue;
+      }
+      // block done: column shifts, XOR over all 64 lanes (each holds its 8 of a column's 32 bits)
+      uint32_t c = mul_nib(acc, sCol[n]);
+#pragma unroll
+      for (int sh = 1; sh < 64; sh <<= 1) c ^= (uint32_t)__shfl_xor((int)c, sh, kWave);
+      c = mul_nib(c, sInv[Cb.t]) ^ 0xFFFFFFFFu;
+      if (lane == cj) res = c;
+      acc = 0;
+      cs = 0;
+      cnext();
+    }
+    // blocks the MFMA path does not take: < 4 bytes, windows past the buffer, unaligned chunks
+    // outside it (a block at the very start / end of an unaligned buffer)
+    uint64_t todo = __ballot(valid && !elig && !oob);
+    while (todo) {
+      const int src = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint64_t bo = (uint64_t)__shfl((long long)off, src, kWave);
+      const uint64_t bl = (uint64_t)__shfl((long long)L, src, kWave);
+      uint32_t c = 0;
+      if (bl >= 4) c = wave_crc32c(data + bo, bl, kTab.byte, lane);
+      else if (lane == 0) c = crc_tiny(data + bo, bl);
+      c = (uint32_t)__shfl((int)c, 0, kWave);
+      if (lane == src) res = c;
+    }
+    if (valid) crc_store(data + off, off, oob, res, (uint32_t)bi, crc_out, bad, framed);
+  }
+}
+
 // Round 3 variants, measured on the cfg2 batch (scripts/crc_ab.py, HIP events, two alternations,
 // profiles/r03/crc_ab.txt) and removed -- all slower than k_crc32c_blocks (0.124-0.126 ms):
 //   1 / 2  the first window loaded one block ahead; slicing-by-8 / slicing-by-72 (72
@@ -172,6 +519,23 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   if (!in || (!crc && !bad && in->nblk)) return MTBLX_E_INVAL;
   if (in->nblk == 0) return MTBLX_OK;
   if (!in->data || !in->blk_off || !in->blk_len) return MTBLX_E_INVAL;
+  // MTBLX_CRC_KERNEL=mfma: the matrix-core kernel (bit-exact; not yet faster than the VALU
+  // table kernel on cfg2), else k_crc32c_blocks
+  const char* kv = getenv("MTBLX_CRC_KERNEL");
+  if (kv && kv[0] == 'm') {
+    static int mgrid = 0;   // persistent: one 8-wave workgroup (152 KiB LDS) per CU
+    if (!mgrid) {
+      int dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      mgrid = ncu > 0 ? ncu : 256;
+    }
+    const uint32_t need = (in->nblk + mtblx_crc::kMWaves - 1u) / mtblx_crc::kMWaves;
+    const dim3 g(need < (uint32_t)mgrid ? need : (uint32_t)mgrid), t(mtblx_crc::kMThreads);
+    hipLaunchKernelGGL(mtblx_crc::k_crc32c_mfma, g, t, 0, reinterpret_cast<hipStream_t>(stream), in->data,
+                       in->data_len, in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
+    return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+  }
   static int grid = 0;
   if (!grid) {
     int dev = 0, ncu = 0;

@@ -182,8 +182,10 @@ struct mtblx_writer {
   // write_block (:203-237): data blocks are compressed with the file's compression type
   // (:214), the index block never (into_inner passes CompressionType::None, :165-173); the
   // checksum covers the STORED bytes (:217-218).  A compressor Err (Lz4 / Lz4hc: "unsupported",
-  // src/compression.rs:70-81; a codec failure) returns at the `?` of :214: nothing is written
-  // and the block is not reset, so the writer stays as it was (MTBLX_E_IO).
+  // src/compression.rs:70-81; a codec failure) returns at the `?` of :214 (MTBLX_E_IO) after
+  // BlockBuilder::finish has already taken the block's bytes and set `finished`
+  // (src/block_builder.rs:85-104): nothing is written, the pending block's records are lost, and
+  // the next insert panics on the builder's !finished assert -- as the reference does.
   int write_block(BlockBuilder& b, bool is_data, uint64_t& written) {
     b.finish(scratch);
     const std::vector<uint8_t>* stored = &scratch;
@@ -246,7 +248,7 @@ extern "C" int mtblx_writer_insert(mtblx_writer* w, const uint8_t* k, uint64_t k
   }
   if (w->data.estimate() + 15 + kl + vl >= w->meta[1]) {  // (:125-130)
     const int r = w->flush();
-    if (r == MTBLX_E_IO) return r;   // Err: this record is not inserted, the writer is unchanged
+    if (r == MTBLX_E_IO) return r;   // Err: this record is not inserted; the flushed block is lost
     if (r != MTBLX_OK) { w->poisoned = true; return r; }
   }
   if (w->pending_index_entry) {  // (:132-138)

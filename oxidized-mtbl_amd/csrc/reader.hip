@@ -263,6 +263,16 @@ __device__ __forceinline__ int iter_init(const Blk& b, It& it) {
   return R_OK;
 }
 
+// decompressed blocks of a compressed file (mtblx_get_decompressed), sorted by stored start
+struct DecTab {
+  const uint64_t* start;
+  const uint64_t* doff;
+  const uint64_t* dlen;
+  const int32_t* st;
+  uint32_t n;
+  const uint8_t* dec;
+};
+
 struct FileCtx {
   const uint8_t* file;
   uint64_t len;
@@ -270,6 +280,7 @@ struct FileCtx {
   int verify;
   const uint32_t* T;   // crc byte table (LDS)
   int lane;
+  DecTab tab;          // tab.dec == nullptr: the file is not compressed
 };
 
 // block_at_index + Reader::block (src/reader.rs:177-186, :139-174):
@@ -292,14 +303,26 @@ __device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk
   const uint64_t start = off + ll + 4;
   if (start > f.len || sz > f.len - start) return R_PANIC;
   if (f.verify && mtblx_crc::wave_crc32c(f.file + start, sz, f.T, f.lane) != rd32g(f.file + off + ll)) return R_PANIC;
-  const int bi = block_init(f.file + start, sz, out);
+  const uint8_t* content = f.file + start;
+  if (f.tab.dec) {   // decompress (src/reader.rs:166-170): the caller's decompressed copy
+    uint32_t lo = 0, hi = f.tab.n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (f.tab.start[mid] < start) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == f.tab.n || f.tab.start[lo] != start || f.tab.st[lo] != 0) return 2;   // Err(Io)
+    content = f.tab.dec + f.tab.doff[lo];
+    sz = f.tab.dlen[lo];
+  }
+  const int bi = block_init(content, sz, out);
   if (bi == 1) return 2;
   if (bi < 0) return R_PANIC;
   return 1;
 }
 
 __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
-                                             uint64_t idx_off, uint64_t idx_len, const uint8_t* qkeys,
+                                             uint64_t idx_off, uint64_t idx_len, DecTab tab, const uint8_t* qkeys,
                                              const uint64_t* qend, uint32_t nq, int32_t* st, uint64_t* voff,
                                              uint64_t* vlen) {
   __shared__ uint32_t T[256];
@@ -307,7 +330,8 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const uint32_t waves = gridDim.x * (blockDim.x / 64);
-  const FileCtx f{file, file_len, version, verify, T, lane};
+  const FileCtx f{file, file_len, version, verify, T, lane, tab};
+  const uint8_t* vbase = tab.dec ? tab.dec : file;   // values are offsets into the scanned bytes
   for (uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); q < nq; q += waves) {
     const uint64_t k0 = q ? qend[q - 1] : 0, k1 = qend[q];
     const uint8_t* t = qkeys + k0;
@@ -333,7 +357,7 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
       // next() (first call, Get)
       if (valid(db, di)) {
         if (di.voff + di.vlen > db.L) { res = MTBLX_GET_PANIC; break; }
-        if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - file) + di.voff; rl = di.vlen; }
+        if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
         break;
       }
       // the seek ran past the end of the block: the next index entry's first record
@@ -350,7 +374,7 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
         // reassigned on Err, src/reader.rs:111-122, :376-379): its `val` is the last entry the
         // seek parsed -> Ok(Some(that value)), or Ok(None) if the seek parsed none (:195-203).
         // block_at_index left db untouched (Block::init failed before assigning it).
-        if (di.has_val) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - file) + di.voff; rl = di.vlen; }
+        if (di.has_val) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
         break;
       }
       if (b == 0) break;
@@ -360,7 +384,7 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
       if (r == R_PANIC) { res = MTBLX_GET_PANIC; break; }
       if (!valid(db, di)) break;
       if (di.voff + di.vlen > db.L) { res = MTBLX_GET_PANIC; break; }
-      if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - file) + di.voff; rl = di.vlen; }
+      if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
     } while (false);
     if (lane == 0) { st[q] = res; voff[q] = ro; vlen[q] = rl; }
   }
@@ -789,8 +813,33 @@ extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t versio
   }
   const uint32_t need = (nq + 3u) / 4u;
   hipLaunchKernelGGL(mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len, keys,
-                     key_end, nq, status, val_off, val_len);
+                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
+                     mtblx_rd::DecTab{nullptr, nullptr, nullptr, nullptr, 0u, nullptr}, keys, key_end, nq, status,
+                     val_off, val_len);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
+                                      uint64_t index_off, uint64_t index_len, const uint64_t* tab_start,
+                                      const uint64_t* tab_doff, const uint64_t* tab_dlen, const int32_t* tab_st,
+                                      uint32_t ntab, const uint8_t* dec, const uint8_t* keys, const uint64_t* key_end,
+                                      uint32_t nq, int32_t* status, uint64_t* val_off, uint64_t* val_len,
+                                      void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!file || !keys || !key_end || !status || !val_off || !val_len || version > 1 || !dec) return MTBLX_E_INVAL;
+  if (ntab && (!tab_start || !tab_doff || !tab_dlen || !tab_st)) return MTBLX_E_INVAL;
+  static int grid = 0;
+  if (!grid) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = (ncu > 0 ? ncu : 256) * 8;
+  }
+  const uint32_t need = (nq + 3u) / 4u;
+  hipLaunchKernelGGL(mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
+                     mtblx_rd::DecTab{tab_start, tab_doff, tab_dlen, tab_st, ntab, dec}, keys, key_end, nq, status,
+                     val_off, val_len);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
 

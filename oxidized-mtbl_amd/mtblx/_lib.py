@@ -29,7 +29,7 @@ EMIT_END, EMIT_PANIC, EMIT_LOOP, EMIT_MAX, EMIT_OVERFLOW = range(5)
 # every symbol the public headers declare (checked by tests/test_abi.py)
 EXPORTS = [
     "mtblx_abi_version", "mtblx_device_ok", "mtblx_decode_workspace_bytes", "mtblx_decode_blocks",
-    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_decode_blocks_verify", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_get", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
+    "mtblx_count_blocks", "mtblx_decode_counted", "mtblx_decode_blocks_verify", "mtblx_crc32c_blocks", "mtblx_block_dir", "mtblx_get", "mtblx_get_decompressed", "mtblx_crc32c", "mtblx_varint_decode64", "mtblx_read_footer", "mtblx_frame_block",
     "mtblx_writer_new", "mtblx_writer_insert", "mtblx_writer_insert_batch", "mtblx_writer_finish",
     "mtblx_writer_block_count", "mtblx_writer_block_dir", "mtblx_writer_free", "mtblx_free",
     "mtblx_snappy_max_compressed_len", "mtblx_snappy_uncompressed_len", "mtblx_snappy_decompress",
@@ -120,6 +120,11 @@ def lib() -> C.CDLL:
         L.mtblx_get.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p,
                                 C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.mtblx_get.restype = C.c_int
+        L.mtblx_get_decompressed.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint64,
+                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
+        L.mtblx_get_decompressed.restype = C.c_int
         L.mtblx_crc32c.argtypes = [u8p, C.c_uint64]
         L.mtblx_crc32c.restype = C.c_uint32
         L.mtblx_varint_decode64.argtypes = [u8p, C.c_uint64, u64p]

@@ -406,12 +406,35 @@ class Reader:
         return "ok", em
 
     # ------------------------------------------------------------------ point queries
+    def _dec_table(self):
+        """Every data block the directory frames, decompressed on the host (Reader::block's
+        decompress step, src/reader.rs:166-170), on the device, with the table
+        mtblx_get_decompressed takes: sorted by stored content start."""
+        if getattr(self, "_dtab", None) is None:
+            off, ln, st = self._framing()
+            buf, doff, dlen, zerr = self._host_stage(off, ln, st)
+            start = off.cpu().numpy().view(np.uint64)
+            ok = st.cpu().numpy() == _lib.DIR_OK
+            start, doff, dlen = start[ok], doff[ok], dlen[ok]
+            zst = zerr[ok].astype(np.int32)
+            order = np.argsort(start, kind="stable")
+            dev = self.file.device
+            t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
+            self._dtab = (t(start[order], np.int64), t(doff[order], np.int64), t(dlen[order], np.int64),
+                          t(zst[order], np.int32), int(order.size), torch.from_numpy(buf).to(dev))
+        return self._dtab
+
+    @property
+    def value_source(self):
+        """the device bytes get_batch's val_off / val_len point into: the file, or for a
+        compressed file its decompressed blocks"""
+        return self.file if self.compression == 0 else self._dec_table()[5]
+
     def get_batch(self, keys, stream=None):
-        """Reader::get for every key at once on the device (mtblx_get, f2).
-        -> (status int32 [nq] (GET_*), val_off int64 [nq], val_len int64 [nq]) device tensors;
-        the value of a FOUND query q is file[val_off[q] : val_off[q] + val_len[q]]."""
-        if self.compression != 0:
-            raise NotImplementedError("mtblx_get reads raw blocks; compressed files use get()")
+        """Reader::get for every key at once on the device (mtblx_get / mtblx_get_decompressed,
+        f2).  -> (status int32 [nq] (GET_*), val_off int64 [nq], val_len int64 [nq]) device
+        tensors; the value of a FOUND query q is value_source[val_off[q] : val_off[q] +
+        val_len[q]] (the file itself unless it is compressed)."""
         dev = self.file.device
         ks = [bytes(k) for k in keys]
         nq = len(ks)
@@ -423,10 +446,20 @@ class Reader:
         st = torch.zeros(n, dtype=torch.int32, device=dev)
         vo = torch.zeros(n, dtype=torch.int64, device=dev)
         vl = torch.zeros(n, dtype=torch.int64, device=dev)
-        rc = _lib.lib().mtblx_get(C.c_void_p(self.file.data_ptr()), self.len, self.version, 1 if self.verify else 0,
-                                  self.index_off, self.index_len, C.c_void_p(kb.data_ptr()),
-                                  C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()), C.c_void_p(vo.data_ptr()),
-                                  C.c_void_p(vl.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
+        if self.compression == 0:
+            rc = _lib.lib().mtblx_get(C.c_void_p(self.file.data_ptr()), self.len, self.version, 1 if self.verify else 0,
+                                      self.index_off, self.index_len, C.c_void_p(kb.data_ptr()),
+                                      C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()),
+                                      C.c_void_p(vo.data_ptr()), C.c_void_p(vl.data_ptr()),
+                                      C.c_void_p(codec._stream_handle(stream)))
+        else:
+            ts, tdo, tdl, tst, ntab, dec = self._dec_table()
+            rc = _lib.lib().mtblx_get_decompressed(
+                C.c_void_p(self.file.data_ptr()), self.len, self.version, 1 if self.verify else 0, self.index_off,
+                self.index_len, C.c_void_p(ts.data_ptr()), C.c_void_p(tdo.data_ptr()), C.c_void_p(tdl.data_ptr()),
+                C.c_void_p(tst.data_ptr()), ntab, C.c_void_p(dec.data_ptr()), C.c_void_p(kb.data_ptr()),
+                C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()), C.c_void_p(vo.data_ptr()),
+                C.c_void_p(vl.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
         if rc != 0:
             raise RuntimeError(f"mtblx_get failed: {rc}")
         return st[:nq], vo[:nq], vl[:nq]

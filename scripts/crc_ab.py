@@ -1,6 +1,7 @@
 """Timing of the CRC-32C kernel over the cfg2 bench batch: each run in its own child process
-(argv names runs; MTBLX_CRC_KERNEL is passed through for A/B builds), HIP events around 50
-launches after a 200 ms preload, two alternations; also decode + verify (two launches).
+(argv names runs: "kernel" sets MTBLX_CRC_KERNEL, "kernel@lib" also MTBLX_LIB = that library,
+e.g. a diagnostic variant; "!" at the end: an ablation whose checksums are wrong by design),
+HIP events around 50 launches after a 200 ms preload, two alternations; also decode + verify.
 Round 3 measured kernels 0-7 with it (profiles/r03/crc_ab.txt); only kernel 0 remains."""
 import json
 import os
@@ -19,7 +20,8 @@ batch = codec.DeviceBatch.from_host(data, off, ln)
 s = torch.cuda.Stream()
 crc, bad = codec.crc32c_blocks(batch, framed=True, stream=s)
 torch.cuda.synchronize()
-assert int(bad.sum().item()) == 0
+ABL = os.environ.get("CRC_AB_ABLATION") == "1"
+assert ABL or int(bad.sum().item()) == 0
 def timed(fn, reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(s):
@@ -43,7 +45,7 @@ g = lambda: codec.decode_verify_into(batch, out, ws, None, vbad, True, s, fused=
 for _ in range(20):
     g()
 dv_ms = timed(g, 50)
-assert int(vbad.sum().item()) == 0
+assert ABL or int(vbad.sum().item()) == 0
 print(json.dumps({"crc_ms": round(crc_ms, 4), "decode_verify_ms": round(dv_ms, 4),
                   "crc_GiBs": round(float(ln.sum()) / crc_ms / 1e-3 / 2**30, 1),
                   "decode_verify_GiBs": round(float(ln.sum()) / dv_ms / 1e-3 / 2**30, 1)}))
@@ -52,8 +54,11 @@ print(json.dumps({"crc_ms": round(crc_ms, 4), "decode_verify_ms": round(dv_ms, 4
 res = {}
 for rnd in range(2):
     for k in sys.argv[1:] or ["0", "1", "2"]:
-        r = subprocess.run([sys.executable, "-c", CHILD], env=dict(os.environ, MTBLX_CRC_KERNEL=k),
-                           capture_output=True, text=True, timeout=300)
+        name, _, lib = k.rstrip("!").partition("@")
+        env = dict(os.environ, MTBLX_CRC_KERNEL=name, CRC_AB_ABLATION="1" if k.endswith("!") else "0")
+        if lib:
+            env["MTBLX_LIB"] = os.path.abspath(lib)
+        r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             print(r.stderr[-2000:])
             sys.exit(1)

@@ -117,3 +117,48 @@ def pack(blocks, align=1, lead=0, rng=None):
         pos += len(b)
     data = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()
     return data, np.array(off, np.uint64), np.array(ln, np.uint32)
+
+
+# ---------------- FormatV1 files (src/metadata.rs:29-33, src/reader.rs:54-56,146-148) ----------------
+MAGIC_V1 = 0x77846676
+
+
+def to_v1(data: bytes, restart_interval=16) -> bytes:
+    """Re-frame a FormatV2 file (an oracle / product Writer output) as FormatV1: every block's
+    varint64 length becomes a u32 LE length (src/reader.rs:146-148; index: :54-56), the stored
+    checksum and content stay (the CRC covers the stored content), the index block is rebuilt
+    with the same separators and the new block offsets as varint64 values (the BlockBuilder
+    the Writer uses for its index, src/writer.rs:72,136,160), and the footer gets the new
+    offsets / byte counts and the V1 magic (src/metadata.rs:29-33, src/lib.rs:17-20).
+    The reference only writes V2 (src/writer.rs:215); its reader takes both."""
+    import pyoracle as o
+    data = bytes(data)
+    meta = [int.from_bytes(data[len(data) - 512 + 8 * i: len(data) - 504 + 8 * i], "little") for i in range(9)]
+    out = bytearray()
+    entries = []
+    for sep, val in o.index_records(data):
+        off, _ = o.varint_decode64(val)
+        n, ll = o.varint_decode64(data[off: off + 10])
+        entries.append((sep, o.varint_encode64(len(out))))
+        out += n.to_bytes(4, "little") + data[off + ll: off + ll + 4 + n]
+    nbytes_data = len(out)
+    ib = o.build_block(entries, restart_interval)
+    idx_off = len(out)
+    out += len(ib).to_bytes(4, "little") + o.crc32c(ib).to_bytes(4, "little") + ib
+    meta[0], meta[5], meta[6] = idx_off, nbytes_data, len(out) - idx_off
+    footer = b"".join(m.to_bytes(8, "little") for m in meta)
+    footer += b"\0" * (508 - len(footer)) + MAGIC_V1.to_bytes(4, "little")
+    return bytes(out) + footer
+
+
+def v1_frames(data: bytes):
+    """(frame offset, content length) of every block of a V1 file, index block last"""
+    import pyoracle as o
+    idx_off = int.from_bytes(data[len(data) - 512: len(data) - 504], "little")
+    n = int.from_bytes(data[idx_off: idx_off + 4], "little")
+    st, recs = o.decode_block(data[idx_off + 8: idx_off + 8 + n])
+    frames = []
+    for _, val in recs:
+        off, _ = o.varint_decode64(val)
+        frames.append((off, int.from_bytes(data[off: off + 4], "little")))
+    return frames + [(idx_off, n)]

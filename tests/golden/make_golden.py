@@ -6,7 +6,12 @@
    `empty` (src/writer.rs:272-298) byte-exactly.
 2. one_key.mtbl / empty.mtbl: the files those vectors describe, written by the oracle
    and checked against kat.json before being (re)written.
-3. quirk_blocks.json: hand-constructed single blocks with the outcome derived by hand
+3. one_key_v1.mtbl / empty_v1.mtbl: the same two files in FormatV1, which the reference reads
+   (src/metadata.rs:29-33: magic 0x77846676; src/reader.rs:54-56,146-148: u32 LE block
+   lengths instead of varint64) but never writes (src/writer.rs:215).  Their bytes are
+   assembled here from the hand-derived pieces in KAT["one_key_v1"] / KAT["empty_v1"] and must
+   equal what tests/corpus.py:to_v1 makes of the V2 files.
+4. quirk_blocks.json: hand-constructed single blocks with the outcome derived by hand
    from src/block.rs (status + records) — pins the oracle's panic / None / loop /
    Vec-capacity semantics independently of its code.
 
@@ -34,6 +39,24 @@ KAT = {
         "metadata": [32, 8192, 0, 1, 1, 32, 22, 5, 11],
         "first_54": "1b020b403f00050b68656c6c6f49276d20746865206f6e650000000001000000115917ecde00050168656c6c6f000000000001000000",
         "sha256": "ba687784368babc7a8bf12033fafd36091e0c05eaa28c5838bace82a023b26b7",
+    },
+    # FormatV1 (hand-derived): u32 LE content lengths, the same checksums and contents; the
+    # index value varint64(0) and the footer offsets move with the 3 extra framing bytes per block
+    "one_key_v1": {
+        "data_frame": "1b000000" "020b403f" "00050b68656c6c6f49276d20746865206f6e650000000001000000",
+        "index_frame": "11000000" "5917ecde" "00050168656c6c6f000000000001000000",
+        "file_len": 572,
+        "metadata": [35, 8192, 0, 1, 1, 35, 25, 5, 11],
+        "magic": "76668477",
+        "sha256": "c8dec613b1bb3032acc16fa0e7f38f0480da6976f70699d41ed18cfaa7b32c8f",
+        "records": [["hello", "I'm the one"]],
+    },
+    "empty_v1": {
+        "index_frame": "08000000" "32186d51" "0000000001000000",
+        "file_len": 528,
+        "metadata": [0, 8192, 0, 0, 0, 0, 16, 0, 0],
+        "magic": "76668477",
+        "records": [],
     },
     "empty": {
         "index_block_content": "0000000001000000",
@@ -137,6 +160,32 @@ def build_files():
     return one, empty
 
 
+def v1_kat_bytes(name):
+    """a FormatV1 KAT file from its hand-derived pieces: frames, zero-padded footer, magic"""
+    k = KAT[name]
+    body = bytes.fromhex(k.get("data_frame", "") + k["index_frame"])
+    footer = b"".join(m.to_bytes(8, "little") for m in k["metadata"])
+    return body + footer + b"\0" * (508 - len(footer)) + bytes.fromhex(k["magic"])
+
+
+def check_v1(one, empty):
+    """the V1 KATs: hand bytes == corpus.to_v1(V2 file); the oracle reads them back"""
+    import pyoracle as o
+    sys.path.insert(0, os.path.dirname(HERE))
+    import corpus
+    for name, v2 in (("one_key_v1", one), ("empty_v1", empty)):
+        k = KAT[name]
+        b = v1_kat_bytes(name)
+        assert len(b) == k["file_len"], (name, len(b))
+        if "sha256" in k:
+            assert hashlib.sha256(b).hexdigest() == k["sha256"]
+        assert corpus.to_v1(v2) == b, name
+        r = o.file_scan(b)
+        assert r["version"] == 0 and r["end"] == 0 and r["meta"] == k["metadata"], (name, r)
+        assert r["records"] == [(a.encode(), v.encode()) for a, v in k["records"]], (name, r["records"])
+    return v1_kat_bytes("one_key_v1"), v1_kat_bytes("empty_v1")
+
+
 def check(one, empty):
     import pyoracle as o
     assert o.crc32c(b"123456789") == int(KAT["crc32c_check"]["crc"], 16)
@@ -155,16 +204,21 @@ def check(one, empty):
 def main():
     one, empty = build_files()
     check(one, empty)
+    one1, empty1 = check_v1(one, empty)
     if "--check" in sys.argv:
         assert open(os.path.join(HERE, "one_key.mtbl"), "rb").read() == one
         assert open(os.path.join(HERE, "empty.mtbl"), "rb").read() == empty
+        assert open(os.path.join(HERE, "one_key_v1.mtbl"), "rb").read() == one1
+        assert open(os.path.join(HERE, "empty_v1.mtbl"), "rb").read() == empty1
         print("golden fixtures OK")
         return
     open(os.path.join(HERE, "one_key.mtbl"), "wb").write(one)
     open(os.path.join(HERE, "empty.mtbl"), "wb").write(empty)
+    open(os.path.join(HERE, "one_key_v1.mtbl"), "wb").write(one1)
+    open(os.path.join(HERE, "empty_v1.mtbl"), "wb").write(empty1)
     json.dump(dict(KAT, seek_kat=SEEK_KAT), open(os.path.join(HERE, "kat.json"), "w"), indent=1)
     json.dump(QUIRKS, open(os.path.join(HERE, "quirk_blocks.json"), "w"), indent=1)
-    print("wrote tests/golden/{one_key,empty}.mtbl, kat.json, quirk_blocks.json")
+    print("wrote tests/golden/{one_key,empty}{,_v1}.mtbl, kat.json, quirk_blocks.json")
 
 
 if __name__ == "__main__":

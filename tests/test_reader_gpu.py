@@ -94,6 +94,7 @@ def _check_get(oracle, data: bytes, queries, verify=True):
     st = st.cpu().numpy()
     vo = vo.cpu().numpy()
     vl = vl.cpu().numpy()
+    src = data if r.compression == 0 else r.value_source.cpu().numpy().tobytes()   # decompressed blocks
     end_of = {rd.END_NONE: _lib.GET_NONE, rd.END_PANIC: _lib.GET_PANIC, rd.END_ERR_OPEN: _lib.GET_ERR,
               rd.END_ERR_NEXT: _lib.GET_ERR, rd.END_LOOP: _lib.GET_LOOP}
     for q, key in enumerate(queries):
@@ -101,7 +102,7 @@ def _check_get(oracle, data: bytes, queries, verify=True):
         if exp["records"]:
             assert exp["end"] == rd.END_NONE
             assert st[q] == _lib.GET_FOUND, (q, key, st[q])
-            assert data[vo[q]: vo[q] + vl[q]] == exp["records"][0][1]
+            assert src[vo[q]: vo[q] + vl[q]] == exp["records"][0][1]
         else:
             assert st[q] == end_of[exp["end"]], (q, key, st[q], exp["end"])
 
@@ -137,6 +138,31 @@ def test_get_batch_corrupted(oracle):
         qs = [recs[int(i)][0] for i in rng.integers(0, len(recs), 40)] + [b"", b"\xff" * 20]
         for verify in (True, False):
             _check_get(oracle, bytes(d), qs, verify=verify)
+
+
+@pytest.mark.parametrize("comp", [1, 2, 5])
+def test_get_batch_compressed(oracle, comp):
+    """the batched Reader::get on Snappy / Zlib / Zstd files (mtblx_get_decompressed: framing and
+    checksum on the stored bytes, the scan on the host-decompressed blocks), valid files and
+    files with a corrupted stored block (Err(Io) / checksum panic), verify on and off"""
+    rng = np.random.default_rng(43 + comp)
+    from mtblx.writer import Writer
+    for bs, iv, n in ((1024, 4, 400), (4096, 16, 2500)):
+        recs = corpus.random_records(rng, n, 0, 40, 0, 200)
+        w = Writer(bs, iv, comp)
+        for k, v in recs:
+            w.insert(k, v)
+        data = w.into_inner()
+        off, ln = w.block_dir
+        keys = [k for k, _ in recs]
+        qs = [keys[int(i)] for i in rng.integers(0, n, 120)]
+        qs += [k + b"\x00" for k in qs[:30]] + [b"", b"\xff" * 30, keys[0], keys[-1], keys[-1] + b"\x01"]
+        _check_get(oracle, data, qs)
+        for b in (1, len(off) // 2):
+            d = bytearray(data)
+            d[int(off[b]) + int(ln[b]) // 2] ^= 0x5A            # a stored byte: checksum / codec error
+            for verify in (True, False):
+                _check_get(oracle, bytes(d), qs[:60] + [keys[-1]], verify=verify)
 
 
 def test_get_stale_value_when_next_block_invalid(oracle):

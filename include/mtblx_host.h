@@ -62,6 +62,8 @@ int mtblx_frame_block(const uint8_t* file, uint64_t len, uint32_t version, uint6
 #define MTBLX_SNAPPY_OK 0
 #define MTBLX_SNAPPY_CORRUPT 1   /* snap::raw::Decoder error -> io::Error -> Error::Io (src/compression.rs:117-118) */
 #define MTBLX_SNAPPY_TOO_SMALL 2 /* destination capacity too small */
+#define MTBLX_SNAPPY_TIMEOUT 3   /* device decompression only: a bounded internal wait (2 s) gave up --
+                                    not a property of the stream; the block's output is not valid */
 uint64_t mtblx_snappy_max_compressed_len(uint64_t n);
 /* the length stored in the preamble (no validation of the body) */
 int mtblx_snappy_uncompressed_len(const uint8_t* src, uint64_t n, uint64_t* out);

@@ -177,9 +177,19 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums must stay below 2^10 for 
 #ifndef MTBLX_CRC_ABL
 #define MTBLX_CRC_ABL 0
 #endif
-constexpr int kMThreads = 512;                 // 8 waves, one workgroup per CU (160 KiB of LDS)
-constexpr int kMWaves = kMThreads / kWave;
-constexpr int kRing = 8;                       // steps per wave ring (16 KiB)
+#ifndef MTBLX_CRC_MWAVES
+#define MTBLX_CRC_MWAVES 16
+#endif
+#ifndef MTBLX_CRC_RING
+#define MTBLX_CRC_RING 8
+#endif
+#ifndef MTBLX_CRC_DMA_AUX
+#define MTBLX_CRC_DMA_AUX 2   // non-temporal: the block bytes are read once
+#endif
+constexpr int kMWaves = MTBLX_CRC_MWAVES;      // waves per workgroup, one workgroup per CU
+constexpr int kMThreads = kMWaves * kWave;
+constexpr int kRing = MTBLX_CRC_RING;          // steps per wave ring (1 KiB each)
+static_assert(32 * 1024 + kMWaves * kRing * kMStep <= 160 * 1024, "LDS: tables + rings");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
@@ -211,9 +221,10 @@ __device__ __forceinline__ uint32_t pack_window(v4f lo, v4f hi) {
   return x | (y << 16);
 }
 
-struct RingSlot {   // one step: its 128 16-byte chunks, lowest address first
-  v4u c[128];
+struct RingSlot {   // one step: its 64 16-byte chunks, lowest address first
+  v4u c[kMStep / 16];
 };
+static_assert(kMStep / 16 == kWave, "one LDS-DMA wave-instruction per step");
 
 // The block's first bytes: a step's chunks lie at block positions a = sb + 16 k, 16-byte aligned
 // in memory while the block is not.  A chunk wholly before the block is zeroed (its DMA read
@@ -239,32 +250,50 @@ __device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
   return v4u{y.x & m(0), y.y & m(1), y.z & m(2), y.w & m(3)};
 }
 
-// s_waitcnt vmcnt(2k): a step has landed once at most the 2k DMA instructions of the k steps
+// s_waitcnt vmcnt(k): a step has landed once at most the k DMA instructions of the k steps
 // issued after it are outstanding (other vector-memory operations of the wave only make the
-// wait stricter: the counter retires in issue order)
+// wait stricter: the counter retires in issue order).  The steady state (k = kRing - 1) first.
 __device__ __forceinline__ void wait_ring(uint32_t k) {
+  if (k >= (uint32_t)(kRing - 1)) {
+    switch (kRing - 1) {
+      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); return;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); return;
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); return;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); return;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); return;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); return;
+      default: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); return;
+    }
+  }
   switch (k) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
   }
 }
-static_assert(kRing == 8, "wait_ring covers kRing - 1 = 7 steps ahead");
+static_assert(kRing >= 2 && kRing <= 8, "wait_ring covers up to 7 steps ahead");
 
 // the lane's two chunks of a landed slot.  Inline asm: the compiler treats an LDS read it can see
 // as aliasing every LDS-DMA in flight and waits vmcnt(0) before it, which would drain the ring;
 // wait_ring has already waited for exactly this slot's DMA.
-__device__ __forceinline__ void ring_read(const RingSlot* sl, uint32_t kx, v4u& x, v4u& y) {
+__device__ __forceinline__ v4u ring_read(const RingSlot* sl, uint32_t kx) {
   const uint32_t ax = (uint32_t)(uintptr_t)(const lds_void*)&sl->c[kx];
-  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
-               : "=&v"(x), "=&v"(y)
-               : "v"(ax)
-               : "memory");
+  v4u x;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(ax) : "memory");
+  return x;
+}
+
+// XOR over the 16 lanes of each DPP row, in every lane of the row (row_ror 8, 4, 2, 1)
+__device__ __forceinline__ uint32_t row_xor(uint32_t x) {
+  x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, false);
+  x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xf, 0xf, false);
+  x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xf, 0xf, false);
+  x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xf, 0xf, false);
+  return x;
 }
 
 // serial CRC-32C of a short block (< 4 bytes), one lane
@@ -295,7 +324,7 @@ struct MBlk {
   int64_t L;        // content length
   int64_t Lp;       // L + t: padded to a 16-byte aligned end address
   uint32_t t;       // pad bytes, < 16
-  uint32_t steps;   // ceil(Lp / 2 KiB)
+  uint32_t steps;   // ceil(Lp / 1 KiB)
   int64_t a0;       // block position of the 16-byte aligned chunk holding byte 0 (in [-15, 0])
 };
 __device__ __forceinline__ MBlk mblk(uint64_t base, uint64_t off, uint64_t L) {
@@ -317,7 +346,7 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
   __shared__ v4i sA2[8 * 2 * 64];              // 16 KiB: stage-2 operands
   __shared__ uint32_t sCol[16][8][16];         // 8 KiB: column shifts
   __shared__ uint32_t sInv[16][8][16];         // 8 KiB: pad removal
-  __shared__ RingSlot sRing[kMWaves][kRing];   // 128 KiB
+  __shared__ RingSlot sRing[kMWaves][kRing];   // 128 KiB at 16 waves x 8 steps
   const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
@@ -328,22 +357,22 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
       (&sInv[0][0][0])[i] = (&kMfma.inv[0][0][0])[i];
     }
   }
-  v4i A[8][2];
+  v4i A[kMKs][2];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
+  for (int t = 0; t < kMKs; ++t) {
     A[t][0] = reinterpret_cast<const v4i*>(&kMfma.a[t][0][0][0])[lane];
     A[t][1] = reinterpret_cast<const v4i*>(&kMfma.a[t][1][0][0])[lane];
   }
   // use A here, so the wait for its loads is placed before the loop: left to its first use
   // inside the loop, the wait would be a vmcnt(0) in every iteration, draining the ring
 #pragma unroll
-  for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(A[t][0]), "v"(A[t][1]));
+  for (int t = 0; t < kMKs; ++t) asm volatile("" ::"v"(A[t][0]), "v"(A[t][1]));
   __syncthreads();
   RingSlot* ring = sRing[wv];
   const uint64_t base = (uint64_t)(uintptr_t)data;
   const uint32_t W = gridDim.x * kMWaves;
   const uint32_t w0 = blockIdx.x * kMWaves + wv;
-  const uint32_t kx = 120u - 8u * (uint32_t)n + (uint32_t)g;   // the lane's first chunk of a step
+  const uint32_t kx = 60u - 4u * (uint32_t)n + (uint32_t)g;   // the lane's chunk of a step
 
   // the wave's blocks w0 + k W, 64 at a time: lane j holds block k = 64 m + j of window m
   for (uint64_t kb = 0; w0 + kb * W < nblk; kb += kWave) {
@@ -376,12 +405,10 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
     auto issue = [&]() {
       RingSlot* sl = ring + (issued % kRing);
       const int64_t sb = I.Lp - (int64_t)kMStep * (is + 1);      // block position of chunk 0
-      const int64_t px = sb + 16 * lane, py = px + 16 * kWave;
+      const int64_t px = sb + 16 * lane;
       // chunks wholly before the block load its first aligned chunk instead (zeroed on read)
       const uint8_t* p = data + I.off + (px + 16 > 0 ? px : I.a0);
-      const uint8_t* q = data + I.off + (py + 16 > 0 ? py : I.a0);
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)&sl->c[0], 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(q, (lds_void*)&sl->c[kWave], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)&sl->c[0], 16, 0, MTBLX_CRC_DMA_AUX);
       ++issued;
       if (++is == I.steps) {
         is = 0;
@@ -412,29 +439,24 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
       }
     };
     cnext();
-    uint32_t cs = 0, acc = 0;
+    uint32_t cs = 0, acc = 0, accS = 0;
     v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
     v4i bb = {0, 0, 0, 0};   // stage-2 operand: dword d = step 4 jq + d of the quad (shifted in)
     while (clive) {
       if (ilive && issued - done < (uint32_t)kRing) issue();
       wait_ring(issued - done - 1 < (uint32_t)(kRing - 1) ? issued - done - 1 : (uint32_t)(kRing - 1));
-      v4u x, y;
-      ring_read(ring + (done % kRing), kx, x, y);
+      v4u x = ring_read(ring + (done % kRing), kx);
       ++done;
       const int64_t sb = Cb.Lp - (int64_t)kMStep * (cs + 1);
-      if (cs == 0 && Cb.t != 0 && lane == 48) y = tail_chunk(y, Cb.t);   // lane (g 3, n 0): chunk 127
-      if (sb < 4) {   // the step holds the block's first bytes (sb >= -2047: 32-bit positions)
-        const int a = (int)sb + 16 * (int)kx;
-        x = head_chunk(x, a);
-        y = head_chunk(y, a + 64);
-      }
+      if (cs == 0 && Cb.t != 0 && lane == 48) x = tail_chunk(x, Cb.t);   // lane (g 3, n 0): chunk 63
+      if (sb < 4) x = head_chunk(x, (int)sb + 16 * (int)kx);   // the block's first bytes (sb > -1024)
 #if MTBLX_CRC_ABL == 1
-      acc ^= x.x ^ x.y ^ x.z ^ x.w ^ y.x ^ y.y ^ y.z ^ y.w;
+      acc ^= x.x ^ x.y ^ x.z ^ x.w;
 #else
-      const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      const uint32_t w[kMKs] = {x.x, x.y, x.z, x.w};
       v4f c1a = {0.f, 0.f, 0.f, 0.f}, c1b = c1a;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < kMKs; ++t) {
         const uint32_t v = w[t];
         const v4i b = {(int)(v & 0x11111111u), (int)(v & 0x22222222u), (int)(v & 0x44444444u),
                        (int)((v >> 1) & 0x44444444u)};
@@ -463,8 +485,8 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
           dv |= (par_bits(c2b.w, kMag0) & 1u) << (sh + 19);
           const uint32_t S = cs >> 5;
           if (S == 0) acc ^= dv;
-          else if (S < 16) acc ^= mul_nib(dv, kMfma.sw[S]);
-          else acc ^= dmultmodp(xpow8((uint64_t)S * (uint64_t)(kMStep * kMSup)), dv);
+          else if (S < 16) accS ^= mul_nib(dv, kMfma.sw[S]);
+          else accS ^= dmultmodp(xpow8((uint64_t)S * (uint64_t)(kMStep * kMSup)), dv);
           c2a = v4f{0.f, 0.f, 0.f, 0.f};
           c2b = c2a;
         }
@@ -473,13 +495,22 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
         ++cs;
         continue;
       }
-      // block done: column shifts, XOR over all 64 lanes (each holds its 8 of a column's 32 bits)
-      uint32_t c = mul_nib(acc, sCol[n]);
-#pragma unroll
-      for (int sh = 1; sh < 64; sh <<= 1) c ^= (uint32_t)__shfl_xor((int)c, sh, kWave);
-      c = mul_nib(c, sInv[Cb.t]) ^ 0xFFFFFFFFu;
-      if (lane == cj) res = c;
+      // block done: column shifts, XOR over all 64 lanes, pad removal.  acc0 (the first super-
+      // window) holds only the lane's own 8 bits of its column -- nibbles g and 4 + g -- so the
+      // column shift takes 2 lookups; later super-windows (accS) were shifted to full words.
+      uint32_t c = sCol[n][g][(acc >> (4 * g)) & 15u] ^ sCol[n][4 + g][(acc >> (16 + 4 * g)) & 15u];
+      if (Cb.steps > (uint32_t)kMSup) c ^= mul_nib(accS, sCol[n]);
+      c = row_xor(c);                                          // over the 16 columns of a row
+      uint32_t C = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 16) ^
+                   (uint32_t)__builtin_amdgcn_readlane((int)c, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
+      if (Cb.t) {   // x^(-8t): nibble j looked up by lane j (j < 8) of each row
+        const uint32_t j = (uint32_t)lane & 15u;
+        const uint32_t v = j < 8u ? sInv[Cb.t][j][(C >> (4 * j)) & 15u] : 0u;
+        C = (uint32_t)__builtin_amdgcn_readlane((int)row_xor(v), 0);
+      }
+      if (lane == cj) res = C ^ 0xFFFFFFFFu;
       acc = 0;
+      accS = 0;
       cs = 0;
       cnext();
     }
@@ -519,10 +550,10 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   if (!in || (!crc && !bad && in->nblk)) return MTBLX_E_INVAL;
   if (in->nblk == 0) return MTBLX_OK;
   if (!in->data || !in->blk_off || !in->blk_len) return MTBLX_E_INVAL;
-  // MTBLX_CRC_KERNEL=mfma: the matrix-core kernel (bit-exact; not yet faster than the VALU
-  // table kernel on cfg2), else k_crc32c_blocks
+  // the matrix-core kernel unless MTBLX_CRC_KERNEL=lanes (the VALU table kernel, kept for A/B):
+  // 0.102 vs 0.120 ms on cfg2 (profiles/r04/crc_mfma)
   const char* kv = getenv("MTBLX_CRC_KERNEL");
-  if (kv && kv[0] == 'm') {
+  if (!kv || kv[0] != 'l') {
     static int mgrid = 0;   // persistent: one 8-wave workgroup (152 KiB LDS) per CU
     if (!mgrid) {
       int dev = 0, ncu = 0;

@@ -1,17 +1,17 @@
 // crc_mfma.h — constant operands of the matrix-core CRC-32C (crc.hip k_crc32c_mfma).
 //
-// CRC-32C without init/xorout ("raw") is linear over GF(2): the raw CRC of a 128-byte window is
-// M_w · bits, M_w a constant 32 x 1024 bit matrix.  With every bit as an fp4 (e2m1) operand
+// CRC-32C without init/xorout ("raw") is linear over GF(2): the raw CRC of a 64-byte window is
+// M_w · bits, M_w a constant 32 x 512 bit matrix.  With every bit as an fp4 (e2m1) operand
 // element the product is one fp4 GEMM whose f32 sums carry the GF(2) result in their parity.
-// A wave reads one block at a time, a STEP = 16 consecutive windows (2 KiB) per MFMA column set:
+// A wave reads one block at a time, a STEP = 16 consecutive windows (1 KiB) per MFMA column set:
 // column n of step s holds window w = 16 s + n, counted from the block's END.
-//   stage 1  C1 = M_w · window bits            16x16x128 fp4 MFMA, K = 1024 over 8 k-steps,
+//   stage 1  C1 = M_w · window bits            16x16x128 fp4 MFMA, K = 512 over 4 k-steps,
 //            (rows = CRC bits, columns = the     two row halves per k-step
 //             step's 16 windows)
-//   stage 2  per column, the steps of a super-window (32 steps = 64 KiB) shifted by
-//            x^(8·2048·t) and summed: [S_0 .. S_31] · parity(C1), one fp4 MFMA pair per 4 steps
-//   stage 3  per column, x^(8·65536·S) · parity(C2_S) summed over super-windows S (nibble
-//            tables sw), then the column shift x^(8·128·n) (nibble tables col) and an XOR over
+//   stage 2  per column, the steps of a super-window (32 steps = 32 KiB) shifted by
+//            x^(8·1024·t) and summed: [S_0 .. S_31] · parity(C1), one fp4 MFMA pair per 4 steps
+//   stage 3  per column, x^(8·32768·S) · parity(C2_S) summed over super-windows S (nibble
+//            tables sw), then the column shift x^(8·64·n) (nibble tables col) and an XOR over
 //            the 16 columns: the raw CRC of the block padded with t < 16 zero bytes to a 16-byte
 //            aligned end, times x^(-8t) (nibble tables inv): the block's raw CRC
 // The reference's checksum is crate crc32c 0.4 over each block's stored bytes
@@ -21,8 +21,8 @@
 // A's lane l and B's lane l hold the same K indices in the same slots (slot s = nibble s & 7 of
 // dword s >> 3), whatever K order the hardware uses.  So a B slot is bound to a data bit by how the
 // kernel fills it, and A's slot in the same lane group carries M_w's entry for that bit:
-//   B: lane (g = l >> 4, n = l & 15), k-step t: raw dword w = window dword D(g, t) of window n,
-//      D = t < 4 ? 4g + t : 16 + 4g + t - 4; the four operand dwords are the bit planes
+//   B: lane (g = l >> 4, n = l & 15), k-step t: raw dword w = window dword D = 4g + t of window
+//      n (the lane holds window bytes [16g, 16g + 16)); the four operand dwords are the bit planes
 //      w & 0x11111111, w & 0x22222222, w & 0x44444444, (w >> 1) & 0x44444444: slot (q, i) is bit
 //      4i + q of w, as an e2m1 value 0.5 / 1 / 2 / 2 (q = 0 / 1 / 2 / 3).
 //   A: the matching entry times 2 / 1 / 0.5 / 0.5, so every product of two set bits is exactly 1.
@@ -34,16 +34,17 @@
 
 namespace mtblx_crc {
 
-constexpr int kMWin = 128;            // stage-1 window: bytes of one column per 8 k-steps
-constexpr int kMStep = 16 * kMWin;     // a step: 16 consecutive windows of one block, 2 KiB
-constexpr int kMSup = 32;              // steps per super-window (stage 2): 64 KiB
+constexpr int kMWin = 64;             // stage-1 window: bytes of one column per 4 k-steps
+constexpr int kMKs = kMWin / 16;       // k-steps per window (one raw dword of the lane each)
+constexpr int kMStep = 16 * kMWin;     // a step: 16 consecutive windows of one block, 1 KiB
+constexpr int kMSup = 32;              // steps per super-window (stage 2): 32 KiB
 constexpr uint32_t kFp4Half = 0x1u, kFp4One = 0x2u, kFp4Two = 0x4u;   // e2m1 codes of 0.5, 1, 2
 
 struct MfmaTabs {
-  uint32_t a[8][2][64][4];    // stage-1 A operand: [k-step][row half][lane][dword]
+  uint32_t a[kMKs][2][64][4];   // stage-1 A operand: [k-step][row half][lane][dword]
   uint32_t a2[8][2][64][4];   // stage-2 A operand: [step quad][row half][lane][dword]
-  uint32_t sw[16][8][16];     // nibble tables of x^(8·65536·S), S < 16 (stage 3)
-  uint32_t col[16][8][16];    // nibble tables of x^(8·128·n): the column shift, n < 16
+  uint32_t sw[16][8][16];     // nibble tables of x^(8·32768·S), S < 16 (stage 3)
+  uint32_t col[16][8][16];    // nibble tables of x^(8·64·n): the column shift, n < 16
   uint32_t inv[16][8][16];    // nibble tables of x^(-8 t), t < 16: t zero bytes appended, removed
   uint32_t max_row;           // largest popcount of an M_w row (the stage-1 sums stay below it)
 
@@ -71,11 +72,11 @@ struct MfmaTabs {
       if (pc > max_row) max_row = pc;
     }
     const uint32_t code[4] = {kFp4Two, kFp4One, kFp4Half, kFp4Half};
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < kMKs; ++t)
       for (int h = 0; h < 2; ++h)
         for (int l = 0; l < 64; ++l) {
           const int g = l >> 4, r = 16 * h + (l & 15);
-          const int D = t < 4 ? 4 * g + t : 16 + 4 * g + (t - 4);
+          const int D = 4 * g + t;
           for (int s = 0; s < 32; ++s) {
             const int q = s >> 3, i = s & 7, beta = 4 * i + q;
             const int byte = 4 * D + beta / 8, bit = beta % 8;
@@ -119,7 +120,7 @@ struct MfmaTabs {
       MulTabs::fill(inv[t], U);
       for (int k = 0; k < 8; ++k) U = unx(U);
     }
-    // K = x^(8·65536) now; stage 3 nibble tables of its powers
+    // K = x^(8·32768) now; stage 3 nibble tables of its powers
     uint32_t P = 0x80000000u;
     for (int s = 0; s < 16; ++s) {
       MulTabs::fill(sw[s], P);

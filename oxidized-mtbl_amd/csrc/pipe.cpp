@@ -505,8 +505,10 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s.e_dec0, s.e_dec) == hipSuccess) st.decode_ms += ms;
     if (dz_mode)   // device decompression failures: Err(Error::Io), the block decoded as empty
-      for (uint32_t j = 0; j < c.nb; ++j)
+      for (uint32_t j = 0; j < c.nb; ++j) {
+        if (s.hz[j] == MTBLX_SNAPPY_TIMEOUT) return MTBLX_E_TIMEOUT;   // an internal wait gave up
         if (s.hz[j] != MTBLX_SNAPPY_OK) zerr[c.b0 + j] = 1;
+      }
     uint64_t nr = s.htot[0], kb = s.htot[1], vb = s.htot[2];
     if (s.htot[3] & 3ull) {
       // bit 0: the slot's output capacity was too small (keys far longer than the block bytes):

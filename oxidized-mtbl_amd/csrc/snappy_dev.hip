@@ -803,6 +803,7 @@ constexpr uint64_t kSpinTicks = 2ull * 100000000ull;   // 2 s of s_memrealtime: 
 
 struct LaneSync {
   uint32_t dpos[kThreads], fpos[kThreads], fvis[kThreads], dend[kThreads];
+  uint32_t gone[kThreads];   // the writer gave up (2 s without its decoder publishing anything)
 };
 
 __device__ __forceinline__ uint32_t vld(const uint32_t* p) { return *reinterpret_cast<const volatile uint32_t*>(p); }
@@ -856,6 +857,7 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     Y.fpos[t] = 0;
     Y.fvis[t] = 0;
     Y.dend[t] = act ? kRun : 0u;
+    Y.gone[t] = 0u;
   }
   __syncthreads();
   if (b >= nblk) return;
@@ -894,7 +896,13 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
         if ((++spins & 15u) == 0u) {
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (t0 == 0) t0 = now;
-          if (now - t0 > kSpinTicks) break;   // the decoder is gone (a bug): do not hang the GPU
+          // 2 s without a chunk or the end from ITS decoder (which publishes dend as soon as its
+          // own block is done, not when the wave is): leave, and say so -- the decoder then
+          // reports MTBLX_SNAPPY_TIMEOUT instead of OK for a block whose bytes were not all stored
+          if (now - t0 > kSpinTicks) {
+            vst(&Y.gone[t], 1u);
+            break;
+          }
         }
       }
     }
@@ -972,6 +980,11 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
         if (now - t0 > kSpinTicks) hang = true;
       }
     }
+    // the load below must not move above the spin: a volatile read orders only other volatile
+    // accesses, so a compiler barrier pins it (the hardware issues it after the last spin read
+    // returned: it depends on the branch).  The 128-byte bound assumes L1 lines of at most 128
+    // bytes (gfx950's vector L1 line is 128 bytes).
+    __asm__ volatile("" ::: "memory");
 #if MTBLX_LANE_FAR_CACHED
     return q4(*reinterpret_cast<const v4u*>(dg + x));
 #else
@@ -1004,11 +1017,21 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
 #else
 #define LANE_PATH(k) ((void)0)
 #endif
+  // the lane's end (status + dend for its writer), as soon as the LANE is done: the wave keeps
+  // looping for its other lanes, possibly for long, and the writer must not wait for them
+  bool published = false;
+  auto publish = [&]() {
+    if (hang || vld(&Y.gone[t])) st = MTBLX_SNAPPY_TIMEOUT;   // an internal wait gave up: not CORRUPT
+    if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
+    vst(&Y.dend[t], st == MTBLX_SNAPPY_OK ? d : 0u);
+    published = true;
+  };
   while (__ballot(!fin)) {
 #ifdef MTBLX_SNAP_STAMPS
     dbg_path = 0;
 #endif
     if (fin) {
+      if (!published) publish();
 #ifdef MTBLX_SNAP_STAMPS
       goto lane_stamp;
 #else
@@ -1133,9 +1156,7 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     }
 #endif
   }
-  if (hang) st = MTBLX_SNAPPY_CORRUPT;
-  if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
-  vst(&Y.dend[t], st == MTBLX_SNAPPY_OK ? d : 0u);
+  if (!published) publish();
   status[b] = st;
   if (dec_len) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
 }

@@ -308,3 +308,20 @@ def test_auto_routing_large_batch(oracle, snappy_kernel):
             assert st[j] == 0 and got[j] == e, j
     ratios = [len(e) / max(len(z), 1) for z, e in zip(distinct, expect) if e is not None]
     assert max(ratios) > 2 and min(ratios) < 2   # both kernels took blocks
+
+
+def test_long_block_beside_short_ones(oracle, snappy_kernel):
+    """one lane decoding a multi-MB block in the same wave as short blocks.  Each
+    decoding lane now publishes its end as soon as its own block is done, so the short blocks'
+    writer lanes finish their last partial chunk at once instead of idling until the whole wave
+    is done (past their 2 s guard, which left the tail unwritten under status OK)."""
+    codec = _dev()
+    rng = np.random.default_rng(77)
+    phrases = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in (5, 9, 17, 33, 300)]
+    big = b"".join(phrases[int(i)] for i in rng.integers(0, 5, 90_000))   # ~6 MB, copies of all offsets
+    xs = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) + b"q" * int(n) for n in rng.integers(1, 3000, 40)]
+    xs.insert(17, big)
+    streams = _streams(xs)
+    got, st, _ = _device(codec, streams, rng)
+    _check(oracle, streams, got, st)
+    assert (st == 0).all()

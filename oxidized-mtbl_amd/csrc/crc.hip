@@ -157,18 +157,21 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
 
 // ---------------------------------------------------------------------------------------------
 // k_crc32c_mfma: the same checksum on the matrix cores (crc_mfma.h has the method and the
-// operand layout).  Persistent: wave w takes the contiguous blocks [nblk w / W, nblk (w + 1) / W)
-// one at a time and reads each one contiguously, a STEP of 16 consecutive 128-byte windows (2 KiB) at a time,
-// counted from the block's END (window w = bytes [L - 128 (w + 1), L - 128 w)), so one set of
-// shift matrices serves every block length; bytes before the block start are zero and the
-// 0xFFFFFFFF init is folded into bytes 0..3.  Lane (g = lane >> 4, n = lane & 15) feeds 32 bytes
-// of window n of the step.  The steps reach the lanes through a per-wave LDS ring filled by
-// LDS-DMA kRing - 1 steps ahead, across block boundaries.  Per step: 4 vector instructions per
-// loaded dword (the fp4 bit planes), 16 MFMAs, 17 to pack the stage-2 operand; per 4 steps 2
-// MFMAs; per block a parity extraction, the column shifts and a 16-lane XOR.
+// operand layout).  Persistent, one kMWaves-wave workgroup per CU: wave w takes the blocks w,
+// w + W, w + 2W, ... (interleaved: concurrent waves read neighbouring blocks, which spreads the
+// reads over the HBM channels), their offsets / lengths 64 at a time in lane registers.  A wave
+// reads each block from its start to its end, a STEP of 16 consecutive 64-byte windows (1 KiB,
+// one LDS-DMA wave-instruction) at a time; windows are counted from the block's 16-byte aligned
+// END, so one set of shift matrices serves every block length; bytes before the block start are
+// zero and the 0xFFFFFFFF init is folded into bytes 0..3.  Lane (g = lane >> 4, n = lane & 15)
+// feeds 16 bytes of window n.  The steps reach the lanes through a per-wave LDS ring of kRing
+// slots filled kRing - 1 steps ahead across block boundaries, so the wait for a step is one
+// constant s_waitcnt.  Per step: 5 vector instructions per loaded dword (the fp4 bit planes),
+// 8 fp4 MFMAs, 4 conversions and 2 f16 MFMAs; per super-window (8 KiB) a parity extraction and
+// a Horner step; per block the column shifts, a 64-lane XOR and the pad removal.
 // ---------------------------------------------------------------------------------------------
 static __constant__ MfmaTabs kMfma = MfmaTabs();
-static_assert(MfmaTabs().max_row < 1024, "stage-1 sums must stay below 2^10 for the bit-12 parity");
+static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in f16 and in the stage-2 sums");
 
 // MTBLX_CRC_ABL=1 (diagnostic, wrong checksums by construction): the ring without stage 1/2
 #if defined(MTBLX_CRC_ABL) && !defined(MTBLX_DIAG)
@@ -181,7 +184,7 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums must stay below 2^10 for 
 #define MTBLX_CRC_MWAVES 16
 #endif
 #ifndef MTBLX_CRC_RING
-#define MTBLX_CRC_RING 8
+#define MTBLX_CRC_RING 7
 #endif
 #ifndef MTBLX_CRC_DMA_AUX
 #define MTBLX_CRC_DMA_AUX 2   // non-temporal: the block bytes are read once
@@ -189,11 +192,13 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums must stay below 2^10 for 
 constexpr int kMWaves = MTBLX_CRC_MWAVES;      // waves per workgroup, one workgroup per CU
 constexpr int kMThreads = kMWaves * kWave;
 constexpr int kRing = MTBLX_CRC_RING;          // steps per wave ring (1 KiB each)
-static_assert(32 * 1024 + kMWaves * kRing * kMStep <= 160 * 1024, "LDS: tables + rings");
+constexpr int kMTabLds = kMSup * 2 * 64 * 16 + 2 * 16 * 8 * 16 * 4;   // 32 KiB
+static_assert(kMTabLds + kMWaves * kRing * kMStep <= 160 * 1024, "LDS: tables + rings");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ v4f mfma_fp4(v4i a, v4i b, v4f c) {
@@ -201,25 +206,15 @@ __device__ __forceinline__ v4f mfma_fp4(v4i a, v4i b, v4f c) {
   const v8i b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 4, 4, 0, 0, 0, 0);
 }
-
-// parity of an exact integer-valued sum v (0 <= v < 2^(22 - k)) at bit k: v + 1.5·2^(23-k) keeps
-// v · 2^k in the low mantissa bits
-__device__ __forceinline__ uint32_t par_bits(float v, float magic) { return __float_as_uint(v + magic); }
-__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (mask & a) | (~mask & b); }
-constexpr float kMag0 = 12582912.0f, kMag4 = 786432.0f, kMag8 = 49152.0f, kMag12 = 3072.0f;
-
-// stage-2 operand dword of one step: parity of C1[h][i] at bit 16 h + 4 i
-__device__ __forceinline__ uint32_t pack_window(v4f lo, v4f hi) {
-  uint32_t x = par_bits(lo.x, kMag0) & 1u;
-  x = bfi(1u << 4, par_bits(lo.y, kMag4), x);
-  x = bfi(1u << 8, par_bits(lo.z, kMag8), x);
-  x = bfi(1u << 12, par_bits(lo.w, kMag12), x);
-  uint32_t y = par_bits(hi.x, kMag0) & 1u;
-  y = bfi(1u << 4, par_bits(hi.y, kMag4), y);
-  y = bfi(1u << 8, par_bits(hi.z, kMag8), y);
-  y = bfi(1u << 12, par_bits(hi.w, kMag12), y);
-  return x | (y << 16);
+__device__ __forceinline__ v4f mfma_f16(v4i a, v4i b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a), __builtin_bit_cast(v8h, b), c, 0, 0, 0);
 }
+// two stage-1 sums as f16 (integers below 2048: exact)
+__device__ __forceinline__ int pk16(float a, float b) { return __builtin_bit_cast(int, __builtin_amdgcn_cvt_pkrtz(a, b)); }
+
+// parity of an exact integer-valued sum v (0 <= v < 2^22): v + 1.5·2^23 keeps v in the low
+// mantissa bits
+__device__ __forceinline__ uint32_t par(float v) { return __float_as_uint(v + 12582912.0f) & 1u; }
 
 struct RingSlot {   // one step: its 64 16-byte chunks, lowest address first
   v4u c[kMStep / 16];
@@ -229,7 +224,7 @@ static_assert(kMStep / 16 == kWave, "one LDS-DMA wave-instruction per step");
 // The block's first bytes: a step's chunks lie at block positions a = sb + 16 k, 16-byte aligned
 // in memory while the block is not.  A chunk wholly before the block is zeroed (its DMA read
 // the block's first aligned chunk instead); the chunk holding byte 0 keeps bytes >= 0 only; the
-// 0xFFFFFFFF init is folded into bytes 0..3 (one or two chunks).  a is in [-2048, 2048) here.
+// 0xFFFFFFFF init is folded into bytes 0..3 (one or two chunks, one or two steps).
 __device__ __forceinline__ uint32_t head_dword(uint32_t w, int pos) {
   if (pos >= 4) return w;
   const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
@@ -241,7 +236,7 @@ __device__ __forceinline__ v4u head_chunk(v4u x, int a) {
   if (a >= 4) return x;
   return v4u{head_dword(x.x, a), head_dword(x.y, a + 4), head_dword(x.z, a + 8), head_dword(x.w, a + 12)};
 }
-// the pad after the block's end: t < 16 zero bytes in the step's last chunk (chunk 127 of step 0)
+// the pad after the block's end: t < 16 zero bytes in the last chunk of the block's last step
 __device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
   const uint32_t k = 16u - t;   // bytes kept
   const auto m = [&](uint32_t d) {
@@ -251,20 +246,9 @@ __device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
 }
 
 // s_waitcnt vmcnt(k): a step has landed once at most the k DMA instructions of the k steps
-// issued after it are outstanding (other vector-memory operations of the wave only make the
-// wait stricter: the counter retires in issue order).  The steady state (k = kRing - 1) first.
+// issued after it are outstanding (the counter retires in issue order).  The steady state waits
+// vmcnt(kRing - 1) inline; this is the drain at the end of the wave's blocks.
 __device__ __forceinline__ void wait_ring(uint32_t k) {
-  if (k >= (uint32_t)(kRing - 1)) {
-    switch (kRing - 1) {
-      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); return;
-      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); return;
-      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); return;
-      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); return;
-      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); return;
-      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); return;
-      default: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); return;
-    }
-  }
   switch (k) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
@@ -275,15 +259,35 @@ __device__ __forceinline__ void wait_ring(uint32_t k) {
     default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
   }
 }
-static_assert(kRing >= 2 && kRing <= 8, "wait_ring covers up to 7 steps ahead");
+__device__ __forceinline__ void wait_steady() {
+  static_assert(kRing >= 2 && kRing <= 8, "wait_ring covers up to 7 steps ahead");
+  switch (kRing - 1) {
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+  }
+}
 
-// the lane's two chunks of a landed slot.  Inline asm: the compiler treats an LDS read it can see
-// as aliasing every LDS-DMA in flight and waits vmcnt(0) before it, which would drain the ring;
-// wait_ring has already waited for exactly this slot's DMA.
-__device__ __forceinline__ v4u ring_read(const RingSlot* sl, uint32_t kx) {
+// the lane's chunk of a landed slot, and the step's two stage-2 operands (issued first, so
+// their latency overlaps).  Inline asm: the compiler treats a read of the ring it can see as
+// aliasing every LDS-DMA in flight and waits vmcnt(0) before it, which would drain the ring;
+// wait_ring / wait_steady has already waited for exactly this slot's DMA.
+__device__ __forceinline__ v4u ring_read(const RingSlot* sl, uint32_t kx, const v4i* a2, v4i& lo, v4i& hi) {
   const uint32_t ax = (uint32_t)(uintptr_t)(const lds_void*)&sl->c[kx];
+  const uint32_t aa = (uint32_t)(uintptr_t)(const lds_void*)a2;
   v4u x;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(ax) : "memory");
+  asm volatile(
+      "ds_read_b128 %1, %4\n\t"
+      "ds_read_b128 %2, %4 offset:1024\n\t"
+      "ds_read_b128 %0, %3\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(x), "=&v"(lo), "=&v"(hi)
+      : "v"(ax), "v"(aa)
+      : "memory");
   return x;
 }
 
@@ -321,21 +325,26 @@ __device__ __forceinline__ void crc_store(const uint8_t* d, uint64_t off, bool o
 // a block of the stream (wave-uniform values)
 struct MBlk {
   uint64_t off;     // block offset in the buffer
-  int64_t L;        // content length
-  int64_t Lp;       // L + t: padded to a 16-byte aligned end address
+  int64_t Lp;       // content length + t: padded to a 16-byte aligned end address
   uint32_t t;       // pad bytes, < 16
   uint32_t steps;   // ceil(Lp / 1 KiB)
-  int64_t a0;       // block position of the 16-byte aligned chunk holding byte 0 (in [-15, 0])
+  int32_t sb0;      // block position of the first step's chunk 0: Lp - 1 KiB · steps, in (-1024, 0]
+  int32_t a0;       // block position of the 16-byte aligned chunk holding byte 0 (in [-15, 0])
 };
 __device__ __forceinline__ MBlk mblk(uint64_t base, uint64_t off, uint64_t L) {
   MBlk m;
   m.off = off;
-  m.L = (int64_t)L;
   m.t = (uint32_t)((16u - ((base + off + L) & 15u)) & 15u);
-  m.Lp = m.L + m.t;
+  m.Lp = (int64_t)L + m.t;
   m.steps = (uint32_t)((m.Lp + kMStep - 1) / kMStep);
-  m.a0 = -(int64_t)((base + off) & 15u);
+  m.sb0 = (int32_t)(m.Lp - (int64_t)kMStep * m.steps);
+  m.a0 = -(int32_t)((base + off) & 15u);
   return m;
+}
+__device__ __forceinline__ MBlk mblk_lane(uint64_t base, uint64_t off, uint64_t L, int j) {
+  return mblk(base, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32),
+              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, j));
 }
 
 __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __restrict__ data, uint64_t data_len,
@@ -343,18 +352,19 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
                                                              const uint32_t* __restrict__ blk_len, uint32_t nblk,
                                                              uint32_t* __restrict__ crc_out, uint8_t* __restrict__ bad,
                                                              int framed) {
-  __shared__ v4i sA2[8 * 2 * 64];              // 16 KiB: stage-2 operands
+  __shared__ v4i sA2[kMSup * 2 * 64];          // 16 KiB: stage-2 operands
   __shared__ uint32_t sCol[16][8][16];         // 8 KiB: column shifts
-  __shared__ uint32_t sInv[16][8][16];         // 8 KiB: pad removal
-  __shared__ RingSlot sRing[kMWaves][kRing];   // 128 KiB at 16 waves x 8 steps
+  __shared__ uint32_t sInv[16][8][16];         // 8 KiB: pad removal, t = 1..15; [0]: one super-window
+  __shared__ RingSlot sRing[kMWaves][kRing];   // 112 KiB at 16 waves x 7 steps
   const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
     const v4i* a2 = reinterpret_cast<const v4i*>(&kMfma.a2[0][0][0][0]);
-    for (int i = threadIdx.x; i < 8 * 2 * 64; i += kMThreads) sA2[i] = a2[i];
+    for (int i = threadIdx.x; i < kMSup * 2 * 64; i += kMThreads) sA2[i] = a2[i];
+    // sInv[0] (t = 0: no pad, never looked up) holds the Horner step's table instead
     for (int i = threadIdx.x; i < 16 * 8 * 16; i += kMThreads) {
       (&sCol[0][0][0])[i] = (&kMfma.col[0][0][0])[i];
-      (&sInv[0][0][0])[i] = (&kMfma.inv[0][0][0])[i];
+      (&sInv[0][0][0])[i] = i < 8 * 16 ? (&kMfma.swk[0][0])[i] : (&kMfma.inv[0][0][0])[i];
     }
   }
   v4i A[kMKs][2];
@@ -369,10 +379,12 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
   for (int t = 0; t < kMKs; ++t) asm volatile("" ::"v"(A[t][0]), "v"(A[t][1]));
   __syncthreads();
   RingSlot* ring = sRing[wv];
+  const v4i* a2l = sA2 + lane;   // stage-2 operand of step t, row half h: a2l[(2 t + h) * 64] (64 v4i = 1 KiB)
   const uint64_t base = (uint64_t)(uintptr_t)data;
   const uint32_t W = gridDim.x * kMWaves;
   const uint32_t w0 = blockIdx.x * kMWaves + wv;
   const uint32_t kx = 60u - 4u * (uint32_t)n + (uint32_t)g;   // the lane's chunk of a step
+  const int32_t lane16 = 16 * lane;
 
   // the wave's blocks w0 + k W, 64 at a time: lane j holds block k = 64 m + j of window m
   for (uint64_t kb = 0; w0 + kb * W < nblk; kb += kWave) {
@@ -390,116 +402,117 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
     const uint64_t em = __ballot(elig);
     uint32_t res = 0;   // lane j: the checksum of block j of the window
 
-    // issue cursor: step is of block ij;   compute cursor: step cs of block cj
+    // issue cursor: step `is` (counted from the block start) of the block whose first step's
+    // chunk 0 is at ip0, into ring slot islot
     uint64_t irest = em;
-    uint32_t is = 0, issued = 0, done = 0;
-    MBlk I{};
-    bool ilive = irest != 0;
-    if (ilive) {
-      const int j = __builtin_ctzll(irest);
-      irest &= irest - 1;
-      I = mblk(base, (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
-                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32),
-               (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, j));
-    }
-    auto issue = [&]() {
-      RingSlot* sl = ring + (issued % kRing);
-      const int64_t sb = I.Lp - (int64_t)kMStep * (is + 1);      // block position of chunk 0
-      const int64_t px = sb + 16 * lane;
-      // chunks wholly before the block load its first aligned chunk instead (zeroed on read)
-      const uint8_t* p = data + I.off + (px + 16 > 0 ? px : I.a0);
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)&sl->c[0], 16, 0, MTBLX_CRC_DMA_AUX);
-      ++issued;
-      if (++is == I.steps) {
+    uint32_t is = 0, isteps = 0, islot = 0, pend = 0;
+    const uint8_t* ip = data;     // chunk 0 of step is
+    const uint8_t* ihead = data;  // the block's first aligned chunk
+    int32_t isb0 = 0;
+    bool ilive = false;
+    auto inext = [&]() {
+      ilive = irest != 0;
+      if (ilive) {
+        const MBlk m = mblk_lane(base, off, L, __builtin_ctzll(irest));
+        irest &= irest - 1;
         is = 0;
-        ilive = irest != 0;
-        if (ilive) {
-          const int j = __builtin_ctzll(irest);
-          irest &= irest - 1;
-          I = mblk(base, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
-                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32),
-                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, j));
-        }
+        isteps = m.steps;
+        isb0 = m.sb0;
+        ip = data + m.off + m.sb0;   // before the block start for a head step: those lanes are redirected
+        ihead = data + m.off + m.a0;
       }
     };
-    while (ilive && issued < (uint32_t)(kRing - 1)) issue();
+    auto issue = [&]() {
+      const uint8_t* p = ip + lane16;
+      if (is == 0) {   // the block's first step: chunks wholly before the block (zeroed on read)
+        asm volatile("");   // a branch, not a select in every step
+        if (isb0 + lane16 + 16 <= 0) p = ihead;
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)&ring[islot].c[0], 16, 0, MTBLX_CRC_DMA_AUX);
+      islot = islot + 1 == (uint32_t)kRing ? 0u : islot + 1;
+      ip += kMStep;
+      if (++is == isteps) inext();
+    };
+    inext();
+    while (ilive && pend < (uint32_t)(kRing - 1)) {
+      issue();
+      ++pend;
+    }
 
     uint64_t crest = em;
-    MBlk Cb{};
-    int cj = 0;
-    bool clive = crest != 0;
-    auto cnext = [&]() {
-      clive = crest != 0;
-      if (clive) {
-        cj = __builtin_ctzll(crest);
-        crest &= crest - 1;
-        Cb = mblk(base, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, cj) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), cj) << 32),
-                  (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, cj));
-      }
-    };
-    cnext();
-    uint32_t cs = 0, acc = 0, accS = 0;
-    v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
-    v4i bb = {0, 0, 0, 0};   // stage-2 operand: dword d = step 4 jq + d of the quad (shifted in)
-    while (clive) {
-      if (ilive && issued - done < (uint32_t)kRing) issue();
-      wait_ring(issued - done - 1 < (uint32_t)(kRing - 1) ? issued - done - 1 : (uint32_t)(kRing - 1));
-      v4u x = ring_read(ring + (done % kRing), kx);
-      ++done;
-      const int64_t sb = Cb.Lp - (int64_t)kMStep * (cs + 1);
-      if (cs == 0 && Cb.t != 0 && lane == 48) x = tail_chunk(x, Cb.t);   // lane (g 3, n 0): chunk 63
-      if (sb < 4) x = head_chunk(x, (int)sb + 16 * (int)kx);   // the block's first bytes (sb > -1024)
-#if MTBLX_CRC_ABL == 1
-      acc ^= x.x ^ x.y ^ x.z ^ x.w;
-#else
-      const uint32_t w[kMKs] = {x.x, x.y, x.z, x.w};
-      v4f c1a = {0.f, 0.f, 0.f, 0.f}, c1b = c1a;
-#pragma unroll
-      for (int t = 0; t < kMKs; ++t) {
-        const uint32_t v = w[t];
-        const v4i b = {(int)(v & 0x11111111u), (int)(v & 0x22222222u), (int)(v & 0x44444444u),
-                       (int)((v >> 1) & 0x44444444u)};
-        c1a = mfma_fp4(A[t][0], b, c1a);
-        c1b = mfma_fp4(A[t][1], b, c1b);
-      }
-      bb = v4i{bb.y, bb.z, bb.w, (int)pack_window(c1a, c1b)};
-#endif
-      const bool last = cs + 1 == Cb.steps;
-      if ((cs & 3u) == 3u || last) {
-        for (uint32_t r = cs & 3u; r < 3u; ++r) bb = v4i{bb.y, bb.z, bb.w, 0};   // a partial last quad
-        const uint32_t jq = (cs >> 2) & 7u;
-        c2a = mfma_fp4(sA2[(2 * jq) * 64 + lane], bb, c2a);
-        c2b = mfma_fp4(sA2[(2 * jq + 1) * 64 + lane], bb, c2b);
-        bb = v4i{0, 0, 0, 0};
-        if (jq == 7u || last) {   // super-window done: each column's raw CRC, shifted into place
-          uint32_t dv = 0;
-          const uint32_t sh = 4u * (uint32_t)g;
-          dv |= (par_bits(c2a.x, kMag0) & 1u) << (sh + 0);
-          dv |= (par_bits(c2a.y, kMag0) & 1u) << (sh + 1);
-          dv |= (par_bits(c2a.z, kMag0) & 1u) << (sh + 2);
-          dv |= (par_bits(c2a.w, kMag0) & 1u) << (sh + 3);
-          dv |= (par_bits(c2b.x, kMag0) & 1u) << (sh + 16);
-          dv |= (par_bits(c2b.y, kMag0) & 1u) << (sh + 17);
-          dv |= (par_bits(c2b.z, kMag0) & 1u) << (sh + 18);
-          dv |= (par_bits(c2b.w, kMag0) & 1u) << (sh + 19);
-          const uint32_t S = cs >> 5;
-          if (S == 0) acc ^= dv;
-          else if (S < 16) accS ^= mul_nib(dv, kMfma.sw[S]);
-          else accS ^= dmultmodp(xpow8((uint64_t)S * (uint64_t)(kMStep * kMSup)), dv);
-          c2a = v4f{0.f, 0.f, 0.f, 0.f};
-          c2b = c2a;
+    uint32_t cslot = 0;
+    while (crest) {
+      const int cj = __builtin_ctzll(crest);
+      crest &= crest - 1;
+      const MBlk Cb = mblk_lane(base, off, L, cj);
+      uint32_t s = Cb.steps - 1;   // the step's window numbering: steps from the block's end
+      int32_t sbc = Cb.sb0;        // block position of the step's chunk 0, while < 4
+      uint32_t acc = 0;
+      bool first_sw = true;
+      v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
+      for (;;) {
+        if (ilive) {   // steady state: kRing - 1 steps stay in flight behind this one
+          issue();
+          wait_steady();
+        } else {
+          wait_ring(pend - 1);
+          --pend;
         }
-      }
-      if (!last) {
-        ++cs;
+        const uint32_t t = s & (uint32_t)(kMSup - 1);
+        v4i a2lo, a2hi;
+        v4u x = ring_read(ring + cslot, kx, a2l + 2 * t * 64, a2lo, a2hi);
+        cslot = cslot + 1 == (uint32_t)kRing ? 0u : cslot + 1;
+        if (sbc < 4) {   // the block's first bytes (sbc > -1024)
+          x = head_chunk(x, sbc + 16 * (int)kx);
+          sbc += kMStep;
+        }
+        if (s == 0 && Cb.t != 0) {   // the pad after the block's end: lane (g 3, n 0) holds chunk 63
+          asm volatile("");          // a branch, not a select in every step
+          if (lane == 48) x = tail_chunk(x, Cb.t);
+        }
+#if MTBLX_CRC_ABL == 1
+        acc ^= x.x ^ x.y ^ x.z ^ x.w;
+        (void)t;
+        if (s == 0) break;
+        --s;
         continue;
+#else
+        const uint32_t w[kMKs] = {x.x, x.y, x.z, x.w};
+        v4f c1a = {0.f, 0.f, 0.f, 0.f}, c1b = c1a;
+#pragma unroll
+        for (int k = 0; k < kMKs; ++k) {
+          const uint32_t v = w[k];
+          const v4i b = {(int)(v & 0x11111111u), (int)(v & 0x22222222u), (int)(v & 0x44444444u),
+                         (int)((v >> 1) & 0x44444444u)};
+          c1a = mfma_fp4(A[k][0], b, c1a);
+          c1b = mfma_fp4(A[k][1], b, c1b);
+        }
+        const v4i b2 = {pk16(c1a.x, c1a.y), pk16(c1a.z, c1a.w), pk16(c1b.x, c1b.y), pk16(c1b.z, c1b.w)};
+        c2a = mfma_f16(a2lo, b2, c2a);
+        c2b = mfma_f16(a2hi, b2, c2b);
+        if (t != 0) {
+          --s;
+          continue;
+        }
+        // super-window done: the column's raw CRC bits 4g + i and 16 + 4g + i, Horner-combined
+        // with the super-windows before it (nearer the block start)
+        const uint32_t sh = 4u * (uint32_t)g;
+        uint32_t dv = (par(c2a.x) | (par(c2a.y) << 1) | (par(c2a.z) << 2) | (par(c2a.w) << 3)) << sh;
+        dv |= (par(c2b.x) | (par(c2b.y) << 1) | (par(c2b.z) << 2) | (par(c2b.w) << 3)) << (sh + 16);
+        acc = first_sw ? dv : mul_nib(acc, sInv[0]) ^ dv;
+        first_sw = false;
+        c2a = v4f{0.f, 0.f, 0.f, 0.f};
+        c2b = c2a;
+        if (s == 0) break;
+        --s;
+#endif
       }
-      // block done: column shifts, XOR over all 64 lanes, pad removal.  acc0 (the first super-
-      // window) holds only the lane's own 8 bits of its column -- nibbles g and 4 + g -- so the
-      // column shift takes 2 lookups; later super-windows (accS) were shifted to full words.
-      uint32_t c = sCol[n][g][(acc >> (4 * g)) & 15u] ^ sCol[n][4 + g][(acc >> (16 + 4 * g)) & 15u];
-      if (Cb.steps > (uint32_t)kMSup) c ^= mul_nib(accS, sCol[n]);
+      // block done: column shift, XOR over all 64 lanes, pad removal.  With one super-window acc
+      // holds only the lane's own 8 bits of its column -- nibbles g and 4 + g -- so the column
+      // shift takes 2 lookups; after a Horner step it is a full word.
+      uint32_t c = Cb.steps <= (uint32_t)kMSup
+                       ? sCol[n][g][(acc >> (4 * g)) & 15u] ^ sCol[n][4 + g][(acc >> (16 + 4 * g)) & 15u]
+                       : mul_nib(acc, sCol[n]);
       c = row_xor(c);                                          // over the 16 columns of a row
       uint32_t C = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 16) ^
                    (uint32_t)__builtin_amdgcn_readlane((int)c, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
@@ -509,10 +522,6 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
         C = (uint32_t)__builtin_amdgcn_readlane((int)row_xor(v), 0);
       }
       if (lane == cj) res = C ^ 0xFFFFFFFFu;
-      acc = 0;
-      accS = 0;
-      cs = 0;
-      cnext();
     }
     // blocks the MFMA path does not take: < 4 bytes, windows past the buffer, unaligned chunks
     // outside it (a block at the very start / end of an unaligned buffer)
@@ -554,7 +563,7 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   // 0.102 vs 0.120 ms on cfg2 (profiles/r04/crc_mfma)
   const char* kv = getenv("MTBLX_CRC_KERNEL");
   if (!kv || kv[0] != 'l') {
-    static int mgrid = 0;   // persistent: one 8-wave workgroup (152 KiB LDS) per CU
+    static int mgrid = 0;   // persistent: one 16-wave workgroup (144.5 KiB LDS) per CU
     if (!mgrid) {
       int dev = 0, ncu = 0;
       (void)hipGetDevice(&dev);

@@ -8,12 +8,15 @@
 //   stage 1  C1 = M_w · window bits            16x16x128 fp4 MFMA, K = 512 over 4 k-steps,
 //            (rows = CRC bits, columns = the     two row halves per k-step
 //             step's 16 windows)
-//   stage 2  per column, the steps of a super-window (32 steps = 32 KiB) shifted by
-//            x^(8·1024·t) and summed: [S_0 .. S_31] · parity(C1), one fp4 MFMA pair per 4 steps
-//   stage 3  per column, x^(8·32768·S) · parity(C2_S) summed over super-windows S (nibble
-//            tables sw), then the column shift x^(8·64·n) (nibble tables col) and an XOR over
-//            the 16 columns: the raw CRC of the block padded with t < 16 zero bytes to a 16-byte
-//            aligned end, times x^(-8t) (nibble tables inv): the block's raw CRC
+//   stage 2  per column, the steps t of a super-window (kMSup = 8 steps = 8 KiB) shifted by
+//            x^(8·1024·t) and summed: S_t · C1_t, one 16x16x32 f16 MFMA pair per step on the
+//            UNREDUCED integer sums (exact in f16 below 2048; their parity is linear, so the
+//            GF(2) shift applied to the integers keeps the parity of the shifted result)
+//   stage 3  per column, Horner over the super-windows from the block's start: acc = acc ·
+//            x^(8·8192) + parity(C2_S) (nibble table swk), then the column shift x^(8·64·n)
+//            (nibble tables col) and an XOR over the 16 columns: the raw CRC of the block padded
+//            with t < 16 zero bytes to a 16-byte aligned end, times x^(-8t) (nibble tables inv):
+//            the block's raw CRC
 // The reference's checksum is crate crc32c 0.4 over each block's stored bytes
 // (/root/reference/src/reader.rs:159-164); polynomial and tables as crc_dev.h.
 //
@@ -26,6 +29,10 @@
 //      w & 0x11111111, w & 0x22222222, w & 0x44444444, (w >> 1) & 0x44444444: slot (q, i) is bit
 //      4i + q of w, as an e2m1 value 0.5 / 1 / 2 / 2 (q = 0 / 1 / 2 / 3).
 //   A: the matching entry times 2 / 1 / 0.5 / 0.5, so every product of two set bits is exactly 1.
+// The stage-2 f16 MFMA (8 halves per lane, again the same K in the same slot of A and B): B lane
+// (g, n) slot j = the stage-1 sum of CRC row rho(g, j) = (j < 4 ? 4g + j : 16 + 4g + j - 4) of
+// window n -- exactly the lane's C1 registers in order, packed by v_cvt_pkrtz; A lane (g, r) slot
+// j = bit r (row half 0) or 16 + r (half 1) of S_t(e_rho) as 1.0 / 0.0.
 // C/D (dtype-independent on gfx950): lane l, register i = row 4 (l >> 4) + i, column l & 15.
 #pragma once
 #include <stdint.h>
@@ -37,13 +44,14 @@ namespace mtblx_crc {
 constexpr int kMWin = 64;             // stage-1 window: bytes of one column per 4 k-steps
 constexpr int kMKs = kMWin / 16;       // k-steps per window (one raw dword of the lane each)
 constexpr int kMStep = 16 * kMWin;     // a step: 16 consecutive windows of one block, 1 KiB
-constexpr int kMSup = 32;              // steps per super-window (stage 2): 32 KiB
+constexpr int kMSup = 8;               // steps per super-window (stage 2): 8 KiB
 constexpr uint32_t kFp4Half = 0x1u, kFp4One = 0x2u, kFp4Two = 0x4u;   // e2m1 codes of 0.5, 1, 2
+constexpr uint32_t kF16One = 0x3C00u;                                 // f16 1.0
 
 struct MfmaTabs {
   uint32_t a[kMKs][2][64][4];   // stage-1 A operand: [k-step][row half][lane][dword]
-  uint32_t a2[8][2][64][4];   // stage-2 A operand: [step quad][row half][lane][dword]
-  uint32_t sw[16][8][16];     // nibble tables of x^(8·32768·S), S < 16 (stage 3)
+  uint32_t a2[kMSup][2][64][4];   // stage-2 f16 A operand: [step][row half][lane][dword]
+  uint32_t swk[8][16];            // nibble tables of x^(8·1024·kMSup): one super-window (stage 3)
   uint32_t col[16][8][16];    // nibble tables of x^(8·64·n): the column shift, n < 16
   uint32_t inv[16][8][16];    // nibble tables of x^(-8 t), t < 16: t zero bytes appended, removed
   uint32_t max_row;           // largest popcount of an M_w row (the stage-1 sums stay below it)
@@ -55,7 +63,7 @@ struct MfmaTabs {
   static constexpr uint32_t unx(uint32_t c) {   // c · x^-1: one step of the reflected CRC undone
     return (c & 0x80000000u) ? (((c ^ kPoly) << 1) | 1u) : (c << 1);
   }
-  constexpr MfmaTabs() : a(), a2(), sw(), col(), inv(), max_row(0) {
+  constexpr MfmaTabs() : a(), a2(), swk(), col(), inv(), max_row(0) {
     // column of M_w for window byte p, bit b: raw CRC of a kMWin-byte message holding only that bit
     uint32_t mcol[kMWin][8] = {};
     for (int b = 0; b < 8; ++b) {
@@ -103,16 +111,14 @@ struct MfmaTabs {
       }
       K = multmodp(xs, K);
     }
-    // stage-2 B: lane (g, n), dword d = step 4 jq + d of the quad, nibble e = 4 h1 + i holds the
-    // parity of C1[h1][i] = CRC bit 16 h1 + 4 g + i of that window, as 0.5 -> A entry 2
-    for (int jq = 0; jq < 8; ++jq)
+    // stage-2 A (f16): lane (g, r), half h, slot j -> dword j >> 1, half j & 1
+    for (int t = 0; t < kMSup; ++t)
       for (int h = 0; h < 2; ++h)
         for (int l = 0; l < 64; ++l) {
           const int g = l >> 4, ro = 16 * h + (l & 15);
-          for (int s = 0; s < 32; ++s) {
-            const int d = s >> 3, e = s & 7;
-            const int tw = 4 * jq + d, r = 16 * (e >> 2) + 4 * g + (e & 3);
-            if ((S[tw][r] >> ro) & 1u) a2[jq][h][l][d] |= kFp4Two << (4 * e);
+          for (int j = 0; j < 8; ++j) {
+            const int rho = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
+            if ((S[t][rho] >> ro) & 1u) a2[t][h][l][j >> 1] |= kF16One << (16 * (j & 1));
           }
         }
     uint32_t U = 0x80000000u;   // x^(-8 t)
@@ -120,12 +126,7 @@ struct MfmaTabs {
       MulTabs::fill(inv[t], U);
       for (int k = 0; k < 8; ++k) U = unx(U);
     }
-    // K = x^(8·32768) now; stage 3 nibble tables of its powers
-    uint32_t P = 0x80000000u;
-    for (int s = 0; s < 16; ++s) {
-      MulTabs::fill(sw[s], P);
-      P = multmodp(K, P);
-    }
+    MulTabs::fill(swk, K);   // K = x^(8·1024·kMSup) now
   }
 };
 

@@ -19,6 +19,13 @@
 #include "crc_dev.h"
 #include "mtblx.h"
 
+// Ablations (outputs incomplete by construction) and the spilling variant build only through the
+// Makefile's diagnostic targets, which define MTBLX_DIAG; the product build rejects them.
+#if (defined(MTBLX_ABL_NOKEY) || defined(MTBLX_ABL_NOVAL) || defined(MTBLX_ABL_NOVSTORE) || \
+     defined(MTBLX_ABL_CRC) || defined(MTBLX_SPILL)) && !defined(MTBLX_DIAG)
+#error "ablation / spill knobs are diagnostic: build them through a Makefile diagnostic target (-DMTBLX_DIAG)"
+#endif
+
 namespace mtblx {
 
 constexpr int kWave = 64;

@@ -39,6 +39,11 @@
 #include <string.h>
 
 #include "mtblx.h"
+
+// timing ablations (wrong output by construction): diagnostic targets only (-DMTBLX_DIAG)
+#if (defined(MTBLX_SNAP_ABL_NOSTORE) || defined(MTBLX_LANE_ABL_NOFAR)) && !defined(MTBLX_DIAG)
+#error "snappy ablation knobs are diagnostic: build them through a Makefile diagnostic target (-DMTBLX_DIAG)"
+#endif
 #include "mtblx_host.h"
 
 namespace mtblx_snap {

@@ -7,7 +7,7 @@ O=gpurun_out/${1:-crcm}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_crc_mfma_gpu.py > $O/tests.log 2>&1 || exit 1
-timeout -k 10 300 python -u scripts/crc_ab.py mfma lanes > $O/crc_ab.log 2>&1 || exit 2
+timeout -k 10 300 python -u scripts/crc_ab.py ${AB:-mfma lanes} > $O/crc_ab.log 2>&1 || exit 2
 timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 P="rocprofv3 --output-format csv"
 timeout -k 10 120 $P --kernel-trace --stats -d $O/stats -o run -- python3 scripts/crc_probe.py > $O/stats.log 2>&1 || exit 3

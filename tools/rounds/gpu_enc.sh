@@ -8,4 +8,4 @@ timeout -k 10 400 python -u -m pytest tests/test_encode_gpu.py tests/test_writer
 rc=$?; tail -3 gpurun_out/t_enc.log; [ $rc -ne 0 ] && exit $rc
 MTBLX_ENC_STAMPS_PRINT=1 timeout -k 10 300 python bench.py --config cfg3 --cfg3-blocks 100000 --no-cpu-baseline --lib oxidized-mtbl_amd/build/libmtblx_estamps.so > gpurun_out/estamps.log 2>&1 || exit 3
 grep "enc stamps" gpurun_out/estamps.log
-LIBS="${LIBS:-cur=}" bash scripts/gpu_ab_enc.sh
+LIBS="${LIBS:-cur=}" bash tools/rounds/gpu_ab_enc.sh

@@ -15,4 +15,4 @@ for v in encp encq enc8; do
   rc=$?; tail -2 $O/t_$v.log; [ $rc -ne 0 ] && { echo "STOP t_$v rc=$rc"; exit $rc; }
 done
 LIBS="cur= encp=oxidized-mtbl_amd/build/libmtblx_encp.so encq=oxidized-mtbl_amd/build/libmtblx_encq.so enc8=oxidized-mtbl_amd/build/libmtblx_enc8.so" \
-  TAG=persist bash scripts/gpu_enc_r03.sh ab
+  TAG=persist bash tools/rounds/gpu_enc_r03.sh ab

@@ -2,7 +2,7 @@
 # profiles/r03 evidence: the driver's bench command under rocprofv3 (kernel trace: per-launch
 # durations of the timed steps), separate FETCH_SIZE / WRITE_SIZE passes for `traffic`, cfg2 at
 # cfg4's 4 KiB-leg size, and the cfg4 line under a kernel trace.  Outputs under
-# gpurun_out/r03/ev_$TAG/; scripts/summarize_r03.py turns them into profiles/r03/.
+# gpurun_out/r03/ev_$TAG/; tools/rounds/summarize_r03.py turns them into profiles/r03/.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

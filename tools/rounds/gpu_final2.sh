@@ -3,8 +3,8 @@
 # the CRC grid A/B (2 vs 1 workgroups per CU)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-TAG=final2 bash scripts/gpu_r03.sh tests || exit 1
-TAG=final2 bash scripts/gpu_r03.sh bench || exit 2
+TAG=final2 bash tools/rounds/gpu_r03.sh tests || exit 1
+TAG=final2 bash tools/rounds/gpu_r03.sh bench || exit 2
 O=gpurun_out/r03/final2
 for r in 1 2; do
   for v in prod crc1; do

@@ -8,4 +8,4 @@ timeout -k 10 400 python -u -m pytest tests/test_decode_gpu.py tests/test_cfg4_g
   -k "key_tails or 64k or cfg4 or large or workspace" > gpurun_out/t_late.log 2>&1
 rc=$?; tail -4 gpurun_out/t_late.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --config cfg3 --cfg3-blocks 100000 --stamps --no-cpu-baseline > gpurun_out/stamps_cfg3_late.log 2>&1 || exit 3
-LIBS="${LIBS:-cur= late0=oxidized-mtbl_amd/build/libmtblx_late0.so lc=oxidized-mtbl_amd/build/libmtblx_lc.so}" CFGS="${CFGS:-cfg3 large}" bash scripts/gpu_ab.sh
+LIBS="${LIBS:-cur= late0=oxidized-mtbl_amd/build/libmtblx_late0.so lc=oxidized-mtbl_amd/build/libmtblx_lc.so}" CFGS="${CFGS:-cfg3 large}" bash tools/rounds/gpu_ab.sh

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """profiles/r02/cfg3/: k_decode_pipe<PipeLarge> and k_encode on one cfg3 chunk, from a
-scripts/gpu_profile_cfg3.sh run (gpurun_out/prof_cfg3).  Per kernel: average duration, PMC bytes
+tools/rounds/gpu_profile_cfg3.sh run (gpurun_out/prof_cfg3).  Per kernel: average duration, PMC bytes
 per launch (FETCH_SIZE x 2, the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE; both KiB)
 against the bench's algorithmic bytes per launch, and SQ wait / active fractions."""
 import csv

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """profiles/r02/decode/: the decode kernel before (round-1 final) and after (current), from a
-scripts/gpu_profile_r02.sh run (gpurun_out/prof_r02).  Copies the kernel stats and PMC rows
+tools/rounds/gpu_profile_r02.sh run (gpurun_out/prof_r02).  Copies the kernel stats and PMC rows
 of the decode kernel and writes summary.json / summary.md.  FETCH_SIZE is doubled (gfx950
 reports half the bytes of wide streaming reads, MI355X_MICROARCH.md); both are KiB."""
 import csv

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""profiles/r03/<tag>/ from a scripts/gpu_evidence_r03.sh run (gpurun_out/r03/ev_<tag>/).
+"""profiles/r03/<tag>/ from a tools/rounds/gpu_evidence_r03.sh run (gpurun_out/r03/ev_<tag>/).
 
 driver/: the driver's command (`bench.py --gpus 1 --steps 20 --warmup 5`) under
   rocprofv3 --kernel-trace --stats.  The timed steps are the LAST K launches of the bench's

@@ -173,7 +173,8 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
 static __constant__ MfmaTabs kMfma = MfmaTabs();
 static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in f16 and in the stage-2 sums");
 
-// MTBLX_CRC_ABL=1 (diagnostic, wrong checksums by construction): the ring without stage 1/2
+// MTBLX_CRC_ABL (diagnostic, wrong checksums by construction): 1 = the ring without stage 1/2,
+// 2 = stage 1/2 on whatever the ring holds, no block reads
 #if defined(MTBLX_CRC_ABL) && !defined(MTBLX_DIAG)
 #error "MTBLX_CRC_ABL is an ablation: build it only through a diagnostic target (-DMTBLX_DIAG)"
 #endif
@@ -184,7 +185,7 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in
 #define MTBLX_CRC_MWAVES 16
 #endif
 #ifndef MTBLX_CRC_RING
-#define MTBLX_CRC_RING 7
+#define MTBLX_CRC_RING 8
 #endif
 #ifndef MTBLX_CRC_DMA_AUX
 #define MTBLX_CRC_DMA_AUX 2   // non-temporal: the block bytes are read once
@@ -192,6 +193,7 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in
 constexpr int kMWaves = MTBLX_CRC_MWAVES;      // waves per workgroup, one workgroup per CU
 constexpr int kMThreads = kMWaves * kWave;
 constexpr int kRing = MTBLX_CRC_RING;          // steps per wave ring (1 KiB each)
+static_assert((kRing & (kRing - 1)) == 0, "ring offsets wrap by a mask");
 constexpr int kMTabLds = kMSup * 2 * 64 * 16 + 2 * 16 * 8 * 16 * 4;   // 32 KiB
 static_assert(kMTabLds + kMWaves * kRing * kMStep <= 160 * 1024, "LDS: tables + rings");
 
@@ -212,9 +214,15 @@ __device__ __forceinline__ v4f mfma_f16(v4i a, v4i b, v4f c) {
 // two stage-1 sums as f16 (integers below 2048: exact)
 __device__ __forceinline__ int pk16(float a, float b) { return __builtin_bit_cast(int, __builtin_amdgcn_cvt_pkrtz(a, b)); }
 
-// parity of an exact integer-valued sum v (0 <= v < 2^22): v + 1.5·2^23 keeps v in the low
-// mantissa bits
-__device__ __forceinline__ uint32_t par(float v) { return __float_as_uint(v + 12582912.0f) & 1u; }
+// the parities of four exact integer-valued sums (0 <= v < 2^19) as a nibble: v + 1.5·2^(23-k)
+// keeps v · 2^k in the low mantissa bits, so bit k of the sum's bits is v's parity
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (mask & a) | (~mask & b); }
+__device__ __forceinline__ uint32_t par_nib(v4f v) {
+  uint32_t x = __float_as_uint(v.x + 12582912.0f) & 1u;
+  x = bfi(2u, __float_as_uint(v.y + 6291456.0f), x);
+  x = bfi(4u, __float_as_uint(v.z + 3145728.0f), x);
+  return bfi(8u, __float_as_uint(v.w + 1572864.0f), x);
+}
 
 struct RingSlot {   // one step: its 64 16-byte chunks, lowest address first
   v4u c[kMStep / 16];
@@ -272,13 +280,11 @@ __device__ __forceinline__ void wait_steady() {
   }
 }
 
-// the lane's chunk of a landed slot, and the step's two stage-2 operands (issued first, so
-// their latency overlaps).  Inline asm: the compiler treats a read of the ring it can see as
-// aliasing every LDS-DMA in flight and waits vmcnt(0) before it, which would drain the ring;
-// wait_ring / wait_steady has already waited for exactly this slot's DMA.
-__device__ __forceinline__ v4u ring_read(const RingSlot* sl, uint32_t kx, const v4i* a2, v4i& lo, v4i& hi) {
-  const uint32_t ax = (uint32_t)(uintptr_t)(const lds_void*)&sl->c[kx];
-  const uint32_t aa = (uint32_t)(uintptr_t)(const lds_void*)a2;
+// the lane's chunk of a landed slot (LDS address ax), and the step's two stage-2 operands (aa,
+// aa + 1 KiB; issued first, so their latency overlaps).  Inline asm: the compiler treats a read
+// of the ring it can see as aliasing every LDS-DMA in flight and waits vmcnt(0) before it, which
+// would drain the ring; wait_ring / wait_steady has already waited for exactly this slot's DMA.
+__device__ __forceinline__ v4u ring_read(uint32_t ax, uint32_t aa, v4i& lo, v4i& hi) {
   v4u x;
   asm volatile(
       "ds_read_b128 %1, %4\n\t"
@@ -322,29 +328,24 @@ __device__ __forceinline__ void crc_store(const uint8_t* d, uint64_t off, bool o
   }
 }
 
-// a block of the stream (wave-uniform values)
+// a block of the stream (wave-uniform values, read from the lane that holds the block)
 struct MBlk {
-  uint64_t off;     // block offset in the buffer
-  int64_t Lp;       // content length + t: padded to a 16-byte aligned end address
-  uint32_t t;       // pad bytes, < 16
-  uint32_t steps;   // ceil(Lp / 1 KiB)
-  int32_t sb0;      // block position of the first step's chunk 0: Lp - 1 KiB · steps, in (-1024, 0]
-  int32_t a0;       // block position of the 16-byte aligned chunk holding byte 0 (in [-15, 0])
+  const uint8_t* p;   // the block's first byte
+  uint32_t steps;     // ceil(Lp / 1 KiB), Lp = content length + t: padded to a 16-byte aligned end
+  uint32_t t;         // pad bytes, < 16
+  int32_t sb0;        // block position of the first step's chunk 0: Lp - 1 KiB · steps, in (-1024, 0]
+  int32_t a0;         // block position of the 16-byte aligned chunk holding byte 0 (in [-15, 0])
 };
-__device__ __forceinline__ MBlk mblk(uint64_t base, uint64_t off, uint64_t L) {
+__device__ __forceinline__ MBlk mblk_lane(const uint8_t* data, uint64_t off, uint32_t pk, int32_t sb0, int j) {
   MBlk m;
-  m.off = off;
-  m.t = (uint32_t)((16u - ((base + off + L) & 15u)) & 15u);
-  m.Lp = (int64_t)L + m.t;
-  m.steps = (uint32_t)((m.Lp + kMStep - 1) / kMStep);
-  m.sb0 = (int32_t)(m.Lp - (int64_t)kMStep * m.steps);
-  m.a0 = -(int32_t)((base + off) & 15u);
+  m.p = data + ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32));
+  const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)pk, j);
+  m.steps = q & 0x7FFFFFu;
+  m.t = (q >> 23) & 15u;
+  m.a0 = -(int32_t)(q >> 27);
+  m.sb0 = __builtin_amdgcn_readlane(sb0, j);
   return m;
-}
-__device__ __forceinline__ MBlk mblk_lane(uint64_t base, uint64_t off, uint64_t L, int j) {
-  return mblk(base, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, j) |
-                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), j) << 32),
-              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L, j));
 }
 
 __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __restrict__ data, uint64_t data_len,
@@ -355,7 +356,7 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
   __shared__ v4i sA2[kMSup * 2 * 64];          // 16 KiB: stage-2 operands
   __shared__ uint32_t sCol[16][8][16];         // 8 KiB: column shifts
   __shared__ uint32_t sInv[16][8][16];         // 8 KiB: pad removal, t = 1..15; [0]: one super-window
-  __shared__ RingSlot sRing[kMWaves][kRing];   // 112 KiB at 16 waves x 7 steps
+  __shared__ RingSlot sRing[kMWaves][kRing];   // 128 KiB at 16 waves x 8 steps
   const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
@@ -378,13 +379,17 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
 #pragma unroll
   for (int t = 0; t < kMKs; ++t) asm volatile("" ::"v"(A[t][0]), "v"(A[t][1]));
   __syncthreads();
-  RingSlot* ring = sRing[wv];
-  const v4i* a2l = sA2 + lane;   // stage-2 operand of step t, row half h: a2l[(2 t + h) * 64] (64 v4i = 1 KiB)
   const uint64_t base = (uint64_t)(uintptr_t)data;
   const uint32_t W = gridDim.x * kMWaves;
   const uint32_t w0 = blockIdx.x * kMWaves + wv;
   const uint32_t kx = 60u - 4u * (uint32_t)n + (uint32_t)g;   // the lane's chunk of a step
+  // LDS addresses: the wave's ring (slot k at + 1 KiB k), the lane's chunk in slot 0, and the
+  // lane's stage-2 operand of step 0, half 0 (step t, half h: + 2 KiB t + 1 KiB h)
+  const uint32_t ring_base = (uint32_t)(uintptr_t)(const lds_void*)&sRing[wv][0];
+  const uint32_t ring_lane = ring_base + 16u * kx;
+  const uint32_t a2_lane = (uint32_t)(uintptr_t)(const lds_void*)&sA2[lane];
   const int32_t lane16 = 16 * lane;
+  constexpr uint32_t kRingMask = (uint32_t)(kRing * kMStep) - 1u;
 
   // the wave's blocks w0 + k W, 64 at a time: lane j holds block k = 64 m + j of window m
   for (uint64_t kb = 0; w0 + kb * W < nblk; kb += kWave) {
@@ -401,37 +406,44 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
                       ((base + off + L + 15u) & ~15ull) <= base + data_len;
     const uint64_t em = __ballot(elig);
     uint32_t res = 0;   // lane j: the checksum of block j of the window
+    // the lane's block parameters, packed for the cursors' readlanes: steps (23 bits), t, -a0
+    const uint32_t bt = (uint32_t)((16u - ((base + off + L) & 15u)) & 15u);
+    const uint64_t Lp = L + bt;
+    const uint32_t bsteps = (uint32_t)((Lp + kMStep - 1) / kMStep);
+    const uint32_t pk = bsteps | (bt << 23) | ((uint32_t)((base + off) & 15u) << 27);
+    const int32_t bsb0 = (int32_t)(uint32_t)(Lp - (uint64_t)kMStep * bsteps);
 
-    // issue cursor: step `is` (counted from the block start) of the block whose first step's
-    // chunk 0 is at ip0, into ring slot islot
+    // issue cursor: the next step to load is at ip (block I, irem steps left, ihd: its first)
     uint64_t irest = em;
-    uint32_t is = 0, isteps = 0, islot = 0, pend = 0;
-    const uint8_t* ip = data;     // chunk 0 of step is
-    const uint8_t* ihead = data;  // the block's first aligned chunk
-    int32_t isb0 = 0;
-    bool ilive = false;
+    uint32_t irem = 0, ioff = 0, pend = 0;
+    const uint8_t* ip = data;
+    MBlk I{};
+    bool ilive = false, ihd = false;
     auto inext = [&]() {
       ilive = irest != 0;
       if (ilive) {
-        const MBlk m = mblk_lane(base, off, L, __builtin_ctzll(irest));
+        I = mblk_lane(data, off, pk, bsb0, __builtin_ctzll(irest));
         irest &= irest - 1;
-        is = 0;
-        isteps = m.steps;
-        isb0 = m.sb0;
-        ip = data + m.off + m.sb0;   // before the block start for a head step: those lanes are redirected
-        ihead = data + m.off + m.a0;
+        irem = I.steps;
+        ip = I.p + I.sb0;   // before the block start: the first step's leading lanes are redirected
+        ihd = true;
       }
     };
     auto issue = [&]() {
       const uint8_t* p = ip + lane16;
-      if (is == 0) {   // the block's first step: chunks wholly before the block (zeroed on read)
+      if (ihd) {   // the block's first step: chunks wholly before the block (zeroed on read)
         asm volatile("");   // a branch, not a select in every step
-        if (isb0 + lane16 + 16 <= 0) p = ihead;
+        if (I.sb0 + lane16 + 16 <= 0) p = I.p + I.a0;
+        ihd = false;
       }
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)&ring[islot].c[0], 16, 0, MTBLX_CRC_DMA_AUX);
-      islot = islot + 1 == (uint32_t)kRing ? 0u : islot + 1;
+#if MTBLX_CRC_ABL != 2
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(uintptr_t)(ring_base + ioff), 16, 0, MTBLX_CRC_DMA_AUX);
+#else
+      (void)p;
+#endif
+      ioff = (ioff + (uint32_t)kMStep) & kRingMask;
       ip += kMStep;
-      if (++is == isteps) inext();
+      if (--irem == 0) inext();
     };
     inext();
     while (ilive && pend < (uint32_t)(kRing - 1)) {
@@ -440,16 +452,16 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
     }
 
     uint64_t crest = em;
-    uint32_t cslot = 0;
+    uint32_t coff = 0;
+    v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;   // zero between super-windows
     while (crest) {
       const int cj = __builtin_ctzll(crest);
       crest &= crest - 1;
-      const MBlk Cb = mblk_lane(base, off, L, cj);
+      const MBlk Cb = mblk_lane(data, off, pk, bsb0, cj);
       uint32_t s = Cb.steps - 1;   // the step's window numbering: steps from the block's end
       int32_t sbc = Cb.sb0;        // block position of the step's chunk 0, while < 4
-      uint32_t acc = 0;
+      uint32_t acc = 0, lo = 0, hi = 0;
       bool first_sw = true;
-      v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
       for (;;) {
         if (ilive) {   // steady state: kRing - 1 steps stay in flight behind this one
           issue();
@@ -460,22 +472,21 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
         }
         const uint32_t t = s & (uint32_t)(kMSup - 1);
         v4i a2lo, a2hi;
-        v4u x = ring_read(ring + cslot, kx, a2l + 2 * t * 64, a2lo, a2hi);
-        cslot = cslot + 1 == (uint32_t)kRing ? 0u : cslot + 1;
+        v4u x = ring_read(ring_lane + coff, a2_lane + t * 2048u, a2lo, a2hi);
+        coff = (coff + (uint32_t)kMStep) & kRingMask;
         if (sbc < 4) {   // the block's first bytes (sbc > -1024)
           x = head_chunk(x, sbc + 16 * (int)kx);
           sbc += kMStep;
         }
-        if (s == 0 && Cb.t != 0) {   // the pad after the block's end: lane (g 3, n 0) holds chunk 63
-          asm volatile("");          // a branch, not a select in every step
-          if (lane == 48) x = tail_chunk(x, Cb.t);
+        if (s == 0) {   // the pad after the block's end: lane (g 3, n 0) holds chunk 63
+          asm volatile("");   // a branch, not a select in every step
+          if (Cb.t != 0 && lane == 48) x = tail_chunk(x, Cb.t);
         }
 #if MTBLX_CRC_ABL == 1
         acc ^= x.x ^ x.y ^ x.z ^ x.w;
-        (void)t;
-        if (s == 0) break;
-        --s;
-        continue;
+        lo = acc & 15u;
+        (void)a2lo;
+        (void)a2hi;
 #else
         const uint32_t w[kMKs] = {x.x, x.y, x.z, x.w};
         v4f c1a = {0.f, 0.f, 0.f, 0.f}, c1b = c1a;
@@ -490,29 +501,29 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
         const v4i b2 = {pk16(c1a.x, c1a.y), pk16(c1a.z, c1a.w), pk16(c1b.x, c1b.y), pk16(c1b.z, c1b.w)};
         c2a = mfma_f16(a2lo, b2, c2a);
         c2b = mfma_f16(a2hi, b2, c2b);
-        if (t != 0) {
-          --s;
-          continue;
+        if (t == 0) {
+          // super-window done: the parities of the column's raw CRC bits 4g + i (lo) and
+          // 16 + 4g + i (hi); with more than one super-window, Horner-combined as a full word with
+          // the super-windows before it (nearer the block start)
+          asm volatile("");
+          lo = par_nib(c2a);
+          hi = par_nib(c2b);
+          c2a = v4f{0.f, 0.f, 0.f, 0.f};
+          c2b = c2a;
+          if (Cb.steps > (uint32_t)kMSup) {
+            const uint32_t dv = (lo << (4 * g)) | (hi << (16 + 4 * g));
+            acc = first_sw ? dv : mul_nib(acc, sInv[0]) ^ dv;
+            first_sw = false;
+          }
         }
-        // super-window done: the column's raw CRC bits 4g + i and 16 + 4g + i, Horner-combined
-        // with the super-windows before it (nearer the block start)
-        const uint32_t sh = 4u * (uint32_t)g;
-        uint32_t dv = (par(c2a.x) | (par(c2a.y) << 1) | (par(c2a.z) << 2) | (par(c2a.w) << 3)) << sh;
-        dv |= (par(c2b.x) | (par(c2b.y) << 1) | (par(c2b.z) << 2) | (par(c2b.w) << 3)) << (sh + 16);
-        acc = first_sw ? dv : mul_nib(acc, sInv[0]) ^ dv;
-        first_sw = false;
-        c2a = v4f{0.f, 0.f, 0.f, 0.f};
-        c2b = c2a;
+#endif
         if (s == 0) break;
         --s;
-#endif
       }
-      // block done: column shift, XOR over all 64 lanes, pad removal.  With one super-window acc
-      // holds only the lane's own 8 bits of its column -- nibbles g and 4 + g -- so the column
+      // block done: column shift, XOR over all 64 lanes, pad removal.  With one super-window the
+      // lane holds only its own 8 bits of the column -- nibbles g and 4 + g -- so the column
       // shift takes 2 lookups; after a Horner step it is a full word.
-      uint32_t c = Cb.steps <= (uint32_t)kMSup
-                       ? sCol[n][g][(acc >> (4 * g)) & 15u] ^ sCol[n][4 + g][(acc >> (16 + 4 * g)) & 15u]
-                       : mul_nib(acc, sCol[n]);
+      uint32_t c = Cb.steps <= (uint32_t)kMSup ? sCol[n][g][lo] ^ sCol[n][4 + g][hi] : mul_nib(acc, sCol[n]);
       c = row_xor(c);                                          // over the 16 columns of a row
       uint32_t C = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 16) ^
                    (uint32_t)__builtin_amdgcn_readlane((int)c, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
@@ -563,7 +574,7 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   // 0.102 vs 0.120 ms on cfg2 (profiles/r04/crc_mfma)
   const char* kv = getenv("MTBLX_CRC_KERNEL");
   if (!kv || kv[0] != 'l') {
-    static int mgrid = 0;   // persistent: one 16-wave workgroup (144.5 KiB LDS) per CU
+    static int mgrid = 0;   // persistent: one 16-wave workgroup (160 KiB LDS) per CU
     if (!mgrid) {
       int dev = 0, ncu = 0;
       (void)hipGetDevice(&dev);

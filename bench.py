@@ -864,7 +864,7 @@ def main():
         hv = out.totals_host()
         if hv != (nrec, kbytes, vbytes, 0) or int(vbad.sum().item()) != 0:
             raise RuntimeError(f"fused verify decode mismatch: {hv}")
-        # the default mtblx_decode_blocks_verify: the decode, then k_crc32c_blocks, one stream
+        # the default mtblx_decode_blocks_verify: the decode, then the CRC kernel, one stream
         vbad.zero_()
         torch.cuda.synchronize()
         _preload(lambda: codec.decode_verify_into(batch, out, ws, None, vbad, True, stream, fused=False), stream,
@@ -877,10 +877,11 @@ def main():
         hv = out.totals_host()
         if hv != (nrec, kbytes, vbytes, 0) or int(vbad.sum().item()) != 0:
             raise RuntimeError(f"decode+verify mismatch: {hv}")
-        crc_info = {"kernel": "k_crc32c_blocks", "ms": round(crc_ms, 4),
+        ck = "k_crc32c_blocks" if os.environ.get("MTBLX_CRC_KERNEL", "").startswith("l") else "k_crc32c_mfma"
+        crc_info = {"kernel": ck, "ms": round(crc_ms, 4),
                     "GiB_per_s": round(block_bytes / (crc_ms * 1e-3) / 2**30, 1),
                     "bad_blocks": int(bad.sum().item()),
-                    "decode_blocks_verify": {"kernels": "k_decode_pipe<PipeSmall> + k_crc32c_blocks", "ms": round(d_ms, 4),
+                    "decode_blocks_verify": {"kernels": "k_decode_pipe<PipeSmall> + " + ck, "ms": round(d_ms, 4),
                                              "GiB_per_s": round(block_bytes / (d_ms * 1e-3) / 2**30, 1)},
                     "fused_decode_verify": {"kernel": "k_decode_pipe<PipeSmallV>", "ms": round(v_ms, 4),
                                             "GiB_per_s": round(block_bytes / (v_ms * 1e-3) / 2**30, 1),

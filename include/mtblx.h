@@ -135,14 +135,18 @@ int mtblx_decode_counted(const mtblx_block_batch* in, const mtblx_decoded* out, 
  * With framed != 0 the batch addresses contents inside an mtbl file, whose framing stores
  * the checksum as the u32 LE right before each content (varint len | crc32c | content,
  * src/writer.rs:213-225): bad[b] = 1 where it differs from crc[b] -- exactly where the
- * reference's assert_eq panics -- else 0.  crc or bad may be NULL (not both). */
+ * reference's assert_eq panics -- else 0.  crc or bad may be NULL (not both).
+ * Kernel: k_crc32c_mfma (CRC-32C as fp4 / f16 matrix-core GEMMs over 1 KiB steps, one
+ * persistent 16-wave workgroup per CU); MTBLX_CRC_KERNEL=lanes in the environment selects the
+ * VALU table kernel k_crc32c_blocks (A/B only).  Same checksums either way. */
 int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, uint8_t* bad, int framed, void* stream);
 
 /* mtblx_decode_blocks + the checksum of every block (f1): crc / crc_bad as
  * mtblx_crc32c_blocks (either may be NULL, not both; `framed` bit 0 as there).  The records
  * are decoded regardless -- the caller applies Reader::block's order (checksum assert before
  * Block::init, src/reader.rs:159-172).
- * Default: the decode launch, then k_crc32c_blocks on the same stream.  With
+ * Default: the decode launch, then the matrix-core CRC kernel (k_crc32c_mfma, as
+ * mtblx_crc32c_blocks) on the same stream.  With
  * MTBLX_VERIFY_FUSED in `framed` the checksum is computed inside the decode launch from the
  * tiles already staged in LDS (by the look-back and loader waves); blocks above ~64 KiB
  * still take a second launch.  On gfx950 the fused form measures slower (DESIGN.md §4:

@@ -82,7 +82,7 @@ extern "C" int mtblx_decode_blocks_verify(const mtblx_block_batch* in, const mtb
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (framed & MTBLX_VERIFY_FUSED)   // one launch: the CRC from the LDS-staged tiles
     return mtblx_impl_run(in, out, ws, wsb, 1, s, 1, crc, crc_bad, framed & 1);
-  // default: the decode, then k_crc32c_blocks on the same stream (faster on gfx950)
+  // default: the decode, then the CRC-32C kernel (k_crc32c_mfma) on the same stream
   const int rc = mtblx_impl_run(in, out, ws, wsb, 1, s, 0, nullptr, nullptr, 0);
   if (rc != MTBLX_OK) return rc;
   return mtblx_crc32c_blocks(in, crc, crc_bad, framed & 1, stream);

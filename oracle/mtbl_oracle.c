@@ -332,8 +332,8 @@ static int obatch_cb(void* c, const uint8_t* k, uint64_t kl, const uint8_t* v, u
     x->overflow = 1;
     return 0;
   }
-  memcpy(x->keys + x->key_base + x->kb - kl, k, kl);
-  memcpy(x->vals + x->val_base + x->vb - vl, v, vl);
+  if (kl) memcpy(x->keys + x->key_base + x->kb - kl, k, kl);   /* k may be NULL when kl == 0 */
+  if (vl) memcpy(x->vals + x->val_base + x->vb - vl, v, vl);
   x->key_end[r] = (uint32_t)x->kb;
   x->val_end[r] = (uint32_t)x->vb;
   return 0;

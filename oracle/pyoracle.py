@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libmtbl_oracle.so")
+# MTBL_ORACLE_LIB: the sanitizer build (oxidized-mtbl_amd/Makefile asan-test)
+_LIB_PATH = os.environ.get("MTBL_ORACLE_LIB") or os.path.join(_HERE, "_build", "libmtbl_oracle.so")
 
 ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW = range(6)
 END_NONE, END_ERR_OPEN, END_ERR_NEXT, END_PANIC, END_LOOP = range(5)

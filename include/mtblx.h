@@ -42,7 +42,10 @@ extern "C" {
 #define MTBLX_E_NODEV (-3)    /* no gfx950 device visible                               */
 #define MTBLX_E_FORMAT (-4)   /* host-side file/format error (reader API)               */
 #define MTBLX_E_TIMEOUT (-5)  /* a decode launch reported a look-back timeout (totals[3] bit 1) twice:
-                                 its outputs were discarded (synchronous entry points only)  */
+                                 its outputs were discarded (synchronous entry points only).
+                                 Worst case: a waiting wave gives up after 20 s (look-back) or
+                                 21 s (hand-off inside a workgroup); with the one retry a stuck
+                                 launch returns this after about 42-45 s                      */
 #define MTBLX_E_IO (-6)       /* the writer's compressor returned Err (Writer::insert / into_inner's
                                  io::Error: Lz4 / Lz4hc "unsupported", src/compression.rs:70-81;
                                  a codec failure); nothing was written, but the records of the

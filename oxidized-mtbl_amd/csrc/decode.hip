@@ -22,7 +22,7 @@
 // Ablations (outputs incomplete by construction) and the spilling variant build only through the
 // Makefile's diagnostic targets, which define MTBLX_DIAG; the product build rejects them.
 #if (defined(MTBLX_ABL_NOKEY) || defined(MTBLX_ABL_NOVAL) || defined(MTBLX_ABL_NOVSTORE) || \
-     defined(MTBLX_ABL_CRC) || defined(MTBLX_SPILL)) && !defined(MTBLX_DIAG)
+     defined(MTBLX_ABL_CRC) || defined(MTBLX_SPILL) || defined(MTBLX_CALL_PROBE)) && !defined(MTBLX_DIAG)
 #error "ablation / spill knobs are diagnostic: build them through a Makefile diagnostic target (-DMTBLX_DIAG)"
 #endif
 
@@ -1947,16 +1947,18 @@ __device__ __forceinline__ void copy_emit(const PipeBuf<P>& B, const TileArgs& a
 }
 
 // Wait for a workgroup-local LDS counter.  Bounded: giving up means this launch's outputs are
-// not trustworthy (look-back / hand-off timeout, totals[3] bit 1), never a hang.  Hand-offs
-// inside a workgroup wait 4x as long as a look-back on other workgroups (kHandoffMul), so a
-// look-back that gives up (and still releases its copy waves) never cascades into a hand-off
-// that gives up with the LDS state unwritten.
-constexpr uint64_t kHandoffMul = 4;
+// not trustworthy (look-back / hand-off timeout, totals[3] bit 1), never a hang.  A hand-off
+// inside a workgroup waits one look-back bound plus a margin (handoff_ticks), so a look-back that
+// gives up (and still releases its copy waves, microseconds later) never cascades into a hand-off
+// that gives up with the LDS state unwritten; with the default 20 s bound a stuck launch reports
+// after ~21 s (the earlier 4x multiple made that 80 s).
+constexpr uint64_t kHandoffMargin = 100000000ull;   // 1 s of s_memrealtime (100 MHz)
+__device__ __forceinline__ uint64_t handoff_ticks(const TileArgs& a) { return a.wait_ticks + kHandoffMargin; }
 __device__ __forceinline__ void wait_flag(const TileArgs& a, const uint32_t* flag, uint32_t want) {
   WaitBound wb;
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
     __builtin_amdgcn_s_sleep(1);
-    if (wb.expired(kHandoffMul * a.wait_ticks)) { ws_timeout(a); break; }
+    if (wb.expired(handoff_ticks(a))) { ws_timeout(a); break; }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
@@ -2111,6 +2113,17 @@ template <class P>
 __device__ MTBLX_PIPE_CRC_INLINE void pipe_crc_copy(const PipeBuf<P>& B, const TileArgs& a, PipeLds<P>& S, uint32_t cw,
                                                     int lane, uint32_t par) {
   if constexpr ((MTBLX_ABL_CRC & 4) != 0) return;
+#ifdef MTBLX_CALL_PROBE   // diagnostic (the outlined-call fault): the callee's arguments
+  if (lane == 0 && cw == 0 && blockIdx.x < 2)
+    printf("probe wg %u par %u B %p a %p data %p len %lu blk_off %p nblk %u crc %p bad %p "
+           "framed %d nb %u b0 %u boff0 %u blen0 %u S %p crcT %p\n",
+           blockIdx.x, par, (const void*)&B, (const void*)&a, (const void*)a.data, (unsigned long)a.data_len,
+           (const void*)a.blk_off, a.nblk, (void*)a.crc, (void*)a.crc_bad, a.crc_framed, B.nb, B.b0, B.boff[0],
+           B.blen[0], (void*)&S, (void*)&S.crcT[0][0]);
+#if MTBLX_CALL_PROBE == 1
+  return;   // arguments only: the body (and the fault) skipped
+#endif
+#endif
   constexpr uint32_t NC = (uint32_t)P::NCOPY;
   constexpr int kIn = MTBLX_CRC_INFLIGHT;
   const uint32_t nb = B.nb;
@@ -2380,7 +2393,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
             WaitBound wb;
             while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
               __builtin_amdgcn_s_sleep(1);
-              if (wb.expired(kHandoffMul * a.wait_ticks)) { ws_timeout(a); break; }
+              if (wb.expired(handoff_ticks(a))) { ws_timeout(a); break; }
             }
             pipe_lookback_issue(a, tc + G, G, lbv, lane);
             pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kCopyW);
@@ -2445,7 +2458,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
           WaitBound wb;
           while (__hip_atomic_load(&S.pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k1 + 1) {
             __builtin_amdgcn_s_sleep(1);
-            if (wb.expired(kHandoffMul * a.wait_ticks)) { ws_timeout(a); break; }
+            if (wb.expired(handoff_ticks(a))) { ws_timeout(a); break; }
           }
           pipe_lookback_issue(a, tc + G, G, lbv, lane);
           pipe_lookback_poll(a, tc + G, G, lbv, lane, &S.cdone, (uint32_t)(it + 1) * kCopyW);

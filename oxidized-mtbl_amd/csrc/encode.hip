@@ -27,9 +27,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
 #include <vector>
 
 #include "crc_dev.h"
+#include "crc_mfma_dev.h"
 #include "mtblx.h"
 
 namespace mtblx_enc {
@@ -214,6 +216,33 @@ struct X8Tab {
 };
 static __constant__ X8Tab kX8 = X8Tab();
 
+// The block CRC on the matrix cores (crc_mfma.h): the operands of k_crc32c_mfma, plus the shift of
+// super-window S (8 KiB steps counted from the block's aligned end) x^(8·8192·S) as nibble tables,
+// S <= 8 for blocks assembled in LDS (kLdsBlock bytes)
+#ifndef MTBLX_ENC_CRC_MFMA
+#define MTBLX_ENC_CRC_MFMA 1
+#endif
+#ifndef MTBLX_ENC_CRC_UNROLL
+#define MTBLX_ENC_CRC_UNROLL 2
+#endif
+constexpr int kEncSup = (kLdsBlock + mtblx_crc::kMStep * mtblx_crc::kMSup - 1) / (mtblx_crc::kMStep * mtblx_crc::kMSup);
+struct EncSw {
+  uint32_t t[kEncSup][8][16];
+  constexpr EncSw() : t() {
+    uint32_t K = 0x80000000u;   // x^8, squared 13 times: x^(8·8192)
+    for (int k = 0; k < 8; ++k) K = (K & 1u) ? (K >> 1) ^ mtblx_crc::kPoly : K >> 1;
+    for (int q = 0; q < 13; ++q) K = mtblx_crc::multmodp(K, K);
+    uint32_t P = 0x80000000u;
+    for (int S = 0; S < kEncSup; ++S) {
+      mtblx_crc::MulTabs::fill(t[S], P);
+      P = mtblx_crc::multmodp(K, P);
+    }
+  }
+};
+static_assert(mtblx_crc::kMStep * mtblx_crc::kMSup == 8192, "EncSw: 8 KiB super-windows");
+static __constant__ mtblx_crc::MfmaTabs kEncMfma = mtblx_crc::MfmaTabs();
+static __constant__ EncSw kEncSw = EncSw();
+
 struct EncArgs {
   Recs R;
   const uint64_t* blk_rec;   // [nblk + 1]
@@ -230,8 +259,24 @@ struct EncArgs {
   uint64_t* lbw;             // [nblk] look-back words
 };
 
+// Entry pieces past the first 64 bytes of a key suffix / value (Zipf keys up to 256 B): one lane
+// per entry would leave its wave waiting on the longest key, so they go to a workgroup list that
+// every lane then copies from (kOvfCap pieces; a lane copies any that do not fit itself)
+#ifndef MTBLX_ENC_OVF   // 0: every piece on the entry's lane (put_entry)
+#define MTBLX_ENC_OVF 0
+#endif
+constexpr uint32_t kOvfCap = MTBLX_ENC_OVF;
+constexpr uint64_t kPiece = 64;
+struct EncPiece {
+  uint32_t dst;    // block offset of the piece
+  uint32_t n;      // bytes (<= kPiece) | bit 31: a value piece (else key)
+  uint64_t src;    // offset in R.keys / R.vals
+};
+
 struct alignas(16) EncLds {
   uint8_t ob[kLdsBlock];
+  EncPiece ovf[kOvfCap > 0 ? kOvfCap : 1];
+  uint32_t novf;
   uint32_t T[4][256];        // slicing-by-4 CRC-32C tables
   uint16_t shc[kShCache];    // phase A's `shared` of the first entries (0xFFFF: recompute)
   uint64_t red[kWaves];
@@ -352,6 +397,73 @@ __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
   return r ^ 0xFFFFFFFFu;
 }
 
+// CRC-32C of the block assembled at S.ob[0..L) (4 <= L <= kLdsBlock; the caller zeroes the pad
+// S.ob[L .. L + t), t = the bytes to a 16-byte boundary) on the matrix cores: windows counted from
+// the padded end as k_crc32c_mfma (crc.hip, crc_mfma.h); wave w takes the super-windows w,
+// w + kWaves, ... (8 steps of 1 KiB each, straight from LDS: every step's chunks are 16-byte
+// aligned, so the block start needs no partial masks) and shifts their raw CRC by x^(8·8192·S)
+// (crc_mfma_part, no barrier: wave 0 runs the look-back first); after a barrier the waves'
+// parts are XOR-combined and the pad is removed by x^(-8t) (crc_mfma_final).  The operands come
+// from constant memory.
+__device__ void crc_mfma_part(EncLds& S, uint32_t L) {
+  using namespace mtblx_crc;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, n = lane & 15;
+  const uint32_t t = (16u - (L & 15u)) & 15u, Lp = L + t;
+  const uint32_t steps = (Lp + kMStep - 1) / kMStep, nsup = (steps + kMSup - 1) / kMSup;
+  const int32_t kx16 = 16 * (60 - 4 * n + g);   // the lane's chunk of a step
+  uint32_t C = 0;
+  if ((uint32_t)w < nsup) {
+    v4i A[kMKs][2];
+#pragma unroll
+    for (int k = 0; k < kMKs; ++k) {
+      A[k][0] = reinterpret_cast<const v4i*>(&kEncMfma.a[k][0][0][0])[lane];
+      A[k][1] = reinterpret_cast<const v4i*>(&kEncMfma.a[k][1][0][0])[lane];
+    }
+    for (uint32_t sw = (uint32_t)w; sw < nsup; sw += kWaves) {
+      v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
+#pragma unroll MTBLX_ENC_CRC_UNROLL
+      for (int tt = kMSup - 1; tt >= 0; --tt) {   // from the super-window's start
+        const uint32_t s = sw * kMSup + (uint32_t)tt;
+        if (s < steps) {
+          const int32_t pos = (int32_t)Lp - (int32_t)(kMStep * (s + 1)) + kx16;   // a multiple of 16
+          v4a x = {0u, 0u, 0u, 0u};
+          if (pos >= 0) x = *reinterpret_cast<const v4a*>(S.ob + pos);
+          if (pos == 0) x.x ^= 0xFFFFFFFFu;   // the init, folded into bytes 0..3
+          const v4i a2lo = reinterpret_cast<const v4i*>(&kEncMfma.a2[tt][0][0][0])[lane];
+          const v4i a2hi = reinterpret_cast<const v4i*>(&kEncMfma.a2[tt][1][0][0])[lane];
+          mfma_step(A, v4u{x.x, x.y, x.z, x.w}, a2lo, a2hi, c2a, c2b);
+        }
+      }
+      // the column's parities (CRC bits 4g + i, 16 + 4g + i), column shift, XOR over the columns
+      uint32_t c = kEncMfma.col[n][g][par_nib(c2a)] ^ kEncMfma.col[n][4 + g][par_nib(c2b)];
+      c = row_xor(c);
+      uint32_t Cs = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 16) ^
+                    (uint32_t)__builtin_amdgcn_readlane((int)c, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
+      if (sw) {   // x^(8·8192·sw): nibble j looked up by lane j (j < 8) of each row
+        const uint32_t j = (uint32_t)lane & 15u;
+        const uint32_t v = j < 8u ? kEncSw.t[sw][j][(Cs >> (4 * j)) & 15u] : 0u;
+        Cs = (uint32_t)__builtin_amdgcn_readlane((int)row_xor(v), 0);
+      }
+      C ^= Cs;
+    }
+  }
+  if (lane == 0) S.redf[w] = C;
+}
+// after a barrier that follows every wave's crc_mfma_part
+__device__ uint32_t crc_mfma_final(const EncLds& S, uint32_t L) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t t = (16u - (L & 15u)) & 15u;
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < kWaves; ++k) r ^= S.redf[k];
+  if (t) {   // x^(-8t): the pad after the block's end removed
+    const uint32_t j = (uint32_t)lane & 15u;
+    const uint32_t v = j < 8u ? kEncMfma.inv[t][j][(r >> (4 * j)) & 15u] : 0u;
+    r = (uint32_t)__builtin_amdgcn_readlane((int)mtblx_crc::row_xor(v), 0);
+  }
+  return r ^ 0xFFFFFFFFu;
+}
+
 // entry i of the block starting at record r0: fields and encoded size
 struct Ent {
   uint64_t k0, kl, v0, vl, sh;
@@ -403,6 +515,45 @@ __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent
   const uint32_t n = l0 + l1 + l2;
   copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys);
   copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl, R.vals);
+}
+// the same entry into the LDS block at block offset eo: the header and the first kPiece bytes of
+// the key suffix and of the value here (straight-line, as put_entry), their further pieces to the
+// workgroup list S.ovf; what does not fit in the list is copied here (one loop over the two
+// parts, so the rare path adds a single copy_bytes body)
+template <class L>
+__device__ __forceinline__ void put_entry_lds(L& S, uint64_t eo, const Recs& R, const Ent& e) {
+  uint8_t* dst = S.ob + eo;
+  const uint64_t ks = e.kl - e.sh, vl = e.vl;
+  const uint32_t l0 = vlen32((uint32_t)e.sh), l1 = vlen32((uint32_t)ks), l2 = vlen32((uint32_t)vl);
+  put_varint(dst, (uint32_t)e.sh, l0);
+  put_varint(dst + l0, (uint32_t)ks, l1);
+  put_varint(dst + l0 + l1, (uint32_t)vl, l2);
+  const uint32_t hk = l0 + l1 + l2;
+  const uint64_t ksrc = e.k0 + e.sh;
+  copy_bytes(dst + hk, R.keys + ksrc, ks < kPiece ? ks : kPiece, R.keys);
+  copy_bytes(dst + hk + ks, R.vals + e.v0, vl < kPiece ? vl : kPiece, R.vals);
+  const uint32_t npk = ks > kPiece ? (uint32_t)((ks - 1) / kPiece) : 0u;   // key pieces after the first
+  const uint32_t npv = vl > kPiece ? (uint32_t)((vl - 1) / kPiece) : 0u;
+  if (npk + npv == 0u) return;
+  const uint32_t slot = atomicAdd(&S.novf, npk + npv);
+  const uint32_t nin = slot >= kOvfCap ? 0u : (kOvfCap - slot < npk + npv ? kOvfCap - slot : npk + npv);
+  for (uint32_t q = 0; q < nin; ++q) {   // pieces q < npk: key piece q + 1; else value piece q - npk + 1
+    const bool isv = q >= npk;
+    const uint64_t po = kPiece * (isv ? q - npk + 1u : q + 1u);
+    const uint64_t len = isv ? vl : ks;
+    const uint32_t nb = (uint32_t)(len - po < kPiece ? len - po : kPiece);
+    S.ovf[slot + q] = EncPiece{(uint32_t)(eo + hk + (isv ? ks : 0) + po), nb | (isv ? 0x80000000u : 0u),
+                               (isv ? e.v0 : ksrc) + po};
+  }
+  if (nin == npk + npv) return;
+  for (uint32_t part = 0; part < 2u; ++part) {   // the list is full: the remaining pieces here
+    const bool isv = part == 1u;
+    const uint32_t np = isv ? npv : npk, done = isv ? (nin > npk ? nin - npk : 0u) : (nin < npk ? nin : npk);
+    if (done >= np) continue;
+    const uint64_t po = kPiece * (done + 1u), len = isv ? vl : ks;
+    const uint8_t* base = isv ? R.vals : R.keys;
+    copy_bytes(dst + hk + (isv ? ks : 0) + po, base + (isv ? e.v0 : ksrc) + po, len - po, base);
+  }
 }
 
 __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
@@ -492,7 +643,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 
   // ---- phase B (LDS path): assemble the block ----
   const uint64_t R = entries;   // restart array offset
-  auto assemble = [&](uint8_t* dst) {
+  auto assemble = [&](uint8_t* dst, auto lds_tag) {
+    constexpr bool lds = decltype(lds_tag)::value;
+    if (tid == 0) S.novf = 0;   // ordered before the pushes by the scan's barriers
     uint64_t carry = 0;
     for (uint64_t base = 0; base < n; base += kThreads) {
       const uint64_t i = base + tid;
@@ -505,21 +658,39 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       uint64_t tot = 0;
       const uint64_t eo = carry + wg_excl_scan(S, sz, tot);
       if (i < n) {
-        put_entry(dst + eo, a.R, e);
+        if constexpr (lds && kOvfCap > 0) put_entry_lds(S, eo, a.R, e);
+        else put_entry(dst + eo, a.R, e);
         if (iv > 0 && i % iv == 0) put32(dst + R + 4 * (i / iv), (uint32_t)eo);
       }
       carry += tot;
+    }
+    if constexpr (lds && kOvfCap > 0) {   // the listed pieces, over all lanes
+      __syncthreads();
+      const uint32_t nov = S.novf < kOvfCap ? S.novf : kOvfCap;
+      for (uint32_t k = (uint32_t)tid; k < nov; k += kThreads) {
+        const EncPiece pc = S.ovf[k];
+        const bool isv = (pc.n >> 31) != 0u;
+        copy_bytes(S.ob + pc.dst, (isv ? a.R.vals : a.R.keys) + pc.src, pc.n & 0x7FFFFFFFu, isv ? a.R.vals : a.R.keys);
+      }
     }
     if (tid == 0) {
       if (n == 0 || iv == 0) put32(dst + R, 0u);      // restarts[0] = 0 (entry 0 writes it otherwise)
       if (iv == 0 && n > 0) put32(dst + R + 4, 0u);   // the push of entry 0 (buf.len() == 0)
       put32(dst + L - 4, (uint32_t)nrest);            // restart count
+      if constexpr (lds)                              // the CRC's pad to a 16-byte boundary
+        for (uint64_t z = L; z & 15u; ++z) S.ob[z] = 0;
     }
   };
-  if (in_lds) assemble(S.ob);
+  if (in_lds) assemble(S.ob, std::true_type{});
   ESTAMP(4);   // assembly in LDS
 
-  // ---- look-back: this block's offset in the output ----
+  // ---- look-back: this block's offset in the output (wave 0), beside the block CRC (all waves,
+  // wave 0 after its look-back) ----
+  const bool crc_mfma = MTBLX_ENC_CRC_MFMA && a.framed && in_lds && L >= 4;
+  if (crc_mfma) {
+    __syncthreads();   // the assembled block (entries, restarts, count, pad) before its CRC
+    if (w != 0) crc_mfma_part(S, (uint32_t)L);
+  }
   if (w == 0) {
     bool to = false;
     const uint64_t excl = b == 0 ? 0 : lookback(a, b, lane, to);
@@ -528,6 +699,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       S.sh_u64[0] = excl;
       if (to) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 1), 2ull);
     }
+    if (crc_mfma) crc_mfma_part(S, (uint32_t)L);
   }
   __syncthreads();
   ESTAMP(5);   // look-back
@@ -538,13 +710,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     uint8_t* dst = a.out + coff;
     const uint8_t* src = S.ob;
     if (!in_lds) {   // large block: assemble in place in HBM
-      assemble(dst);
+      assemble(dst, std::false_type{});
       __threadfence_block();
       __syncthreads();
       src = dst;
     }
     if (a.framed) {
-      const uint32_t crc = wg_crc32c(S, src, L);
+      const uint32_t crc = crc_mfma ? crc_mfma_final(S, (uint32_t)L) : wg_crc32c(S, src, L);
       ESTAMP(6);   // CRC-32C
       if (tid == 0) {
         uint32_t hl;   // varint64(L) | crc32c (write_block, src/writer.rs:203-237)

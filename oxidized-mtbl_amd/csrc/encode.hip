@@ -259,24 +259,8 @@ struct EncArgs {
   uint64_t* lbw;             // [nblk] look-back words
 };
 
-// Entry pieces past the first 64 bytes of a key suffix / value (Zipf keys up to 256 B): one lane
-// per entry would leave its wave waiting on the longest key, so they go to a workgroup list that
-// every lane then copies from (kOvfCap pieces; a lane copies any that do not fit itself)
-#ifndef MTBLX_ENC_OVF   // 0: every piece on the entry's lane (put_entry)
-#define MTBLX_ENC_OVF 0
-#endif
-constexpr uint32_t kOvfCap = MTBLX_ENC_OVF;
-constexpr uint64_t kPiece = 64;
-struct EncPiece {
-  uint32_t dst;    // block offset of the piece
-  uint32_t n;      // bytes (<= kPiece) | bit 31: a value piece (else key)
-  uint64_t src;    // offset in R.keys / R.vals
-};
-
 struct alignas(16) EncLds {
   uint8_t ob[kLdsBlock];
-  EncPiece ovf[kOvfCap > 0 ? kOvfCap : 1];
-  uint32_t novf;
   uint32_t T[4][256];        // slicing-by-4 CRC-32C tables
   uint16_t shc[kShCache];    // phase A's `shared` of the first entries (0xFFFF: recompute)
   uint64_t red[kWaves];
@@ -516,46 +500,6 @@ __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent
   copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys);
   copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl, R.vals);
 }
-// the same entry into the LDS block at block offset eo: the header and the first kPiece bytes of
-// the key suffix and of the value here (straight-line, as put_entry), their further pieces to the
-// workgroup list S.ovf; what does not fit in the list is copied here (one loop over the two
-// parts, so the rare path adds a single copy_bytes body)
-template <class L>
-__device__ __forceinline__ void put_entry_lds(L& S, uint64_t eo, const Recs& R, const Ent& e) {
-  uint8_t* dst = S.ob + eo;
-  const uint64_t ks = e.kl - e.sh, vl = e.vl;
-  const uint32_t l0 = vlen32((uint32_t)e.sh), l1 = vlen32((uint32_t)ks), l2 = vlen32((uint32_t)vl);
-  put_varint(dst, (uint32_t)e.sh, l0);
-  put_varint(dst + l0, (uint32_t)ks, l1);
-  put_varint(dst + l0 + l1, (uint32_t)vl, l2);
-  const uint32_t hk = l0 + l1 + l2;
-  const uint64_t ksrc = e.k0 + e.sh;
-  copy_bytes(dst + hk, R.keys + ksrc, ks < kPiece ? ks : kPiece, R.keys);
-  copy_bytes(dst + hk + ks, R.vals + e.v0, vl < kPiece ? vl : kPiece, R.vals);
-  const uint32_t npk = ks > kPiece ? (uint32_t)((ks - 1) / kPiece) : 0u;   // key pieces after the first
-  const uint32_t npv = vl > kPiece ? (uint32_t)((vl - 1) / kPiece) : 0u;
-  if (npk + npv == 0u) return;
-  const uint32_t slot = atomicAdd(&S.novf, npk + npv);
-  const uint32_t nin = slot >= kOvfCap ? 0u : (kOvfCap - slot < npk + npv ? kOvfCap - slot : npk + npv);
-  for (uint32_t q = 0; q < nin; ++q) {   // pieces q < npk: key piece q + 1; else value piece q - npk + 1
-    const bool isv = q >= npk;
-    const uint64_t po = kPiece * (isv ? q - npk + 1u : q + 1u);
-    const uint64_t len = isv ? vl : ks;
-    const uint32_t nb = (uint32_t)(len - po < kPiece ? len - po : kPiece);
-    S.ovf[slot + q] = EncPiece{(uint32_t)(eo + hk + (isv ? ks : 0) + po), nb | (isv ? 0x80000000u : 0u),
-                               (isv ? e.v0 : ksrc) + po};
-  }
-  if (nin == npk + npv) return;
-  for (uint32_t part = 0; part < 2u; ++part) {   // the list is full: the remaining pieces here
-    const bool isv = part == 1u;
-    const uint32_t np = isv ? npv : npk, done = isv ? (nin > npk ? nin - npk : 0u) : (nin < npk ? nin : npk);
-    if (done >= np) continue;
-    const uint64_t po = kPiece * (done + 1u), len = isv ? vl : ks;
-    const uint8_t* base = isv ? R.vals : R.keys;
-    copy_bytes(dst + hk + (isv ? ks : 0) + po, base + (isv ? e.v0 : ksrc) + po, len - po, base);
-  }
-}
-
 __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
   uint64_t excl = 0;
   int64_t j = (int64_t)b - 1;
@@ -645,7 +589,6 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   const uint64_t R = entries;   // restart array offset
   auto assemble = [&](uint8_t* dst, auto lds_tag) {
     constexpr bool lds = decltype(lds_tag)::value;
-    if (tid == 0) S.novf = 0;   // ordered before the pushes by the scan's barriers
     uint64_t carry = 0;
     for (uint64_t base = 0; base < n; base += kThreads) {
       const uint64_t i = base + tid;
@@ -658,20 +601,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       uint64_t tot = 0;
       const uint64_t eo = carry + wg_excl_scan(S, sz, tot);
       if (i < n) {
-        if constexpr (lds && kOvfCap > 0) put_entry_lds(S, eo, a.R, e);
-        else put_entry(dst + eo, a.R, e);
+        put_entry(dst + eo, a.R, e);
         if (iv > 0 && i % iv == 0) put32(dst + R + 4 * (i / iv), (uint32_t)eo);
       }
       carry += tot;
-    }
-    if constexpr (lds && kOvfCap > 0) {   // the listed pieces, over all lanes
-      __syncthreads();
-      const uint32_t nov = S.novf < kOvfCap ? S.novf : kOvfCap;
-      for (uint32_t k = (uint32_t)tid; k < nov; k += kThreads) {
-        const EncPiece pc = S.ovf[k];
-        const bool isv = (pc.n >> 31) != 0u;
-        copy_bytes(S.ob + pc.dst, (isv ? a.R.vals : a.R.keys) + pc.src, pc.n & 0x7FFFFFFFu, isv ? a.R.vals : a.R.keys);
-      }
     }
     if (tid == 0) {
       if (n == 0 || iv == 0) put32(dst + R, 0u);      // restarts[0] = 0 (entry 0 writes it otherwise)

@@ -191,7 +191,9 @@ def end_to_end(data, off, ln, nrec, kbytes, vbytes, reps, dist=None):
         pipe.unregister(data)
     # cfg5: the cfg2 records written with CompressionType::Snappy (same blocks once decompressed)
     nr_file = int(synth.cfg2_file.last_block_nrec.sum(dtype=np.uint64))
-    keys, vals, kl, vl = synth.cfg2_arrays(int(off.size * ((4096 - 64) // 79) * 1.02) + 64)
+    rk = dist.get_rank() if dist is not None else 0   # the rank's own shard records (synth.cfg2_shard)
+    keys, vals, kl, vl = synth.cfg2_arrays(int(off.size * ((4096 - 64) // 79) * 1.02) + 64, seed=synth.SEED_CFG2 + rk,
+                                           c0=rk << synth.SHARD_KEY_BITS)
     w = Writer(4096, 16, 1)
     n_in = nr_file
     w.insert_batch(keys[: n_in * kl], np.arange(1, n_in + 1, dtype=np.uint64) * np.uint64(kl), vals[: n_in * vl],
@@ -435,7 +437,7 @@ def maybe_launch(args, argv) -> int | None:
     if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
         return None
     nvis = torch.cuda.device_count()
-    if nvis < args.gpus:
+    if nvis < args.gpus and not args.share_gpu:
         log(f"--gpus {args.gpus}: only {nvis} GPU(s) visible")
         return 2
     import socket
@@ -459,6 +461,8 @@ def init_ranks(args, backend: str = "nccl"):
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--gpus {world}: only {torch.cuda.device_count()} GPU(s) visible")
         torch.cuda.set_device(local)
+    elif getattr(args, "share_gpu", False):
+        torch.cuda.set_device(0)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -726,6 +730,9 @@ def run_cfg4(args, dist, world, rank):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="diagnostic: the --gpus N ranks all on GPU 0 with gloo collectives -- exercises the "
+                         "multi-rank path (launch, shards, barriers, max-over-ranks) on a 1-GPU box; not scaling")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=100_000)
@@ -767,7 +774,9 @@ def main():
         os.environ["MTBLX_LIB"] = args.lib or os.path.join(ROOT, "oxidized-mtbl_amd", "mtblx", "libmtblx_stamps.so")
     elif args.lib:
         os.environ["MTBLX_LIB"] = args.lib
-    dist, world, rank, local = init_ranks(args)
+    dist, world, rank, local = init_ranks(args, backend="gloo" if args.share_gpu else "nccl")
+    if args.share_gpu and world > 1:   # each rank's look-back launches stay co-resident on its CUs
+        os.environ["MTBLX_PIPE_CUS"] = str(max(1, torch.cuda.get_device_properties(0).multi_processor_count // world))
 
     from mtblx import codec, synth
 
@@ -996,7 +1005,9 @@ def main():
                    "records_per_gpu": int(nrec), "key_bytes_per_gpu": int(kbytes), "value_bytes_per_gpu": int(vbytes),
                    "parallelism": f"block-sharded x{world}, no collective" + (
                        f" (rank-partitioned key space, synth.cfg2_shard; {total_bytes} block bytes over all ranks)"
-                       if world > 1 else "")},
+                       if world > 1 else "") + (
+                       f" -- DIAGNOSTIC: all {world} ranks on GPU 0, gloo collectives (rank path check, not scaling)"
+                       if args.share_gpu else "")},
         "kernels_ms": {f"{kernel} (HIP events around the timed region / steps)": round(k_decode_ms, 4)},
         "host_enqueue_ms_per_step": round(t_enq * 1e3 / args.steps, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -2574,13 +2574,18 @@ Plan make_plan(uint32_t nblk, uint32_t max_len) {
 
 
 
+// One workgroup per CU: every workgroup of a launch is resident, which the look-back between
+// workgroups needs.  MTBLX_PIPE_CUS caps it (diagnostic: several processes sharing one GPU, e.g.
+// bench.py --share-gpu, each keep their launches co-resident on their share of the CUs).
 int pipe_grid(uint32_t ntiles) {
   static int cached = 0;
   if (!cached) {
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    cached = std::max(1, std::min(ncu, kMaxLookbackLoads * kWave + 1));  // 1 workgroup per CU
+    const char* cap = getenv("MTBLX_PIPE_CUS");
+    if (cap && atoi(cap) > 0) ncu = std::min(ncu, atoi(cap));
+    cached = std::max(1, std::min(ncu, kMaxLookbackLoads * kWave + 1));
   }
   return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
 }

@@ -169,3 +169,22 @@ def test_bench_launch_and_world_checks(monkeypatch):
     monkeypatch.delenv("WORLD_SIZE")
     one = bench.parse_args([])
     assert one.gpus == 1 and bench.maybe_launch(one, []) is None
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_share_gpu():
+    """the driver's N > 1 path end to end on a real GPU: `bench.py --gpus 2` relaunches itself
+    through torch.distributed.run; with --share-gpu both ranks decode their shards on GPU 0 and
+    the collectives go over gloo -- the JSON line must report both ranks' shards and records"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-gpu", "--steps", "3",
+           "--warmup", "1", "--blocks", "20000", "--no-crc", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=root)
+    assert r.returncode == 0, "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[rank"))[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "x2" in d["config"]["parallelism"] and "DIAGNOSTIC" in d["config"]["parallelism"]

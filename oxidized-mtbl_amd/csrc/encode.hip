@@ -222,6 +222,9 @@ static __constant__ X8Tab kX8 = X8Tab();
 #ifndef MTBLX_ENC_CRC_MFMA
 #define MTBLX_ENC_CRC_MFMA 1
 #endif
+#ifndef MTBLX_ENC_LAZY_T   // slicing-by-4 tables built only by blocks that use them
+#define MTBLX_ENC_LAZY_T 1
+#endif
 #ifndef MTBLX_ENC_CRC_UNROLL
 #define MTBLX_ENC_CRC_UNROLL 2
 #endif
@@ -546,15 +549,22 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   uint64_t tprev = __builtin_amdgcn_s_memtime();
 #endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < 256; i += kThreads) {   // slicing-by-4 tables from the byte table
-    uint32_t t = mtblx_crc::kTab.byte[i];
-    S.T[0][i] = t;
+  // slicing-by-4 tables from the byte table: only the blocks whose CRC is not on the matrix cores
+  // need them (built there; four dependent constant-memory loads were ~5k cycles of every block)
+  auto build_tables = [&]() {
+    for (int i = tid; i < 256; i += kThreads) {
+      uint32_t t = mtblx_crc::kTab.byte[i];
+      S.T[0][i] = t;
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
-      S.T[k][i] = t;
+      for (int k = 1; k < 4; ++k) {
+        t = (t >> 8) ^ mtblx_crc::kTab.byte[t & 0xffu];
+        S.T[k][i] = t;
+      }
     }
-  }
+  };
+#if !MTBLX_ENC_LAZY_T
+  build_tables();
+#endif
   if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
   __syncthreads();
   const uint32_t b = S.sh_u32[0];
@@ -568,7 +578,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   for (uint64_t i = tid; i < n; i += kThreads) {
     const Ent e = entry_of(a.R, r0, i, iv);
     part += entry_bytes(e.sh, e.kl, e.vl);
-    if (i < kShCache) S.shc[i] = e.sh < 0xFFFFu ? (uint16_t)e.sh : (uint16_t)0xFFFFu;
+    if (i < kShCache)
+      S.shc[i] = e.sh < 0xFFFFu ? (uint16_t)e.sh : (uint16_t)0xFFFFu;
   }
   uint64_t entries = 0;
   (void)wg_excl_scan(S, part, entries);
@@ -649,6 +660,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       src = dst;
     }
     if (a.framed) {
+#if MTBLX_ENC_LAZY_T
+      if (!crc_mfma) {   // uniform over the workgroup
+        build_tables();
+        __syncthreads();
+      }
+#endif
       const uint32_t crc = crc_mfma ? crc_mfma_final(S, (uint32_t)L) : wg_crc32c(S, src, L);
       ESTAMP(6);   // CRC-32C
       if (tid == 0) {

@@ -37,6 +37,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <utility>
 
 #include "mtblx.h"
 
@@ -1167,6 +1168,240 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
 }
 }  // namespace lanes
 
+// ---- Compressible blocks (round 4): two passes, PARSE then EXECUTE ----
+//
+// k_snappy_lanes runs the tag parse and the byte moves in one per-lane chain (~390 vector and
+// ~390 scalar instructions per 16-byte chunk, divergent element kinds); k_snappy_quads runs them
+// in one per-group chain (~1000 cycles of dependent latency per element).  Here:
+//  - k_snappy_parse: one LANE per block walks the tag stream only (positions, no data): every
+//    element becomes an 8-byte entry {output offset | length << 16, source | literal << 16}
+//    (source = the literal's stream position, or the copy's offset) with the quad kernel's checks
+//    (corrupt streams, the shared-buffer overrun) -- written into the block's OWN output slot
+//    after an 8-byte header {entries, output length} (a compressible block's table is smaller than
+//    its output; a block whose table does not fit is left to the one-wave kernel);
+//  - k_snappy_exec: four blocks per wave as k_snappy_quads (the stored bytes staged in LDS, the
+//    output assembled beside them), but each element comes from the table: 16 entries per group
+//    load at once, so an element costs its byte moves (one LDS read -> write round trip) and no
+//    header decode; the table is read before the output overwrites it.
+namespace two {
+using lanes::Q4;
+using lanes::ld16;
+using lanes::alignb;
+constexpr int32_t kTable = 0x7ffffffd;   // internal status: the block's element table is in its slot
+constexpr int kParseThreads = 256;
+template <typename F, int... Ks>
+__device__ __forceinline__ void each_k(F&& f, std::integer_sequence<int, Ks...>) {   // f(K) for K in Ks, unrolled
+  (f(std::integral_constant<int, Ks>{}), ...);
+}
+
+// 8 stream bytes at window byte k < 16 of the window words (c0, c1)
+__device__ __forceinline__ void hdr8w(const Q4& c0, const Q4& c1, uint32_t k, uint32_t& lo, uint32_t& hi) {
+  const uint32_t q = k >> 2, r = k & 3u;
+  const uint32_t x0 = q == 0u ? c0.w[0] : q == 1u ? c0.w[1] : q == 2u ? c0.w[2] : c0.w[3];
+  const uint32_t x1 = q == 0u ? c0.w[1] : q == 1u ? c0.w[2] : q == 2u ? c0.w[3] : c1.w[0];
+  const uint32_t x2 = q == 0u ? c0.w[2] : q == 1u ? c0.w[3] : q == 2u ? c1.w[0] : c1.w[1];
+  lo = alignb(x1, x0, r);
+  hi = alignb(x2, x1, r);
+}
+
+__global__ void __launch_bounds__(kParseThreads) k_snappy_parse(const uint8_t* src, const uint64_t* src_off,
+                                                                const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                                const uint64_t* dst_off, const uint32_t* dst_len,
+                                                                uint32_t max_out, int32_t* status, uint32_t* dec_len) {
+  const uint32_t b = blockIdx.x * kParseThreads + threadIdx.x;
+  if (b >= nblk || status[b] != quad::kLanes) return;   // the blocks k_snappy_quads marked
+  const uint8_t* s = src + src_off[b];
+  const uint32_t n = src_len[b], cap = dst_len[b];
+  uint8_t* dg = dst + dst_off[b];
+  // the quad kernel already read the preamble: it is valid and fits the slot (else not marked)
+  uint64_t want = 0;
+  uint32_t pos = 0;
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+    const uint32_t byte = s[i];
+    want |= (uint64_t)(byte & 0x7fu) << (7 * i);
+    if (!(byte & 0x80u)) {
+      pos = i + 1;
+      break;
+    }
+  }
+  const uint32_t W = (uint32_t)want;
+  // the exec kernel's LDS layout (as k_snappy_quads): stream position p at buffer offset p + sh
+  const int32_t wb = -(int32_t)((uintptr_t)s & 15u);
+  const uint32_t span = n + (uint32_t)(-wb);
+  int32_t st = kTable;
+  if (span > (uint32_t)quad::BUF || W > min(max_out, (uint32_t)quad::OUT) || cap < 8u) st = quad::kDefer;
+  const uint32_t nch = (span + 15u) / 16u, ib = (uint32_t)quad::BUF - 16u * nch, sh = ib - (uint32_t)wb;
+  const uint32_t tcap = cap >= 8u ? (cap - 8u) / 8u : 0u;   // entries the slot holds after the header
+  uint32_t d = 0, ne = 0;
+  uint32_t wp = pos;
+  Q4 c0 = ld16(s, n, wp), c1 = ld16(s, n, wp + 16u), c2 = ld16(s, n, wp + 32u);
+  bool work = st == kTable && pos < n;
+  while (work) {
+    uint32_t lo, hi;
+    hdr8w(c0, c1, pos - wp, lo, hi);
+    const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2, avail = n - pos - 1u;
+    const uint32_t raw = (lo >> 8) | (hi << 24);
+    const bool lg = t2 >= 60u;
+    const uint32_t nb = t2 - 59u;
+    const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * (nb & 3u))) - 1u);
+    const uint32_t llit = lg ? ext + 1u : t2 + 1u, hlit = lg ? 1u + nb : 1u;
+    const bool lbad = lg && (avail < nb || ext == 0xFFFFFFFFu);
+    const uint32_t lc = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
+    const uint32_t off = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
+    const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
+    const bool lit = kind == 0u;
+    const uint32_t L0 = lit ? llit : lc, hl = lit ? hlit : need + 1u, sp = pos + hl;
+    bool bad = lit ? (lbad || n - sp < L0) : (avail < need || off == 0u || off > d);
+    bad = bad || W - d < L0;
+    const uint32_t np = lit ? sp + L0 : sp;
+    if (bad) {
+      st = MTBLX_SNAPPY_CORRUPT;
+      break;
+    }
+    if (d + L0 + 3u > np + sh || ne >= tcap) {   // the exec kernel's writes would reach unread bytes / table full
+      st = quad::kDefer;
+      break;
+    }
+    const uint32_t e0 = d | (L0 << 16), e1 = (lit ? sp : off) | (lit ? 0x10000u : 0u);
+    *reinterpret_cast<uint2*>(dg + 8u + 8u * ne) = make_uint2(e0, e1);
+    ++ne;
+    d += L0;
+    pos = np;
+    work = pos < n;
+    // keep pos - wp < 16: shift the window (the next chunk loaded 32 bytes ahead), or reload it
+    // after a long literal
+    if (work) {
+      if (pos - wp >= 48u) {
+        wp = pos;
+        c0 = ld16(s, n, wp);
+        c1 = ld16(s, n, wp + 16u);
+        c2 = ld16(s, n, wp + 32u);
+      } else {
+        while (pos - wp >= 16u) {
+          c0 = c1;
+          c1 = c2;
+          c2 = ld16(s, n, wp + 48u);
+          wp += 16u;
+        }
+      }
+    }
+  }
+  if (st == kTable && d != W) st = MTBLX_SNAPPY_CORRUPT;
+  if (st == kTable) *reinterpret_cast<uint2*>(dg) = make_uint2(ne, W);
+  status[b] = st;   // kTable (to k_snappy_exec), kDefer (to k_snappy_deferred) or CORRUPT (final)
+  if (st == MTBLX_SNAPPY_CORRUPT && dec_len) dec_len[b] = 0u;
+}
+
+__global__ void __launch_bounds__(kWave) k_snappy_exec(const uint8_t* src, const uint64_t* src_off,
+                                                       const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                       const uint64_t* dst_off, int32_t* status, uint32_t* dec_len) {
+  using namespace quad;
+  __shared__ Blk S[NG];
+  const int lane = threadIdx.x, g = lane >> 4, l = lane & 15;
+  uint8_t* base = S[g].b;
+  const uint32_t nquad = (nblk + NG - 1) / NG;
+  for (uint32_t q = blockIdx.x; q < nquad; q += gridDim.x) {
+    const uint32_t b = q * NG + (uint32_t)g;
+    const bool on = b < nblk && status[b] == kTable;
+    if (__ballot(on) == 0ull) continue;
+    const uint8_t* s = on ? src + src_off[b] : src;
+    const uint32_t n = on ? src_len[b] : 0u;
+    uint8_t* dg = on ? dst + dst_off[b] : dst;
+    const int32_t wb = -(int32_t)((uintptr_t)s & 15u);
+    const uint32_t span = n + (uint32_t)(-wb);
+    const uint32_t nch = on ? (span + 15u) / 16u : 0u;
+    const uint32_t ib = (uint32_t)BUF - 16u * nch, sh = ib - (uint32_t)wb;
+    {   // stage the stored bytes right-aligned (as k_snappy_quads)
+      uint4 v[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        const int32_t c = l + G * k, bp = wb + 16 * c;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if ((uint32_t)c < nch && bp >= 0 && bp + 16 <= (int32_t)n) v[k] = *reinterpret_cast<const uint4*>(s + bp);
+      }
+      const int32_t ph = wb + l;
+      const uint32_t hb = (on && ph >= 0 && ph < (int32_t)n) ? s[ph] : 0u;
+      const uint32_t ct = nch ? nch - 1u : 0u;
+      const int32_t pt = wb + 16 * (int32_t)ct + l;
+      const uint32_t tb = (on && pt >= 0 && pt < (int32_t)n) ? s[pt] : 0u;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        const uint32_t c = (uint32_t)(l + G * k);
+        if (c < nch) *reinterpret_cast<uint4*>(base + ib + 16 * c) = v[k];
+      }
+      if (nch) {
+        base[ib + l] = (uint8_t)hb;
+        base[ib + 16 * ct + l] = (uint8_t)tb;
+      }
+    }
+    uint2 hd = make_uint2(0u, 0u);
+    if (on) hd = *reinterpret_cast<const uint2*>(dg);
+    const uint32_t ne = hd.x, W = hd.y;
+    const uint2* tab = reinterpret_cast<const uint2*>(dg + 8);
+    // entries 16 at a time: lane l holds entry e0 + l; the next batch is loaded a batch ahead
+    uint2 cur = make_uint2(0u, 0u), nxt = make_uint2(0u, 0u);
+    if ((uint32_t)l < ne) cur = tab[l];
+    if ((uint32_t)l + 16u < ne) nxt = tab[16 + l];
+    // element K of the batch: broadcast from lane K of each group's row by DPP row_newbcast (a
+    // VALU modifier; a __shfl here is two LDS round trips per element)
+    auto elem = [&](auto kc, const uint2 bat, uint32_t e0) {
+      constexpr int K = decltype(kc)::value;
+      const uint32_t x0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bat.x, 0x150 + K, 0xf, 0xf, false);
+      const uint32_t x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bat.y, 0x150 + K, 0xf, 0xf, false);
+      const bool act = e0 + (uint32_t)K < ne;
+      if (__ballot(act) == 0ull) return;
+      const uint32_t d = x0 & 0xffffu, L = act ? x0 >> 16 : 0u, v = x1 & 0xffffu;
+      const bool lit = (x1 >> 16) != 0u;
+      const uint32_t so = lit ? v + sh : d - v;
+      const uint32_t P = (!lit && v < L) ? v : 0xFFFFFFFFu;   // overlapping copy: period v
+      const float rcp = __builtin_amdgcn_rcpf((float)(P & 0xffffu));
+      for (uint32_t s0 = 0; __ballot(s0 < L); s0 += 4u * G) {
+        const uint32_t j = s0 + 4u * (uint32_t)l;
+        if (j < L) {
+          uint32_t w;
+          uint32_t r = P == 0xFFFFFFFFu ? j : umod(j, P, rcp);
+          if (r + 4u <= P) {
+            w = *reinterpret_cast<const u32u*>(base + so + r);
+          } else {
+            w = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              w |= (uint32_t)base[so + r] << (8 * t);
+              r = r + 1u == P ? 0u : r + 1u;
+            }
+          }
+          *reinterpret_cast<u32u*>(base + d + j) = w;
+        }
+      }
+    };
+    for (uint32_t e0 = 0; __ballot(e0 < ne); e0 += 16u) {
+      const uint2 bat = cur;
+      cur = nxt;
+      if (e0 + 32u + (uint32_t)l < ne) nxt = tab[e0 + 32u + l];
+      each_k([&](auto kc) { elem(kc, bat, e0); }, std::make_integer_sequence<int, 16>{});
+    }
+    // output to HBM (the table in the slot is read: every load above has returned), statuses
+    if (on) {
+      if (((uintptr_t)dg & 15u) == 0) {
+        const uint32_t n16 = W / 16u;
+        for (uint32_t c = (uint32_t)l; c < n16; c += G)
+          reinterpret_cast<uint4*>(dg)[c] = *reinterpret_cast<const uint4*>(base + 16 * c);
+        const uint32_t tb = 16u * n16 + (uint32_t)l;
+        if (tb < W) dg[tb] = base[tb];
+      } else {
+#pragma unroll 1
+        for (uint32_t j = (uint32_t)l; j < W; j += G) dg[j] = base[j];
+      }
+      if (l == 0) {
+        status[b] = MTBLX_SNAPPY_OK;
+        if (dec_len) dec_len[b] = W;
+      }
+    }
+  }
+}
+}  // namespace two
+
+
 // ---- directory: preamble lengths, 16-byte aligned exclusive prefix ----
 constexpr int kDirThreads = 256, kDirPer = 8, kDirSpan = kDirThreads * kDirPer;
 
@@ -1311,7 +1546,12 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   // >= kLanesMinBlocks, blocks expanding > 2x go to k_snappy_lanes, the rest to the quad /
   // one-wave kernels), "lanes" (every block), "quads"
   const char* e = getenv("MTBLX_SNAPPY_KERNEL");
-  const int mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : 0;
+  const int mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : (e && !strcmp(e, "two")) ? 3 : 0;
+  // the compressible blocks k_snappy_quads marks: two passes (parse, execute) or one lane each
+#ifndef MTBLX_SNAPPY_TWO_DEFAULT
+#define MTBLX_SNAPPY_TWO_DEFAULT 0
+#endif
+  const bool two_pass = mode == 3 || (mode == 0 && MTBLX_SNAPPY_TWO_DEFAULT);
   const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(2 * lanes::kThreads);
   if (mode == 2) {
     hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
@@ -1320,13 +1560,20 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
     // k_snappy_lanes costs about one block's serial decode however many blocks run (all are in
     // flight), the quads ~0.19 ms per round of 8 192 blocks: the lanes win from ~50 000 blocks
     // (25 000 compressible blocks: quads 0.66 ms, lanes ~1.0 ms; 100 000: 2.33 vs 1.24 ms)
-    const uint32_t lanes_x = (mode == 0 && nblk >= kLanesMinBlocks) ? 2u : 0u;
+    const uint32_t lanes_x = ((mode == 0 && nblk >= kLanesMinBlocks) || mode == 3) ? 2u : 0u;
     hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len, lanes_x);
-    if (lanes_x)
+    if (lanes_x && two_pass) {
+      hipLaunchKernelGGL(two::k_snappy_parse, dim3((nblk + two::kParseThreads - 1) / two::kParseThreads),
+                         dim3(two::kParseThreads), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len,
+                         status, dec_len);
+      hipLaunchKernelGGL(two::k_snappy_exec, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
+                         dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, status, dec_len);
+    } else if (lanes_x) {
       hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
                          dst_len, status, dec_len, 1);
+    }
     hipLaunchKernelGGL(quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
                        src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   } else {

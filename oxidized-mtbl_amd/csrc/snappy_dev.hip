@@ -704,6 +704,9 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
 #ifndef MTBLX_LANE_THREADS   // decoding lanes per workgroup (as many writer lanes again)
 #define MTBLX_LANE_THREADS 256
 #endif
+#ifndef MTBLX_LANE_RING_ALL5   // ring_put writes all five words (no per-word branch)
+#define MTBLX_LANE_RING_ALL5 1
+#endif
 #ifndef MTBLX_LANE_RING_WORDS   // per-lane ring, 4-byte words (a power of two)
 #define MTBLX_LANE_RING_WORDS 64
 #endif
@@ -775,9 +778,18 @@ __device__ __forceinline__ void ring_put(uint32_t (*R)[kThreads], int t, uint32_
   w[3] = r ? alignb(v.w[3], v.w[2], 4u - r) : v.w[3];
   w[4] = r ? v.w[3] >> (32u - 8u * r) : 0u;
   const uint32_t e = r + cnt, nw = (e + 3u) >> 2;
+#if MTBLX_LANE_RING_ALL5
+  // all five words, unconditionally: the words past the chunk hold bytes at or past the new
+  // position, which no reader uses before a later put rewrites them (the carry lives in a
+  // register), and room() has already waited for the writer to take up to position + 20
+  (void)nw;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) R[(q + k) & (kRingWords - 1)][t] = w[k];
+#else
 #pragma unroll
   for (int k = 0; k < 5; ++k)
     if ((uint32_t)k < nw) R[(q + k) & (kRingWords - 1)][t] = w[k];
+#endif
   const uint32_t c = e >> 2;
   carry = c == 0u ? w[0] : c == 1u ? w[1] : c == 2u ? w[2] : c == 3u ? w[3] : w[4];
 }

@@ -24,3 +24,15 @@ def oracle():
 def mtblx_lib():
     import mtblx
     return mtblx.lib()
+
+
+@pytest.fixture(autouse=True)
+def _sync_after_gpu_test(request):
+    """GPU tests end with a device synchronize, so an asynchronous fault is reported by the test
+    whose launches caused it, not by the next test's first copy"""
+    yield
+    if request.node.get_closest_marker("gpu") is None or "torch" not in sys.modules:
+        return
+    import torch
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()

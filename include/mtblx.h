@@ -394,8 +394,9 @@ int mtblx_encode_index(const mtblx_records* rec, const uint64_t* blk_rec, uint32
  * (dst_len[b] = capacity); status[b]; dec_len[b] (device [nblk], may be NULL) = the
  * decompressed length, or 0 if the block failed -- i.e. {dst, dst_off, dec_len} is directly
  * the mtblx_block_batch directory of the decompressed blocks.  max_dst_len: host hint (max
- * of dst_len; 0 = unknown) selecting the kernel variant.  Both calls are asynchronous on
- * `stream`. */
+ * of dst_len; 0 = unknown) selecting the kernel variant; the environment variable
+ * MTBLX_SNAPPY_KERNEL (read per call: auto | quads | lanes | two) forces one for A/B runs and
+ * tests, with identical outputs and statuses.  Both calls are asynchronous on `stream`. */
 size_t mtblx_snappy_workspace_bytes(uint32_t nblk);
 int mtblx_snappy_dir(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint32_t nblk,
                      uint64_t* dst_off, uint32_t* dst_len, int32_t* status, uint64_t* totals, void* workspace,

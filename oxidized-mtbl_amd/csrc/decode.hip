@@ -2361,6 +2361,7 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
       if (wv == 0) {
         if (k1 < nloc) {
           wait_flag(a, &S.staged, (k1 + 1) * (uint32_t)P::LOADW);
+          ST.hit(8);   // stamps: the DMA-landing wait counts with the barrier, "trailers" is the trailers alone
           pipe_walk(S.buf[k1 & 1u], a, g + k1 * G, lane, ST, wmode);
           if (lane == 0) __hip_atomic_store(&S.pub, k1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }

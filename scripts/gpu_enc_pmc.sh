@@ -1,8 +1,8 @@
 #!/bin/bash
-# SQ counters of k_encode on one cfg3 chunk (two PMC passes); outputs under gpurun_out/r03/encpmc/
+# SQ counters of k_encode on one cfg3 chunk (two PMC passes); outputs under gpurun_out/${ROUND:-r04}/encpmc/
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r03/encpmc
+O=gpurun_out/${ROUND:-r04}/encpmc
 mkdir -p $O
 export TMPDIR=/tmp
 A="bench.py --config cfg3 --cfg3-blocks 100000 --no-cpu-baseline"

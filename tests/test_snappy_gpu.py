@@ -283,9 +283,9 @@ def test_snappy_file_device_decompress_then_decode(oracle):
 def test_auto_routing_large_batch(oracle, snappy_kernel):
     """a batch of 60 000 blocks (>= the 49 152 from which auto routes blocks expanding > 2x to
     k_snappy_lanes): compressible, random and corrupt streams mixed, so the quad kernel, the
-    lanes kernel (blocks the quads mark) and the deferred pass all run in one call"""
-    if snappy_kernel != "auto":
-        pytest.skip("the routing itself")
+    lanes kernel (blocks the quads mark) and the deferred pass all run in one call; under
+    "two" the marked blocks take the parse / execute kernels, whose workgroups then loop over
+    several quads each, and under "lanes" every block is one lane's"""
     codec = _dev()
     from mtblx import pipe, synth
     rng = np.random.default_rng(21)

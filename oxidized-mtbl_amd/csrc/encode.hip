@@ -232,7 +232,7 @@ static __constant__ X8Tab kX8 = X8Tab();
 #define MTBLX_ENC_LAZY_T 1
 #endif
 #ifndef MTBLX_ENC_CRC_UNROLL
-#define MTBLX_ENC_CRC_UNROLL 2
+#define MTBLX_ENC_CRC_UNROLL 4
 #endif
 constexpr int kEncSup = (kLdsBlock + mtblx_crc::kMStep * mtblx_crc::kMSup - 1) / (mtblx_crc::kMStep * mtblx_crc::kMSup);
 struct EncSw {

@@ -194,6 +194,10 @@ int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t version, co
 #define MTBLX_GET_PANIC 2   /* the reference panics                          */
 #define MTBLX_GET_ERR 3     /* Err(InvalidBlock)                             */
 #define MTBLX_GET_LOOP 4    /* the reference never returns (zero-progress entry) */
+#define MTBLX_GET_MISSING 5 /* mtblx_get_decompressed only: the lookup reached a stored block the
+                               caller's table does not hold; val_off / val_len = its stored content
+                               (framing valid, checksum verified when verify).  Decompress it, add
+                               it to the table and run the query again. */
 int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
               uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
               uint64_t* val_off, uint64_t* val_len, void* stream);
@@ -205,7 +209,10 @@ int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int veri
  * tab_start = the file offset of the stored content (Reader::block's raw_start), whose content
  * is dec[tab_doff[i] .. + tab_dlen[i]) when tab_st[i] == 0, and Err(Io) otherwise (the
  * crate's decompress error; reported like Err(InvalidBlock)).  A stored block missing from the
- * table is treated as Err(Io).  val_off of FOUND is an offset into `dec`. */
+ * table is reported as MTBLX_GET_MISSING with its stored extent: a corrupt index read with
+ * verification off can land a seek on a block the caller's linear walk of the index never
+ * reached (the reference reads, decompresses and scans it like any other).  val_off of FOUND is
+ * an offset into `dec`. */
 int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
                            uint64_t index_off, uint64_t index_len, const uint64_t* tab_start,
                            const uint64_t* tab_doff, const uint64_t* tab_dlen, const int32_t* tab_st, uint32_t ntab,
@@ -308,7 +315,8 @@ int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* keys, const 
  *     live, any key capacity) never returns early, lands on the scan chain, rebuilds the scan's
  *     keys and cannot hit the key-capacity assert: the host may then follow the directory
  *     (entries i+1, i+2, ...) after a seek.  Otherwise the host drives the live index iterator
- *     with mtblx_block_seek_batch (seek / resume) over the index block. */
+ *     with mtblx_block_seek_batch (seek / resume) over the index block.  Synchronous: returns
+ *     after the launch completed (its scratch is freed then). */
 int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t* offs, uint64_t cap, uint64_t* count,
                         uint32_t* regular, void* stream);
 

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "mtblx.h"
+#include "bounds.h"
 
 namespace {
 
@@ -37,10 +38,10 @@ __global__ void __launch_bounds__(256) k_stream_copy(const v4u* __restrict__ src
 template <int U>
 void launch(int variant, dim3 g, hipStream_t s, const v4u* src, v4u* dst, uint64_t n16) {
   switch (variant & (MTBLX_COPY_NT_STORES | MTBLX_COPY_NT_LOADS)) {
-    case 0: hipLaunchKernelGGL((k_stream_copy<U, false, false>), g, dim3(256), 0, s, src, dst, n16); break;
-    case MTBLX_COPY_NT_STORES: hipLaunchKernelGGL((k_stream_copy<U, true, false>), g, dim3(256), 0, s, src, dst, n16); break;
-    case MTBLX_COPY_NT_LOADS: hipLaunchKernelGGL((k_stream_copy<U, false, true>), g, dim3(256), 0, s, src, dst, n16); break;
-    default: hipLaunchKernelGGL((k_stream_copy<U, true, true>), g, dim3(256), 0, s, src, dst, n16); break;
+    case 0: MTBLX_LAUNCH((src, dst), (k_stream_copy<U, false, false>), g, dim3(256), 0, s, src, dst, n16); break;
+    case MTBLX_COPY_NT_STORES: MTBLX_LAUNCH((src, dst), (k_stream_copy<U, true, false>), g, dim3(256), 0, s, src, dst, n16); break;
+    case MTBLX_COPY_NT_LOADS: MTBLX_LAUNCH((src, dst), (k_stream_copy<U, false, true>), g, dim3(256), 0, s, src, dst, n16); break;
+    default: MTBLX_LAUNCH((src, dst), (k_stream_copy<U, true, true>), g, dim3(256), 0, s, src, dst, n16); break;
   }
 }
 

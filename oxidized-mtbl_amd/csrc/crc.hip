@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "bounds.h"
 #include "crc_dev.h"
 #include "crc_mfma.h"
 #include "crc_mfma_dev.h"
@@ -39,6 +40,7 @@ constexpr int kWords = kCrcWin / 4;
 #endif
 typedef uint32_t v2u __attribute__((ext_vector_type(2), aligned(1)));
 __device__ __forceinline__ v4u crc_ld16(const uint8_t* p) {
+  MTBLX_CHK(p, 16);
 #if MTBLX_CRC_NT_LOADS
   return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
 #else
@@ -46,6 +48,7 @@ __device__ __forceinline__ v4u crc_ld16(const uint8_t* p) {
 #endif
 }
 __device__ __forceinline__ v2u crc_ld8(const uint8_t* p) {
+  MTBLX_CHK(p, 8);
 #if MTBLX_CRC_NT_LOADS
   return __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
 #else
@@ -70,6 +73,7 @@ __device__ __forceinline__ uint32_t window_crc(const uint8_t* d, int64_t hi, con
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const int64_t p = lo + 4 * m + b;
+        if (p >= 0) MTBLX_CHK(d + p, 1);
         v |= (p >= 0 ? (uint32_t)d[p] : 0u) << (8 * b);
       }
       w[m] = v;
@@ -121,6 +125,8 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
   const int lane = threadIdx.x & 63;
   const uint32_t waves = gridDim.x * (kCrcThreads / kWave);
   for (uint32_t b = blockIdx.x * (kCrcThreads / kWave) + (threadIdx.x >> 6); b < nblk; b += waves) {
+    MTBLX_CHK(blk_off + b, 8);
+    MTBLX_CHK(blk_len + b, 4);
     const uint64_t off = blk_off[b];
     const uint64_t L = blk_len[b];
     const uint8_t* d = data + off;
@@ -143,6 +149,9 @@ __global__ void __launch_bounds__(kCrcThreads) k_crc32c_blocks(const uint8_t* da
       acc = wave_crc32c(d, L, S.t[0], lane);   // < kCrcWin bytes (wave_crc32c: byte-wise under 64)
     }
     if (lane == 0) {
+      if (crc_out) MTBLX_CHK(crc_out + b, 4);
+      if (bad) MTBLX_CHK(bad + b, 1);
+      if (bad && !oob && framed && off >= 4) MTBLX_CHK(d - 4, 4);
       if (crc_out) crc_out[b] = acc;
       if (bad && oob) {
         bad[b] = 1;
@@ -276,12 +285,18 @@ __device__ __forceinline__ v4u ring_read(uint32_t ax, uint32_t aa, v4i& lo, v4i&
 // serial CRC-32C of a short block (< 4 bytes), one lane
 __device__ __forceinline__ uint32_t crc_tiny(const uint8_t* d, uint64_t L) {
   uint32_t c = 0xFFFFFFFFu;
-  for (uint64_t i = 0; i < L; ++i) c = kTab.byte[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  for (uint64_t i = 0; i < L; ++i) {
+    MTBLX_CHK(d + i, 1);
+    c = kTab.byte[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  }
   return c ^ 0xFFFFFFFFu;
 }
 
 __device__ __forceinline__ void crc_store(const uint8_t* d, uint64_t off, bool oob, uint32_t c, uint32_t b,
                                           uint32_t* crc_out, uint8_t* bad, int framed) {
+  if (crc_out) MTBLX_CHK(crc_out + b, 4);
+  if (bad) MTBLX_CHK(bad + b, 1);
+  if (bad && !oob && framed && off >= 4) MTBLX_CHK(d - 4, 4);
   if (crc_out) crc_out[b] = oob ? 0u : c;
   if (bad) {
     if (oob) {
@@ -364,6 +379,8 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
     const bool valid = bi < nblk;
     uint64_t off = 0, L = 0;
     if (valid) {
+      MTBLX_CHK(blk_off + bi, 8);
+      MTBLX_CHK(blk_len + bi, 4);
       off = blk_off[bi];
       L = blk_len[bi];
     }
@@ -403,6 +420,7 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
         if (I.sb0 + lane16 + 16 <= 0) p = I.p + I.a0;
         ihd = false;
       }
+      MTBLX_CHK(p, 16);
 #if MTBLX_CRC_ABL != 2
       __builtin_amdgcn_global_load_lds(p, (lds_void*)(uintptr_t)(ring_base + ioff), 16, 0, MTBLX_CRC_DMA_AUX);
 #else
@@ -538,7 +556,8 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     }
     const uint32_t need = (in->nblk + mtblx_crc::kMWaves - 1u) / mtblx_crc::kMWaves;
     const dim3 g(need < (uint32_t)mgrid ? need : (uint32_t)mgrid), t(mtblx_crc::kMThreads);
-    hipLaunchKernelGGL(mtblx_crc::k_crc32c_mfma, g, t, 0, reinterpret_cast<hipStream_t>(stream), in->data,
+    MTBLX_LAUNCH((in->data, in->blk_off, in->blk_len, crc, bad), mtblx_crc::k_crc32c_mfma, g, t, 0,
+                 reinterpret_cast<hipStream_t>(stream), in->data,
                        in->data_len, in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
     return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
   }
@@ -557,7 +576,8 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   const uint32_t wpg = mtblx_crc::kCrcThreads / mtblx_crc::kWave;   // waves (blocks in flight) per workgroup
   const uint32_t need = (in->nblk + wpg - 1u) / wpg;
   const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);
-  hipLaunchKernelGGL(mtblx_crc::k_crc32c_blocks, g, t, 0, reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
+  MTBLX_LAUNCH((in->data, in->blk_off, in->blk_len, crc, bad), mtblx_crc::k_crc32c_blocks, g, t, 0,
+               reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
                      in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bounds.h"
+
 namespace mtblx_crc {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -161,6 +163,7 @@ __device__ __forceinline__ uint32_t wave_crc32c(const uint8_t* d, uint64_t L, co
       uint32_t w[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        MTBLX_CHK(d + lo + 16 * q, 16);
         const v4u x = *reinterpret_cast<const v4u*>(d + lo + 16 * q);
         w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
       }
@@ -181,7 +184,10 @@ __device__ __forceinline__ uint32_t wave_crc32c(const uint8_t* d, uint64_t L, co
     return acc ^ 0xFFFFFFFFu;
   }
   uint32_t c = 0xFFFFFFFFu;   // short block: every lane serially (same result everywhere)
-  for (uint64_t i = 0; i < L; ++i) c = T[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  for (uint64_t i = 0; i < L; ++i) {
+    MTBLX_CHK(d + i, 1);
+    c = T[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  }
   return c ^ 0xFFFFFFFFu;
 }
 

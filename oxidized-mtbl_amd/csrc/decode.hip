@@ -8,7 +8,8 @@
 // with ONE single-pass launch over a batch of blocks, output laid out contiguously
 // (include/mtblx.h).  See k_decode_tiles below and DESIGN.md "Kernels".
 //
-// Everything is integer/byte work: HBM-bandwidth bound, no MFMA.
+// Everything is integer/byte work: HBM-bandwidth bound (the fused verify's CRC is VALU slicing
+// here; the separate-launch CRC, crc.hip, runs it on the matrix cores).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -16,6 +17,7 @@
 
 #include <algorithm>
 
+#include "bounds.h"
 #include "crc_dev.h"
 #include "mtblx.h"
 
@@ -53,6 +55,7 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& w, uint32_t t) {
 // `lds` is the 16-byte aligned base of a stage buffer; up to 4 bytes past the window are read.
 __device__ __forceinline__ uint4 lds_win16(const uint8_t* lds, uint32_t a) {   // bytes [a, a + 16)
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (a >> 2);
+  MTBLX_LCHK(w, 20);
   const uint32_t sh = (a & 3u) * 8u;
   const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
   return make_uint4(__builtin_amdgcn_alignbit(x1, x0, sh), __builtin_amdgcn_alignbit(x2, x1, sh),
@@ -61,6 +64,7 @@ __device__ __forceinline__ uint4 lds_win16(const uint8_t* lds, uint32_t a) {   /
 
 __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t a) {   // bytes [a, a + 4)
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (a >> 2);
+  MTBLX_LCHK(w, 8);
   return __builtin_amdgcn_alignbit(w[1], w[0], (a & 3u) * 8u);
 }
 
@@ -106,9 +110,9 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 #define MTBLX_WSEND_LIGHT 1
 #endif
 #if MTBLX_NT_STORES
-#define ost(p, ...) __builtin_nontemporal_store((__VA_ARGS__), (p))
+#define ost(p, ...) (MTBLX_CHK((p), sizeof(*(p))), __builtin_nontemporal_store((__VA_ARGS__), (p)))
 #else
-#define ost(p, ...) (void)(*(p) = (__VA_ARGS__))
+#define ost(p, ...) (MTBLX_CHK((p), sizeof(*(p))), (void)(*(p) = (__VA_ARGS__)))
 #endif
 // byte-granular stores (keys of any length, value tails): MTBLX_NT_STORES == 1 streams them
 // too; == 2 keeps them in L2, where partial lines merge before they are written back
@@ -120,6 +124,7 @@ typedef uint16_t __attribute__((aligned(1))) u16u;
 
 // store the first m (0..16) bytes of w at p
 __device__ __forceinline__ void store_bytes(uint8_t* p, uint4 w, uint32_t m) {
+  MTBLX_CHK(p, m);
   if (m == 16) { ostb(reinterpret_cast<v4u*>(p), v4u{w.x, w.y, w.z, w.w}); return; }
   if (m & 8) { ostb(reinterpret_cast<v2u*>(p), v2u{w.x, w.y}); w = make_uint4(w.z, w.w, 0, 0); p += 8; }
   if (m & 4) { ostb(reinterpret_cast<u32u*>(p), w.x); w.x = w.y; p += 4; }
@@ -178,12 +183,14 @@ struct GenOut {
 };
 
 __device__ __forceinline__ uint32_t grd32(const uint8_t* p) {
+  MTBLX_CHK(p, 4);
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
 // varint_decode32 on global bytes d[0..avail), avail >= 1
 __device__ uint32_t gdec32(const uint8_t* d, uint64_t avail, uint32_t& val) {
   uint32_t win = avail < 5 ? (uint32_t)avail : 5u;
+  MTBLX_CHK(d, win);
   uint32_t len = 0;
   for (uint32_t t = 0; t < win; ++t) {
     if (!(d[t] & 0x80u)) { len = t + 1; break; }
@@ -222,6 +229,7 @@ __device__ GenOut generic_block(const uint8_t* d, uint64_t L, uint8_t* keys, uin
     // decode_entry (:216-238)
     uint64_t p = cur;
     if (R - p < 3) { o.st = MTBLX_ST_CORRUPT; break; }
+    MTBLX_CHK(d + p, 3);
     uint32_t sh = d[p], ns = d[p + 1], vl = d[p + 2];
     if ((sh | ns | vl) < 128u) {
       p += 3;
@@ -247,6 +255,12 @@ __device__ GenOut generic_block(const uint8_t* d, uint64_t L, uint8_t* keys, uin
     if (WRITE) {
       uint8_t* kd = keys + o.kb;
       const uint8_t* ks = keys + kprev;
+      if (m) { MTBLX_CHK(ks, m); }
+      if (newlen) { MTBLX_CHK(kd, newlen); }
+      if (ns) { MTBLX_CHK(d + p, ns); }
+      if (vl) { MTBLX_CHK(d + p + ns, vl); MTBLX_CHK(vals + o.vb, vl); }
+      MTBLX_CHK(key_end + o.nrec, 4);
+      MTBLX_CHK(val_end + o.nrec, 4);
       for (uint64_t i = 0; i < m; ++i) kd[i] = ks[i];
       for (uint64_t i = 0; i < ns; ++i) kd[m + i] = d[p + i];
       uint8_t* vd = vals + o.vb;
@@ -539,6 +553,8 @@ __device__ __forceinline__ void pipe_close(const TileArgs& a) {   // last tile's
 __device__ __forceinline__ void tile_range(const TileArgs& a, uint32_t t, uint32_t tb, uint64_t& r0, uint64_t& r1) {
   uint32_t b0, nb;
   tile_span(a, t, b0, nb);
+  MTBLX_CHK(a.blk_off + b0, 8 * nb);
+  MTBLX_CHK(a.blk_len + b0, 4 * nb);
   const uint64_t s = a.blk_off[b0];
   const uint64_t e = a.blk_off[b0 + nb - 1] + a.blk_len[b0 + nb - 1];
   const uint64_t base = reinterpret_cast<uintptr_t>(a.data);
@@ -551,10 +567,13 @@ __device__ __forceinline__ void tile_range(const TileArgs& a, uint32_t t, uint32
 
 // prefetch chunk c (16 B) of a contiguous range into v (zero-filled outside the buffer)
 __device__ __forceinline__ uint4 load_chunk(const TileArgs& a, uint64_t off) {
-  if (off + 16 <= a.data_len) return *reinterpret_cast<const uint4*>(a.data + off);
+  if (off + 16 <= a.data_len) {
+    MTBLX_CHK(a.data + off, 16);
+    return *reinterpret_cast<const uint4*>(a.data + off);
+  }
   uint32_t t[4] = {0, 0, 0, 0};
   for (int i = 0; i < 16; ++i)
-    if (off + i < a.data_len) t[i >> 2] |= (uint32_t)a.data[off + i] << (8 * (i & 3));
+    if (off + i < a.data_len) MTBLX_CHK(a.data + off + i, 1), t[i >> 2] |= (uint32_t)a.data[off + i] << (8 * (i & 3));
   return make_uint4(t[0], t[1], t[2], t[3]);
 }
 
@@ -586,7 +605,7 @@ __device__ __forceinline__ bool walk_interval(const uint8_t* stage, Rec* recs, u
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   while (p < e) {
     const uint32_t ad = bo + p;
-    uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
+    uint32_t hw = (MTBLX_LCHK(st32 + (ad >> 2), 8), __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u));
     uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu, h = 3;
     if (__builtin_expect((hw & 0x808080u) != 0u, 0)) {  // multi-byte varint header (slow path)
       if (R - p < 3u) return false;
@@ -639,7 +658,7 @@ __device__ __forceinline__ bool walk_fast(const uint8_t* stage, Rec* recs, uint3
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   do {
     const uint32_t ad = bo + p;
-    const uint32_t hw = __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u);
+    const uint32_t hw = (MTBLX_LCHK(st32 + (ad >> 2), 8), __builtin_amdgcn_alignbit(st32[(ad >> 2) + 1], st32[ad >> 2], (ad & 3u) * 8u));
     const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
     const uint32_t np = p + 3u + ns + vl;
     bad |= (hw & 0x808080u) | (uint32_t)(sh > prevlen) | (uint32_t)(np > R);
@@ -793,6 +812,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         for (; c < nch; c += kThreads) *reinterpret_cast<uint4*>(S.stage + 16 + 16 * c) = load_chunk(a, r0 + 16ull * c);
       }
       if (tid < (int)nb) {
+        MTBLX_CHK(a.blk_off + b0 + tid, 8);
+        MTBLX_CHK(a.blk_len + b0 + tid, 4);
         const uint64_t off = a.blk_off[b0 + tid];
         const uint32_t L = a.blk_len[b0 + tid];
         S.boff[tid] = off + L > a.data_len ? kOutOfBounds
@@ -802,6 +823,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
     } else {
       // fallback: one 16-aligned slot per block, wave w stages blocks w, w+4, ...
       for (uint32_t j = wv; j < nb; j += kThreads / kWave) {
+        MTBLX_CHK(a.blk_off + b0 + j, 8);
+        MTBLX_CHK(a.blk_len + b0 + j, 4);
         const uint32_t L = a.blk_len[b0 + j];
         const uint64_t off = a.blk_off[b0 + j];
         const uint32_t so = 16u + j * a.slot;
@@ -1015,6 +1038,7 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         S.tpre[0] = pre0; S.tpre[1] = pre1; S.tpre[2] = pre2;
         S.tinc[0] = pre0 + agg_r; S.tinc[1] = pre1 + agg_k; S.tinc[2] = pre2 + agg_v;
         if (t == a.ntiles - 1) {
+          MTBLX_CHK(a.totals, 24);
           a.totals[0] = pre0 + agg_r;
           a.totals[1] = pre1 + agg_k;
           a.totals[2] = pre2 + agg_v;
@@ -1029,6 +1053,11 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
     if (tid < (int)nb) {
       const uint32_t j = tid, b = b0 + j;
       const uint64_t rb = pr + S.brb[j], kb = pk + S.bkbb[j], vb = pv + S.bvbb[j];
+      MTBLX_CHK(a.nrec + b, 4);
+      MTBLX_CHK(a.rec_base + b, 8);
+      MTBLX_CHK(a.key_base + b, 8);
+      MTBLX_CHK(a.val_base + b, 8);
+      MTBLX_CHK(a.status + b, 4);
       a.nrec[b] = S.bcnt[j];
       a.rec_base[b] = rb;
       a.key_base[b] = kb;
@@ -1056,6 +1085,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
         const uint32_t klen = shr + ns;
         // key_end / val_end: END offsets relative to the block's bases
         const uint64_t gr = pr + S.brb[j] + (q + rlo - S.brf[j]);
+        MTBLX_CHK(a.key_end + gr, 4);
+        MTBLX_CHK(a.val_end + gr, 4);
         a.key_end[gr] = ks + klen - S.bkbb[j];
         a.val_end[gr] = vs + vl - S.bvbb[j];
 #ifndef MTBLX_ABL_NOVAL
@@ -1311,12 +1342,14 @@ __device__ __forceinline__ bool walk_pos(const uint8_t* stage, uint16_t* pos, ui
   uint32_t p = s, prevlen = 0, orf = 0, badsh = 0, ssh = 0, svl = 0, c = 0;
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   uint32_t ad = bo + p;
+  MTBLX_LCHK(st32 + (ad >> 2), 8);
   uint32_t w0 = st32[ad >> 2], w1 = st32[(ad >> 2) + 1];
   do {
     const uint32_t hw = __builtin_amdgcn_alignbit(w1, w0, (ad & 3u) * 8u);
     const uint32_t sh = hw & 0xffu, ns = (hw >> 8) & 0xffu, vl = (hw >> 16) & 0xffu;
     const uint32_t np = p + 3u + ns + vl;
     ad = bo + np;
+    MTBLX_LCHK(st32 + (ad >> 2), 8);
     w0 = st32[ad >> 2];
     w1 = st32[(ad >> 2) + 1];
     pos[slot0 + c] = (uint16_t)p;
@@ -1348,6 +1381,7 @@ __device__ __forceinline__ bool walk_pos2(const uint8_t* stage, uint16_t* pos, u
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
   do {
     const uint32_t ad = bo + p, q = ad >> 2, sft = (ad & 3u) * 8u;
+    MTBLX_LCHK(st32 + q, 12);
     const uint32_t w0 = st32[q], w1 = st32[q + 1], w2 = st32[q + 2];
     uint64_t x = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sft) |
                  ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sft) << 32);
@@ -1452,12 +1486,12 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
     if (mlo <= part) m = part;
     const uint8_t* gp = a.data + r0 + 16ull * ((uint64_t)m * kWave + (uint32_t)lane);
     for (; m < mfull; m += P::LOADW, gp += 16 * kWave * P::LOADW)
-      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
+      MTBLX_CHK(gp, 16), MTBLX_LCHK(B.stage + 16 + 1024 * m, 1024), __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
     for (; m * kWave < nch && m < mhi; m += P::LOADW) {
       const uint32_t c = m * kWave + lane;
       const uint64_t go = r0 + 16ull * c;
       if (c < nfull)
-        __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
+        MTBLX_CHK(a.data + go, 16), MTBLX_LCHK(B.stage + 16 + 1024 * m, 1024), __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + 16 + 1024 * m), 16, 0, MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
       else if (c < nch)
         *reinterpret_cast<uint4*>(B.stage + 16 + 16 * c) = load_chunk(a, go);
     }
@@ -1485,7 +1519,7 @@ __device__ __forceinline__ void pipe_dma(PipeBuf<P>& B, const TileArgs& a, uint3
           const uint64_t go = a0 + 16ull * c;
           if (c < nch) {
             if (go + 16 <= a.data_len && ((base + go) & 15ull) == 0)
-              __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + so + 1024 * m), 16, 0,
+              MTBLX_CHK(a.data + go, 16), MTBLX_LCHK(B.stage + so + 1024 * m, 1024), __builtin_amdgcn_global_load_lds((g_void*)(a.data + go), (lds_void*)(B.stage + so + 1024 * m), 16, 0,
                                                MTBLX_NT_LOADS ? MTBLX_DMA_AUX : 0);
             else
               *reinterpret_cast<uint4*>(B.stage + so + 16 * c) = load_chunk(a, go);
@@ -1577,6 +1611,7 @@ __device__ __forceinline__ void pipe_walk(PipeBuf<P>& B, const TileArgs& a, uint
   uint32_t gc = 0, gk = 0, gv = 0;
   int32_t gst = MTBLX_ST_OK;
   if (lane < (int)nb && !ok) {
+    if (bo == kNotStaged) MTBLX_CHK(a.blk_off + b0 + lane, 8);
     const uint8_t* d = (bo != kNotStaged) ? (B.stage + bo) : (a.data + a.blk_off[b0 + lane]);
     const GenOut o = bo == kOutOfBounds ? GenOut{0, 0, 0, MTBLX_ST_CORRUPT}
                                         : generic_block<false>(d, L, nullptr, nullptr, nullptr, nullptr);
@@ -1722,6 +1757,7 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
   tinc[2] = pv + B.ttot[2];
   if (lane == 0) {
     B.tpre[0] = pr; B.tpre[1] = pk; B.tpre[2] = pv;
+    if (t == a.ntiles - 1) MTBLX_CHK(a.totals, 24);
     if (t == a.ntiles - 1) { a.totals[0] = tinc[0]; a.totals[1] = tinc[1]; a.totals[2] = tinc[2]; }
   }
   // the copy waves need only tpre, and bwr where a block overflows the caller's buffers: when
@@ -1734,6 +1770,11 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
   if (lane < (int)nb) {
     const uint32_t j = lane, b = b0 + j;
     const uint64_t rb = pr + B.brb[j], kb = pk + B.bkbb[j], vb = pv + B.bvbb[j];
+    MTBLX_CHK(a.nrec + b, 4);
+    MTBLX_CHK(a.rec_base + b, 8);
+    MTBLX_CHK(a.key_base + b, 8);
+    MTBLX_CHK(a.val_base + b, 8);
+    MTBLX_CHK(a.status + b, 4);
     a.nrec[b] = B.bcnt[j];
     a.rec_base[b] = rb;
     a.key_base[b] = kb;
@@ -2050,6 +2091,7 @@ constexpr uint32_t kCrcRounds = (65664u + 64u * kCrcWinB - 1u) / (64u * kCrcWinB
 template <class P>
 __device__ __forceinline__ uint32_t lds_window_raw(const PipeLds<P>& S, const uint32_t* st32, int32_t A, int32_t p0) {
   const int32_t q = A >> 2;                       // floor
+  if (q + (int32_t)kCrcWinB / 4 >= 0) MTBLX_LCHK(st32 + (q > 0 ? q : 0), 4 * (q + (int32_t)kCrcWinB / 4 + 1 - (q > 0 ? q : 0)));
   const uint32_t sft = (uint32_t)(A & 3) * 8u;
   uint32_t d0 = q >= 0 ? st32[q] : 0u;
   uint32_t c = 0;
@@ -2083,6 +2125,7 @@ __device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileAr
       crc = S.cacc[par][lane] ^ 0xFFFFFFFFu;
     } else if (o < kOutOfBounds) {   // < 4 bytes: byte-wise with the init
       uint32_t x = 0xFFFFFFFFu;
+      MTBLX_LCHK(B.stage + o, L);
       for (uint32_t t = 0; t < L; ++t) x = S.crcT[0][(x ^ B.stage[o + t]) & 0xffu] ^ (x >> 8);
       crc = x ^ 0xFFFFFFFFu;
     }
@@ -2091,12 +2134,15 @@ __device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileAr
   // blocks that were not staged (larger than a slot): from HBM, the wave together
   for (uint32_t j = 0; j < nb; ++j) {
     if (B.boff[j] != kNotStaged) continue;
+    MTBLX_CHK(a.blk_off + b0 + j, 8);
     const uint64_t off = a.blk_off[b0 + j];
     const uint32_t x = mtblx_crc::wave_crc32c(a.data + off, B.blen[j], &S.crcT[0][0], lane);
     if (lane == (int)j) crc = x;
   }
   if (lane < (int)nb) {
     const uint32_t b = b0 + lane;
+    if (a.crc) MTBLX_CHK(a.crc + b, 4);
+    if (a.crc_bad) MTBLX_CHK(a.crc_bad + b, 1);
     if (a.crc) a.crc[b] = crc;
     if (a.crc_bad) {
       uint8_t bad = 0;
@@ -2130,9 +2176,13 @@ __device__ MTBLX_PIPE_CRC_INLINE void pipe_crc_copy(const PipeBuf<P>& B, const T
   // copy wave 0: the stored checksums (framed batches), loaded now, written to LDS at the end
   uint32_t stored = 0, framed = 0;
   if (cw == 0 && lane < (int)nb && a.crc_framed && (MTBLX_ABL_CRC & 2) == 0) {
+    MTBLX_CHK(a.blk_off + B.b0 + lane, 8);
     const uint64_t off = a.blk_off[B.b0 + lane];
-    if (off >= 4) {
+    // a window past the buffer (a corrupt directory) is never read: pipe_crc_final reports it as
+    // bad without its stored checksum (r05: this read was unguarded)
+    if (off >= 4 && off <= a.data_len) {
       const uint8_t* d = a.data + off;
+      MTBLX_CHK(d - 4, 4);
       stored = (uint32_t)d[-4] | ((uint32_t)d[-3] << 8) | ((uint32_t)d[-2] << 16) | ((uint32_t)d[-1] << 24);
       framed = 1;
     }
@@ -2282,6 +2332,8 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
     uint32_t b0, nb;
     tile_span(a, g + kk * G, b0, nb);
     const uint32_t j = (uint32_t)lane < nb ? (uint32_t)lane : nb - 1;
+    MTBLX_CHK(a.blk_off + b0 + j, 8);
+    MTBLX_CHK(a.blk_len + b0 + j, 4);
     ioff = a.blk_off[b0 + j];
     ilen = a.blk_len[b0 + j];
   };
@@ -2653,18 +2705,20 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
              wscap,        0,             0,            debug_flags()};
   a.wait_ticks = debug_ms("MTBLX_DEBUG_WAIT_MS", kWaitTicks);
   a.dbg_delay0 = debug_ms("MTBLX_DEBUG_DELAY0_MS", 0);
+#define MTBLX_DECODE_PTRS (in->data, in->blk_off, in->blk_len, out->nrec, out->rec_base, out->key_base, out->val_base, \
+                           out->status, out->key_end, out->val_end, out->keys, out->vals, out->totals, ws, crc, crc_bad)
   if (p.kind == 0) {
     if (verify)
-      hipLaunchKernelGGL(k_decode_pipe<PipeSmallV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+      MTBLX_LAUNCH(MTBLX_DECODE_PTRS, k_decode_pipe<PipeSmallV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
     else
-      hipLaunchKernelGGL(k_decode_pipe<PipeSmall>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+      MTBLX_LAUNCH(MTBLX_DECODE_PTRS, k_decode_pipe<PipeSmall>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   } else if (p.kind == 1) {
     if (verify)
-      hipLaunchKernelGGL(k_decode_pipe<PipeLargeV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+      MTBLX_LAUNCH(MTBLX_DECODE_PTRS, k_decode_pipe<PipeLargeV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
     else
-      hipLaunchKernelGGL(k_decode_pipe<PipeLarge>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
+      MTBLX_LAUNCH(MTBLX_DECODE_PTRS, k_decode_pipe<PipeLarge>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);
   } else {
-    hipLaunchKernelGGL(k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
+    MTBLX_LAUNCH(MTBLX_DECODE_PTRS, k_decode_tiles<CfgLarge>, dim3(resident_grid<CfgLarge>(p.ntiles)), dim3(kThreads), 0, s, a);
     // blocks above ~64 KiB: the checksum is a separate launch (k_crc32c_blocks)
     if (verify && hipGetLastError() == hipSuccess) return mtblx_crc32c_blocks(in, crc, crc_bad, framed, s);
   }

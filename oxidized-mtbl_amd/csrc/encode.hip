@@ -18,7 +18,7 @@
 // array, count); then the look-back resolves the block's file offset, the CRC-32C of the
 // content is computed from LDS and the block streams out with 16-byte stores.  Blocks larger
 // than the LDS buffer are assembled in place in HBM after the look-back.
-// All integer/byte work (HBM bound, no MFMA).
+// Integer/byte work, HBM bound; the block CRC-32C runs on the matrix cores (crc_mfma_dev.h).
 // Round 3 variants, measured on cfg3 (2 x 200 000 blocks, profiles/r03/late, product 914-916
 // GiB/s) and removed: persistent workgroups (2 per CU) claiming the next block's ticket at the
 // block's start 900-901 / at the look-back 905-908 (the block loop raised scratch 48 -> 96-104
@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "crc_dev.h"
+#include "bounds.h"
 #include "crc_mfma_dev.h"
 #include "mtblx.h"
 
@@ -765,7 +766,7 @@ extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard
              d, d + nshard, blk_rec, dflags, 0};
   if (hipMemsetAsync(dflags, 0, 16, s) != hipSuccess) rc = MTBLX_E_HIP;
   if (rc == MTBLX_OK) {
-    hipLaunchKernelGGL(k_plan, dim3(nshard), dim3(kWave), 0, s, a);
+    MTBLX_LAUNCH((rec->keys, rec->key_end, rec->vals, rec->val_end, shard_rec, d, blk_rec), k_plan, dim3(nshard), dim3(kWave), 0, s, a);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(cnt.data(), d, 8ull * nshard, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(&fl, dflags, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
@@ -782,7 +783,7 @@ extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard
     a.write = 1;
     if (hipMemcpyAsync(d + nshard, first.data(), 8ull * nshard, hipMemcpyHostToDevice, s) != hipSuccess) rc = MTBLX_E_HIP;
     if (rc == MTBLX_OK) {
-      hipLaunchKernelGGL(k_plan, dim3(nshard), dim3(kWave), 0, s, a);
+      MTBLX_LAUNCH((rec->keys, rec->key_end, rec->vals, rec->val_end, shard_rec, d, blk_rec), k_plan, dim3(nshard), dim3(kWave), 0, s, a);
       // blk_rec[total] = the end of the last shard
       if (hipGetLastError() != hipSuccess ||
           hipMemcpyAsync(blk_rec + total, shard_rec + nshard, 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -824,6 +825,6 @@ extern "C" int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk
             totals,
             reinterpret_cast<uint32_t*>(ws),
             reinterpret_cast<uint64_t*>(ws + 256)};
-  hipLaunchKernelGGL(k_encode, dim3(nblk), dim3(kThreads), 0, s, a);
+  MTBLX_LAUNCH((rec->keys, rec->key_end, rec->vals, rec->val_end, blk_rec, out, blk_off, blk_len, status, totals, workspace), k_encode, dim3(nblk), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include "mtblx.h"
+#include "bounds.h"
 
 namespace mtblx_idx {
 
@@ -186,8 +187,8 @@ extern "C" int mtblx_encode_index(const mtblx_records* rec, const uint64_t* blk_
   uint64_t kbytes = 0, vbytes = 0;
   if (nblk) {
     const dim3 g((nblk + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_index_len, g, dim3(kThreads), 0, s, a);
-    hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, s, key_end, val_end, nblk);
+    MTBLX_LAUNCH((blk_off, blk_len, key_end, val_end, blk_rec), k_index_len, g, dim3(kThreads), 0, s, a);
+    MTBLX_LAUNCH((key_end, val_end), k_scan2, dim3(1), dim3(1024), 0, s, key_end, val_end, nblk);
     if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&kbytes, key_end + nblk - 1, 8, hipMemcpyDeviceToHost, s) ||
         hipMemcpyAsync(&vbytes, val_end + nblk - 1, 8, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
       return MTBLX_E_HIP;
@@ -197,7 +198,7 @@ extern "C" int mtblx_encode_index(const mtblx_records* rec, const uint64_t* blk_
   a.keys = kv.as<uint8_t>();
   a.vals = kv.as<uint8_t>(kbytes + 8);
   if (nblk) {
-    hipLaunchKernelGGL(k_index_write, dim3((nblk + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a);
+    MTBLX_LAUNCH((blk_off, blk_len, key_end, val_end, blk_rec, kv.p), k_index_write, dim3((nblk + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a);
     if (hipGetLastError() != hipSuccess) return MTBLX_E_HIP;
   }
   // Writer::into_inner: the index block, written like any block (write_block, None, framed)

@@ -87,3 +87,40 @@ extern "C" int mtblx_decode_blocks_verify(const mtblx_block_batch* in, const mtb
   if (rc != MTBLX_OK) return rc;
   return mtblx_crc32c_blocks(in, crc, crc_bad, framed & 1, stream);
 }
+
+// ---- bounds-checked diagnostic build only (csrc/bounds.h, Makefile target `bounds`) ----
+#ifdef MTBLX_BOUNDS
+#include <stdio.h>
+
+#include <mutex>
+#include <string>
+static std::mutex g_bounds_mu;
+static unsigned long long g_bounds_viol = 0, g_bounds_fault = 0;
+static std::string g_bounds_first;
+
+extern "C" void mtblx_bounds_note(const char* kernel, uint64_t line, uint64_t addr, uint64_t nbytes, int fault) {
+  std::lock_guard<std::mutex> lk(g_bounds_mu);
+  if (fault) ++g_bounds_fault;
+  else ++g_bounds_viol;
+  if (g_bounds_first.empty()) {
+    char buf[512];
+    snprintf(buf, sizeof(buf), "%s %s line %llu addr 0x%llx bytes %llu", fault ? "FAULT" : "OOB", kernel,
+             (unsigned long long)line, (unsigned long long)addr, (unsigned long long)nbytes);
+    g_bounds_first = buf;
+  }
+}
+#endif
+
+// Violations recorded by the bounds-checked build (violations | faults << 32), the first one
+// described in buf.  The product build has nothing to report: -1.
+extern "C" long long mtblx_bounds_report(char* buf, size_t cap) {
+#ifdef MTBLX_BOUNDS
+  std::lock_guard<std::mutex> lk(g_bounds_mu);
+  if (buf && cap) snprintf(buf, cap, "%s", g_bounds_first.c_str());
+  return (long long)(g_bounds_viol | (g_bounds_fault << 32));
+#else
+  (void)buf;
+  (void)cap;
+  return -1;
+#endif
+}

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "mtblx.h"
+#include "bounds.h"
 #include "mtblx_host.h"
 
 
@@ -545,7 +546,7 @@ extern "C" int mtblx_pipe_decode(mtblx_pipe* p, const uint8_t* file, uint64_t fi
     if (hipStreamWaitEvent(so, s.e_dec, 0) != hipSuccess) return MTBLX_E_HIP;
     const bool fits = R + nr <= out->rec_cap && K + kb <= out->keys_cap && V + vb <= out->vals_cap &&
                       (!nr || (out->key_end && out->val_end)) && (!kb || out->keys) && (!vb || out->vals);
-    hipLaunchKernelGGL(k_rebase, dim3((c.nb + 255) / 256), dim3(256), 0, so, s.o.rec_base, s.o.key_base, s.o.val_base,
+    MTBLX_LAUNCH((s.o.rec_base, s.o.key_base, s.o.val_base), k_rebase, dim3((c.nb + 255) / 256), dim3(256), 0, so, s.o.rec_base, s.o.key_base, s.o.val_base,
                        c.nb, R, K, V);
     auto d2h = [&](void* dst, const void* srcp, uint64_t n) {
       st.d2h_bytes += n;

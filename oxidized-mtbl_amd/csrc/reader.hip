@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bounds.h"
 #include "crc_dev.h"
 #include "mtblx.h"
 
@@ -20,8 +21,10 @@ namespace mtblx_rd {
 
 // varint_length_packed over d[0..n) (src/varint.rs:1-10): 0 if no terminator
 __device__ __forceinline__ uint32_t length_packed(const uint8_t* d, uint64_t n) {
-  for (uint64_t i = 0; i < n; ++i)
+  for (uint64_t i = 0; i < n; ++i) {
+    MTBLX_CHK(d + i, 1);
     if (!(d[i] & 0x80u)) return (uint32_t)i + 1;
+  }
   return 0;
 }
 
@@ -30,6 +33,7 @@ __device__ __forceinline__ uint32_t length_packed(const uint8_t* d, uint64_t n) 
 // (n == 0: it indexes data[0]; fewer than 4 bytes on the 64-bit path: data[1..3]).
 __device__ __forceinline__ int dec64(const uint8_t* d, uint64_t n, uint64_t& v) {
   if (n == 0) return -1;
+  MTBLX_CHK(d, 1);
   const uint32_t l = length_packed(d, n < 10 ? n : 10);
   if (l < 5) {
     const uint32_t l32 = length_packed(d, n < 5 ? n : 5);
@@ -41,6 +45,7 @@ __device__ __forceinline__ int dec64(const uint8_t* d, uint64_t n, uint64_t& v) 
     v = val;
     return (int)l32;
   }
+  MTBLX_CHK(d, l);
   uint64_t val = (uint64_t)(d[0] & 0x7fu) | ((uint64_t)(d[1] & 0x7fu) << 7) | ((uint64_t)(d[2] & 0x7fu) << 14) |
                  ((uint64_t)(d[3] & 0x7fu) << 21);
   uint32_t shift = 28;
@@ -57,6 +62,8 @@ __global__ void k_block_dir(const uint8_t* file, uint64_t file_len, uint32_t ver
                             uint32_t* blk_len, int32_t* dir_st) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nent) return;
+  MTBLX_CHK(val_end + i, 4);
+  if (i) MTBLX_CHK(val_end + i - 1, 4);
   const uint64_t v0 = val_base + (i ? val_end[i - 1] : 0u), v1 = val_base + val_end[i];
   uint64_t off = 0, start = 0, sz = 0;
   int32_t st = MTBLX_DIR_OK;
@@ -70,6 +77,7 @@ __global__ void k_block_dir(const uint8_t* file, uint64_t file_len, uint32_t ver
       if (off + 4 > file_len) st = MTBLX_DIR_PANIC;
       else {
         ll = 4;
+        MTBLX_CHK(file + off, 4);
         sz = (uint64_t)file[off] | ((uint64_t)file[off + 1] << 8) | ((uint64_t)file[off + 2] << 16) |
              ((uint64_t)file[off + 3] << 24);
       }
@@ -84,6 +92,9 @@ __global__ void k_block_dir(const uint8_t* file, uint64_t file_len, uint32_t ver
     if (start > file_len || sz > file_len - start) st = MTBLX_DIR_PANIC;   // BytesView::slice assert
     else if (sz > 0xFFFFFFFFull) st = MTBLX_DIR_UNSUPPORTED;
   }
+  MTBLX_CHK(blk_off + i, 8);
+  MTBLX_CHK(blk_len + i, 4);
+  MTBLX_CHK(dir_st + i, 4);
   blk_off[i] = (st == MTBLX_DIR_OK || st == MTBLX_DIR_UNSUPPORTED) ? start : 0;   // >= 4 GiB: start only
   blk_len[i] = st == MTBLX_DIR_OK ? (uint32_t)sz : 0u;
   dir_st[i] = st;
@@ -121,11 +132,13 @@ struct It {
 enum { R_OK = 1, R_END = 0, R_PANIC = -1, R_LOOP = -2 };
 
 __device__ __forceinline__ uint32_t rd32g(const uint8_t* p) {
+  MTBLX_CHK(p, 4);
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
 // varint_decode32 on d[0..n), n >= 1
 __device__ __forceinline__ uint32_t dec32g(const uint8_t* d, uint64_t n, uint32_t& v) {
+  MTBLX_CHK(d, 1);
   const uint32_t l = length_packed(d, n < 5 ? n : 5);
   uint32_t val = d[0] & 0x7fu;
   if (l > 1) val |= (uint32_t)(d[1] & 0x7fu) << 7;
@@ -164,6 +177,7 @@ __device__ __forceinline__ int decode_entry(const Blk& b, uint64_t p, uint64_t l
                                             uint32_t& vl, uint64_t& pout) {
   if (limit - p < 3) return R_PANIC;
   if (p + 2 >= b.L) return R_PANIC;
+  MTBLX_CHK(b.d + p, 3);
   uint32_t x = b.d[p], y = b.d[p + 1], z = b.d[p + 2];
   if ((x | y | z) < 128u) {
     p += 3;
@@ -213,7 +227,7 @@ __device__ int parse_next_key(const Blk& b, It& it, const uint8_t* t, uint64_t t
   }
   if (m <= it.c) {            // the kept prefix matches the target: compare the suffix
     uint64_t c = m, j = 0;
-    while (j < ns && c < tlen && b.d[p + j] == t[c]) { ++j; ++c; }
+    while (j < ns && c < tlen && (MTBLX_CHK(b.d + p + j, 1), MTBLX_CHK(t + c, 1), b.d[p + j] == t[c])) { ++j; ++c; }
     it.cmp = (j < ns && c < tlen) ? (b.d[p + j] < t[c] ? -1 : 1) : 0;
     it.c = c;
   }                           // else: the first difference lies in the kept prefix
@@ -238,7 +252,7 @@ __device__ int seek(const Blk& b, It& it, const uint8_t* t, uint64_t tlen) {
     if (sh != 0) return R_OK;                                 // "corruption": early return
     if (ko + ns > b.L) return R_PANIC;
     uint64_t c = 0;
-    while (c < ns && c < tlen && b.d[ko + c] == t[c]) ++c;
+    while (c < ns && c < tlen && (MTBLX_CHK(b.d + ko + c, 1), MTBLX_CHK(t + c, 1), b.d[ko + c] == t[c])) ++c;
     const int r = (c < ns && c < tlen) ? (b.d[ko + c] < t[c] ? -1 : 1) : (ns < tlen ? -1 : (ns > tlen ? 1 : 0));
     if (r < 0) left = mid;
     else right = mid - 1;
@@ -284,8 +298,10 @@ struct FileCtx {
 };
 
 // block_at_index + Reader::block (src/reader.rs:177-186, :139-174):
-// 1 = Some(block), 0 = None, R_PANIC, 2 = Err(InvalidBlock)
-__device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk& out) {
+// 1 = Some(block), 0 = None, R_PANIC, 2 = Err(InvalidBlock), 3 = a compressed block the caller's
+// table does not hold (its stored content [mstart, + msz) passed framing and the checksum)
+__device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk& out, uint64_t& mstart,
+                              uint64_t& msz) {
   if (!valid(ib, ii)) return 0;                                // get() -> None
   if (ii.voff + ii.vlen > ib.L) return R_PANIC;
   uint64_t off = 0;
@@ -308,10 +324,18 @@ __device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk
     uint32_t lo = 0, hi = f.tab.n;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) / 2;
+      MTBLX_CHK(f.tab.start + mid, 8);
       if (f.tab.start[mid] < start) lo = mid + 1;
       else hi = mid;
     }
-    if (lo == f.tab.n || f.tab.start[lo] != start || f.tab.st[lo] != 0) return 2;   // Err(Io)
+    if (lo == f.tab.n || f.tab.start[lo] != start) {   // not decompressed by the caller (yet)
+      mstart = start;
+      msz = sz;
+      return 3;
+    }
+    if (f.tab.st[lo] != 0) return 2;   // the crate's decompress error: Err(Io)
+    MTBLX_CHK(f.tab.doff + lo, 8);
+    MTBLX_CHK(f.tab.dlen + lo, 8);
     content = f.tab.dec + f.tab.doff[lo];
     sz = f.tab.dlen[lo];
   }
@@ -333,6 +357,7 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
   const FileCtx f{file, file_len, version, verify, T, lane, tab};
   const uint8_t* vbase = tab.dec ? tab.dec : file;   // values are offsets into the scanned bytes
   for (uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); q < nq; q += waves) {
+    MTBLX_CHK(qend + q, 8);
     const uint64_t k0 = q ? qend[q - 1] : 0, k1 = qend[q];
     const uint8_t* t = qkeys + k0;
     const uint64_t tl = k1 - k0;
@@ -347,8 +372,10 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
       if (iter_init(ib, ii) != R_OK) { res = MTBLX_GET_PANIC; break; }
       int r = seek(ib, ii, t, tl);                                // new_from: index_iter.seek(key)
       if (r != R_OK) { res = r == R_LOOP ? MTBLX_GET_LOOP : MTBLX_GET_PANIC; break; }
-      int b = block_at_index(f, ib, ii, db);
+      uint64_t ms = 0, ml = 0;
+      int b = block_at_index(f, ib, ii, db, ms, ml);
       if (b == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+      if (b == 3) { res = MTBLX_GET_MISSING; ro = ms; rl = ml; break; }
       if (b == 2) { res = MTBLX_GET_ERR; break; }                  // Err at open (new_get)
       if (b == 0) break;                                           // no block: next() -> None
       if (iter_init(db, di) != R_OK) { res = MTBLX_GET_PANIC; break; }
@@ -366,8 +393,9 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
       if (r == R_PANIC) { res = MTBLX_GET_PANIC; break; }
       if (r == R_LOOP) { res = MTBLX_GET_LOOP; break; }
       if (!valid(ib, ii)) break;
-      b = block_at_index(f, ib, ii, db);
+      b = block_at_index(f, ib, ii, db, ms, ml);
       if (b == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+      if (b == 3) { res = MTBLX_GET_MISSING; ro = ms; rl = ml; break; }
       if (b == 2) {
         // next() returned Some(Err(InvalidBlock)).  Reader::get matches Some(_) and returns
         // Ok(ReaderIntoGet::new(iter.bi)) with iter.bi still the OLD block iterator (it is not
@@ -386,6 +414,9 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
       if (di.voff + di.vlen > db.L) { res = MTBLX_GET_PANIC; break; }
       if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
     } while (false);
+    MTBLX_CHK(st + q, 4);
+    MTBLX_CHK(voff + q, 8);
+    MTBLX_CHK(vlen + q, 8);
     if (lane == 0) { st[q] = res; voff[q] = ro; vlen[q] = rl; }
   }
 }
@@ -427,6 +458,7 @@ __global__ void __launch_bounds__(256) k_index_seek(const uint8_t* file, uint64_
   const uint32_t waves = gridDim.x * (blockDim.x / 64);
   const FileCtx f{file, file_len, version, verify, T, lane};
   for (uint32_t q = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); q < nq; q += waves) {
+    MTBLX_CHK(qend + q, 8);
     const uint64_t k0 = q ? qend[q - 1] : 0;
     const uint8_t* t = qkeys + k0;
     const uint64_t tl = qend[q] - k0;
@@ -452,6 +484,7 @@ __global__ void __launch_bounds__(256) k_index_seek(const uint8_t* file, uint64_
       r.data_off = start;
       r.data_len = sz;
     } while (false);
+    MTBLX_CHK(out + q, sizeof(mtblx_index_seek));
     if (lane == 0) out[q] = r;
   }
 }
@@ -471,6 +504,7 @@ __device__ int wave_cmp(const uint8_t* K, uint64_t kl, const uint8_t* t, uint64_
   const uint64_t m = kl < tl ? kl : tl;
   for (uint64_t c0 = 0; c0 < m; c0 += 64) {
     const uint64_t c = c0 + (uint64_t)lane;
+    if (c < m) { MTBLX_CHK(K + c, 1); MTBLX_CHK(t + c, 1); }
     const bool diff = c < m && K[c] != t[c];
     const uint64_t bal = __ballot(diff);
     if (bal) {
@@ -499,7 +533,11 @@ __device__ __forceinline__ int s_parse(const Blk& b, SIt& it, uint8_t* K, uint64
     it.kcap = c;
   }
   if (m + ns > klim) return R_TOOLONG;
-  for (uint32_t j = (uint32_t)lane; j < ns; j += 64) K[m + j] = b.d[p + j];
+  for (uint32_t j = (uint32_t)lane; j < ns; j += 64) {
+    MTBLX_CHK(K + m + j, 1);
+    MTBLX_CHK(b.d + p + j, 1);
+    K[m + j] = b.d[p + j];
+  }
   __syncthreads();   // one-wave workgroup: orders the key writes (LDS or global) before other lanes read K
   it.klen = m + ns;
   it.has_next = true;
@@ -552,6 +590,8 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
   const uint64_t klim = GK ? kbuf_cap : kSeekKey;
   for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
     uint8_t* K = GK ? kbuf + (uint64_t)q * kbuf_cap : Klds;
+    MTBLX_CHK(qs + q, sizeof(mtblx_block_seek));
+    MTBLX_CHK(qend + q, 8);
     mtblx_block_seek Q = qs[q];
     const uint64_t k0 = q ? qend[q - 1] : 0;
     const uint8_t* t = qkeys + k0;
@@ -570,7 +610,10 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
     do {
       __syncthreads();
       if (L <= kSeekStage) {
-        for (uint64_t i = (uint64_t)lane; i < L; i += 64) stage[i] = src[i];
+        for (uint64_t i = (uint64_t)lane; i < L; i += 64) {
+          MTBLX_CHK(src + i, 1);
+          stage[i] = src[i];
+        }
         __syncthreads();
         d = stage;
       }
@@ -592,7 +635,11 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
         if (tl > klim) {
           r = R_TOOLONG;
         } else {
-          for (uint64_t j = (uint64_t)lane; j < tl; j += 64) K[j] = t[j];
+          for (uint64_t j = (uint64_t)lane; j < tl; j += 64) {
+            MTBLX_CHK(K + j, 1);
+            MTBLX_CHK(t + j, 1);
+            K[j] = t[j];
+          }
           __syncthreads();
           it.klen = tl;
           it.has_next = true;
@@ -620,7 +667,11 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
         const uint64_t kb = Q.key_bytes + it.klen, vb = Q.val_bytes + it.vlen;
         if (!ovf && (Q.nrec >= rec_cap || kb > keys_cap || vb > vals_cap)) ovf = true;
         if (!ovf) {
-          for (uint64_t j = (uint64_t)lane; j < it.klen; j += 64) kd[Q.key_bytes + j] = K[j];
+          for (uint64_t j = (uint64_t)lane; j < it.klen; j += 64) {
+            MTBLX_CHK(kd + Q.key_bytes + j, 1);
+            MTBLX_CHK(K + j, 1);
+            kd[Q.key_bytes + j] = K[j];
+          }
           uint64_t j0 = 0;
           if (it.vlen >= 4096) {   // big values (blocks >= 4 GiB hold values of GiBs): 16 B per lane
             typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -633,14 +684,31 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
             for (; c + (kU - 1) * 64 < nv; c += kU * 64) {
               v4u x[kU];
 #pragma unroll
-              for (uint32_t u = 0; u < kU; ++u) x[u] = *reinterpret_cast<const v4u*>(vs + 16 * (c + 64 * u));
+              for (uint32_t u = 0; u < kU; ++u) {
+                MTBLX_CHK(vs + 16 * (c + 64 * u), 16);
+                x[u] = *reinterpret_cast<const v4u*>(vs + 16 * (c + 64 * u));
+              }
 #pragma unroll
-              for (uint32_t u = 0; u < kU; ++u) *reinterpret_cast<v4u*>(vo + 16 * (c + 64 * u)) = x[u];
+              for (uint32_t u = 0; u < kU; ++u) {
+                MTBLX_CHK(vo + 16 * (c + 64 * u), 16);
+                *reinterpret_cast<v4u*>(vo + 16 * (c + 64 * u)) = x[u];
+              }
             }
-            for (; c < nv; c += 64) *reinterpret_cast<v4u*>(vo + 16 * c) = *reinterpret_cast<const v4u*>(vs + 16 * c);
+            for (; c < nv; c += 64) {
+              MTBLX_CHK(vo + 16 * c, 16);
+              MTBLX_CHK(vs + 16 * c, 16);
+              *reinterpret_cast<v4u*>(vo + 16 * c) = *reinterpret_cast<const v4u*>(vs + 16 * c);
+            }
             j0 = 16 * nv;
           }
-          for (uint64_t j = j0 + (uint64_t)lane; j < it.vlen; j += 64) vd[Q.val_bytes + j] = d[it.voff + j];
+          for (uint64_t j = j0 + (uint64_t)lane; j < it.vlen; j += 64) {
+            MTBLX_CHK(vd + Q.val_bytes + j, 1);
+            MTBLX_CHK(d + it.voff + j, 1);
+            vd[Q.val_bytes + j] = d[it.voff + j];
+          }
+          MTBLX_CHK(oke + (uint64_t)q * rec_cap + Q.nrec, 8);
+          MTBLX_CHK(ove + (uint64_t)q * rec_cap + Q.nrec, 8);
+          if (okcap) MTBLX_CHK(okcap + (uint64_t)q * rec_cap + Q.nrec, 8);
           if (lane == 0) {
             oke[(uint64_t)q * rec_cap + Q.nrec] = kb;
             ove[(uint64_t)q * rec_cap + Q.nrec] = vb;
@@ -662,6 +730,7 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
     Q.has_val = it.has_val ? 1 : 0;
     Q.last_voff = it.voff;
     Q.last_vlen = it.vlen;
+    MTBLX_CHK(qs + q, sizeof(mtblx_block_seek));
     if (lane == 0) qs[q] = Q;
   }
 }
@@ -709,7 +778,9 @@ __global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint
     while (ok && cur < e0) {
       uint64_t nx;
       uint32_t sh, ns;
-      if (!chain_step(b, cur, nx, sh, ns)) { ok = false; break; }
+      // a zero-progress entry (unterminated varints, ns = vl = 0) makes the interval irregular:
+      // the serial walk below stops on it (r05: this loop spun on it forever)
+      if (!chain_step(b, cur, nx, sh, ns) || nx <= cur) { ok = false; break; }
       if (c == 0 ? sh != 0 : sh > klen) kok = false;
       klen = (sh < klen ? sh : klen) + ns;
       cur = nx;
@@ -717,6 +788,7 @@ __global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint
     }
     if (!ok || cur != e0) irregular = 1;
     if (!kok) keys_irregular = 1;
+    MTBLX_CHK(scratch + r, 8);
     scratch[r] = c;
   }
   __syncthreads();
@@ -725,6 +797,7 @@ __global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint
     // exclusive scan of scratch[0..n) in chunks of blockDim.x
     for (uint32_t base = 0; base < n; base += blockDim.x) {
       const uint32_t r = base + tid;
+      if (r < n) MTBLX_CHK(scratch + r, 8);
       const uint64_t v = r < n ? scratch[r] : 0;
       uint64_t x = v;
       for (int o = 1; o < 64; o <<= 1) {
@@ -745,7 +818,7 @@ __global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint
       const uint64_t e0 = (r + 1 < n) ? restart_point(b, r + 1) : b.R;
       uint64_t i = scratch[r], cur = restart_point(b, r);
       while (cur < e0) {
-        if (i < cap) offs[i] = cur;
+        if (i < cap) { MTBLX_CHK(offs + i, 8); offs[i] = cur; }
         uint64_t nx;
         chain_step(b, cur, nx);
         cur = nx;
@@ -759,7 +832,7 @@ __global__ void __launch_bounds__(1024) k_entry_offsets(const uint8_t* blk, uint
   if (tid != 0) return;
   uint64_t i = 0, cur = restart_point(b, 0);
   while (cur < b.R) {
-    if (i < cap) offs[i] = cur;
+    if (i < cap) { MTBLX_CHK(offs + i, 8); offs[i] = cur; }
     ++i;
     uint64_t nx;
     if (!chain_step(b, cur, nx) || nx <= cur) break;
@@ -772,17 +845,18 @@ __global__ void k_key_filter(const uint8_t* keys, const uint64_t* key_end, uint6
                              uint64_t kl, unsigned long long* first_fail) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  MTBLX_CHK(key_end + i, 8);
   const uint64_t a = i ? key_end[i - 1] : 0, l = key_end[i] - a;
   const uint8_t* key = keys + a;
   const uint64_t m = l < kl ? l : kl;
   uint64_t c = 0;
-  while (c < m && key[c] == k[c]) ++c;
+  while (c < m && (MTBLX_CHK(key + c, 1), MTBLX_CHK(k + c, 1), key[c] == k[c])) ++c;
   const int cmp = (c < m) ? (key[c] < k[c] ? -1 : 1) : (l < kl ? -1 : (l > kl ? 1 : 0));
   bool fail = false;
   if (type == 1) fail = cmp != 0;
   else if (type == 2) fail = !(kl <= l && c == kl);
   else if (type == 3) fail = cmp > 0;
-  if (fail) atomicMin(first_fail, (unsigned long long)i);
+  if (fail) { MTBLX_CHK(first_fail, 8); atomicMin(first_fail, (unsigned long long)i); }
 }
 
 }  // namespace mtblx_rd
@@ -793,8 +867,8 @@ extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t 
   if (nent == 0) return MTBLX_OK;
   if (!file || !vals || !val_end || !blk_off || !blk_len || !dir_st || version > 1) return MTBLX_E_INVAL;
   const uint32_t threads = 256;
-  hipLaunchKernelGGL(mtblx_rd::k_block_dir, dim3((nent + threads - 1) / threads), dim3(threads), 0,
-                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, vals, val_end, val_base, nent,
+  MTBLX_LAUNCH((file, vals, val_end, blk_off, blk_len, dir_st), mtblx_rd::k_block_dir,
+               dim3((nent + threads - 1) / threads), dim3(threads), 0, reinterpret_cast<hipStream_t>(stream), file, file_len, version, vals, val_end, val_base, nent,
                      blk_off, blk_len, dir_st);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
@@ -812,7 +886,8 @@ extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t versio
     grid = (ncu > 0 ? ncu : 256) * 8;
   }
   const uint32_t need = (nq + 3u) / 4u;
-  hipLaunchKernelGGL(mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
+  MTBLX_LAUNCH((file, keys, key_end, status, val_off, val_len), mtblx_rd::k_get,
+               dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
                      mtblx_rd::DecTab{nullptr, nullptr, nullptr, nullptr, 0u, nullptr}, keys, key_end, nq, status,
                      val_off, val_len);
@@ -836,7 +911,8 @@ extern "C" int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, ui
     grid = (ncu > 0 ? ncu : 256) * 8;
   }
   const uint32_t need = (nq + 3u) / 4u;
-  hipLaunchKernelGGL(mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
+  MTBLX_LAUNCH((file, tab_start, tab_doff, tab_dlen, tab_st, dec, keys, key_end, status, val_off, val_len),
+               mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
                      mtblx_rd::DecTab{tab_start, tab_doff, tab_dlen, tab_st, ntab, dec}, keys, key_end, nq, status,
                      val_off, val_len);
@@ -849,7 +925,7 @@ extern "C" int mtblx_index_seek_batch(const uint8_t* file, uint64_t file_len, ui
   if (nq == 0) return MTBLX_OK;
   if (!file || !keys || !key_end || !out || version > 1) return MTBLX_E_INVAL;
   const uint32_t need = (nq + 3u) / 4u;
-  hipLaunchKernelGGL(mtblx_rd::k_index_seek, dim3(need < 2048u ? need : 2048u), dim3(256), 0,
+  MTBLX_LAUNCH((file, keys, key_end, out), mtblx_rd::k_index_seek, dim3(need < 2048u ? need : 2048u), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
                      keys, key_end, nq, out);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
@@ -861,7 +937,8 @@ extern "C" int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, 
                                       uint64_t* kcap_out, uint64_t rec_cap, void* stream) {
   if (nq == 0) return MTBLX_OK;
   if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out) return MTBLX_E_INVAL;
-  hipLaunchKernelGGL(mtblx_rd::k_block_seek<false>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
+  MTBLX_LAUNCH((data, keys, key_end, q, out_keys, out_vals, key_end_out, val_end_out, kcap_out),
+               mtblx_rd::k_block_seek<false>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
                      vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, nullptr, 0);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
@@ -876,7 +953,8 @@ extern "C" int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* k
   if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out || !key_buf ||
       key_buf_cap == 0)
     return MTBLX_E_INVAL;
-  hipLaunchKernelGGL(mtblx_rd::k_block_seek<true>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
+  MTBLX_LAUNCH((data, keys, key_end, q, out_keys, out_vals, key_end_out, val_end_out, kcap_out, key_buf),
+               mtblx_rd::k_block_seek<true>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
                      vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, key_buf, key_buf_cap);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
@@ -888,12 +966,14 @@ extern "C" int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t*
   if (len > mtblx_rd::kU32) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint64_t nr = len / 4 + 1;   // restart count bound: 4 bytes per restart point
+  // the per-interval counts: a plain allocation freed once the launch has completed (once per
+  // Reader; r05: no stream-ordered pool allocations next to the caller's caching allocator)
   uint64_t* scratch = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&scratch), nr * sizeof(uint64_t), s) != hipSuccess) return MTBLX_E_HIP;
-  hipLaunchKernelGGL(mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch,
+  if (hipMalloc(reinterpret_cast<void**>(&scratch), nr * sizeof(uint64_t)) != hipSuccess) return MTBLX_E_HIP;
+  MTBLX_LAUNCH((block, offs, count, scratch, regular), mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch,
                      regular);
-  const bool ok = hipGetLastError() == hipSuccess;
-  (void)hipFreeAsync(scratch, s);
+  const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+  (void)hipFree(scratch);
   return ok ? MTBLX_OK : MTBLX_E_HIP;
 }
 
@@ -903,7 +983,8 @@ extern "C" int mtblx_key_filter(const uint8_t* keys, const uint64_t* key_end, ui
   if (!keys || !key_end || !first_fail || (klen && !k) || type < 1 || type > 3) return MTBLX_E_INVAL;
   const uint64_t blocks = (n + 255) / 256;
   if (blocks > 0x7FFFFFFFull) return MTBLX_E_INVAL;
-  hipLaunchKernelGGL(mtblx_rd::k_key_filter, dim3((uint32_t)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  MTBLX_LAUNCH((keys, key_end, k, first_fail), mtblx_rd::k_key_filter, dim3((uint32_t)blocks), dim3(256), 0,
+               reinterpret_cast<hipStream_t>(stream),
                      keys, key_end, n, type, k, klen, reinterpret_cast<unsigned long long*>(first_fail));
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

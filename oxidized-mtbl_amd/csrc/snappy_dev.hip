@@ -39,6 +39,7 @@
 #include <string.h>
 #include <utility>
 
+#include "bounds.h"
 #include "mtblx.h"
 
 // timing ablations (wrong output by construction): diagnostic targets only (-DMTBLX_DIAG)
@@ -401,12 +402,15 @@ __global__ void __launch_bounds__(C::WAVES * kWave) k_snappy_blocks(const uint8_
   if (b >= nblk) return;
   const uint8_t* s = src + src_off[b];
   uint32_t n = src_len[b];
+  if (n) MTBLX_CHK(s, n);
   Window<C> pf;
   pf.load(s, n, 0, lane);
   for (; b < nblk; b += nw) {
     const uint32_t b2 = b + nw;
     const uint8_t* s2 = b2 < nblk ? src + src_off[b2] : s;
     const uint32_t n2 = b2 < nblk ? src_len[b2] : 0u;
+    if (n2) MTBLX_CHK(s2, n2);
+    if (dst_len[b]) MTBLX_CHK(dst + dst_off[b], dst_len[b]);
     snap_block<C>(S[wv], pf, s, n, s2, n2, dst + dst_off[b], dst_len[b], lane, status + b,
                   dec_len ? dec_len + b : nullptr);
     s = s2;
@@ -464,6 +468,8 @@ __device__ __forceinline__ Meta load_meta(uint32_t b, uint32_t nblk, const uint8
     m.n = src_len[b];
     m.dg = dst + dst_off[b];
     m.cap = dst_len[b];
+    if (m.n) MTBLX_CHK(m.s, m.n);
+    if (m.cap) MTBLX_CHK(m.dg, m.cap);
   }
   return m;
 }
@@ -671,6 +677,8 @@ __global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, c
       m &= m - 1ull;
       const uint8_t* s = src + src_off[b];
       const uint32_t n = src_len[b];
+      if (n) MTBLX_CHK(s, n);
+      if (dst_len[b]) MTBLX_CHK(dst + dst_off[b], dst_len[b]);
       Window<Large> pf;
       pf.load(s, n, 0, lane);
       snap_block<Large>(SL, pf, s, n, s, 0u, dst + dst_off[b], dst_len[b], lane, status + b,
@@ -727,9 +735,10 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t r)
 // and shifted down by r = p + 16 - n bytes: one load and a funnel shift instead of 16 byte
 // loads (a wave has some lane near its stream's end in most iterations).
 __device__ __forceinline__ Q4 ld16(const uint8_t* s, uint32_t n, uint32_t p) {
-  if ((uint64_t)p + 16u <= n) return q4(*reinterpret_cast<const v4u*>(s + p));
+  if ((uint64_t)p + 16u <= n) return MTBLX_CHK(s + p, 16), q4(*reinterpret_cast<const v4u*>(s + p));
   Q4 q{{0u, 0u, 0u, 0u}};
   if (n >= 16u) {
+    MTBLX_CHK(s + n - 16u, 16);
     const Q4 x = q4(*reinterpret_cast<const v4u*>(s + n - 16u));
     const uint32_t r = p >= n ? 16u : p + 16u - n, rq = r >> 2, rb = r & 3u;   // r in [1, 16]
     uint32_t y[6];
@@ -759,6 +768,7 @@ __device__ __forceinline__ void st16(uint8_t* dg, uint32_t o, const Q4& v, uint3
   return;
 #endif
   if ((uint64_t)o + 16u <= cap) {
+    MTBLX_CHK(dg + o, 16);
     *reinterpret_cast<v4u*>(dg + o) = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
   } else {
 #pragma unroll
@@ -814,6 +824,7 @@ __device__ __forceinline__ Q4 ring_get(const uint32_t (*R)[kThreads], int t, uin
 // from dpos / fpos covers every ring write / read issued before it.  Short literals come from the
 // register window (48 bytes: two in use, the third loaded 16 bytes ahead).
 constexpr uint32_t kRun = 0xFFFFFFFFu;   // dend while the decoder runs
+constexpr uint32_t kGone = 0xFFFFFFFEu;  // dend after the writer gave up (it won the CAS from kRun)
 #ifndef MTBLX_SNAP_WSLEEP
 #define MTBLX_SNAP_WSLEEP 8   // writer's idle sleep, x 64 cycles
 #endif
@@ -821,7 +832,6 @@ constexpr uint64_t kSpinTicks = 2ull * 100000000ull;   // 2 s of s_memrealtime: 
 
 struct LaneSync {
   uint32_t dpos[kThreads], fpos[kThreads], fvis[kThreads], dend[kThreads];
-  uint32_t gone[kThreads];   // the writer gave up (2 s without its decoder publishing anything)
 };
 
 __device__ __forceinline__ uint32_t vld(const uint32_t* p) { return *reinterpret_cast<const volatile uint32_t*>(p); }
@@ -875,7 +885,6 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
     Y.fpos[t] = 0;
     Y.fvis[t] = 0;
     Y.dend[t] = act ? kRun : 0u;
-    Y.gone[t] = 0u;
   }
   __syncthreads();
   if (b >= nblk) return;
@@ -916,10 +925,13 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
           if (t0 == 0) t0 = now;
           // 2 s without a chunk or the end from ITS decoder (which publishes dend as soon as its
           // own block is done, not when the wave is): leave, and say so -- the decoder then
-          // reports MTBLX_SNAPPY_TIMEOUT instead of OK for a block whose bytes were not all stored
+          // reports MTBLX_SNAPPY_TIMEOUT instead of OK for a block whose bytes were not all stored.
+          // One CAS on dend decides between giving up and the decoder's end (a plain
+          // flag could be set after the decoder had already published OK, truncating silently):
+          // if the decoder published first, the loop goes on and stores the block's tail.
           if (now - t0 > kSpinTicks) {
-            vst(&Y.gone[t], 1u);
-            break;
+            if (atomicCAS(&Y.dend[t], kRun, kGone) == kRun) break;
+            t0 = 0;
           }
         }
       }
@@ -932,6 +944,8 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
   const uint8_t* s = src + src_off[b];
   const uint32_t n = src_len[b];
   const uint32_t cap = dst_len[b];
+  if (n) MTBLX_CHK(s, n);
+  if (cap) MTBLX_CHK(dg, cap);
   uint64_t want = 0;
   uint32_t pos = 0;
   bool term = false;
@@ -1039,9 +1053,10 @@ __global__ void __launch_bounds__(2 * kThreads) k_snappy_lanes(const uint8_t* sr
   // looping for its other lanes, possibly for long, and the writer must not wait for them
   bool published = false;
   auto publish = [&]() {
-    if (hang || vld(&Y.gone[t])) st = MTBLX_SNAPPY_TIMEOUT;   // an internal wait gave up: not CORRUPT
+    if (hang) st = MTBLX_SNAPPY_TIMEOUT;   // an internal wait gave up: not CORRUPT
     if (st == MTBLX_SNAPPY_OK && d != W) st = MTBLX_SNAPPY_CORRUPT;
-    vst(&Y.dend[t], st == MTBLX_SNAPPY_OK ? d : 0u);
+    // the writer's give-up and this end race for dend: whoever moves it off kRun decides
+    if (atomicCAS(&Y.dend[t], kRun, st == MTBLX_SNAPPY_OK ? d : 0u) != kRun) st = MTBLX_SNAPPY_TIMEOUT;
     published = true;
   };
   while (__ballot(!fin)) {
@@ -1225,6 +1240,8 @@ __global__ void __launch_bounds__(kParseThreads) k_snappy_parse(const uint8_t* s
   const uint8_t* s = src + src_off[b];
   const uint32_t n = src_len[b], cap = dst_len[b];
   uint8_t* dg = dst + dst_off[b];
+  if (n) MTBLX_CHK(s, n);
+  if (cap) MTBLX_CHK(dg, cap);
   // the quad kernel already read the preamble: it is valid and fits the slot (else not marked)
   uint64_t want = 0;
   uint32_t pos = 0;
@@ -1319,6 +1336,7 @@ __global__ void __launch_bounds__(kWave) k_snappy_exec(const uint8_t* src, const
     const uint8_t* s = on ? src + src_off[b] : src;
     const uint32_t n = on ? src_len[b] : 0u;
     uint8_t* dg = on ? dst + dst_off[b] : dst;
+    if (n) MTBLX_CHK(s, n);
     const int32_t wb = -(int32_t)((uintptr_t)s & 15u);
     const uint32_t span = n + (uint32_t)(-wb);
     const uint32_t nch = on ? (span + 15u) / 16u : 0u;
@@ -1461,6 +1479,7 @@ __global__ void __launch_bounds__(kDirThreads) k_snap_len(const uint8_t* src, co
     const uint32_t b = b0 + j;
     if (b >= nblk) break;
     bool ok = false;
+    if (src_len[b]) MTBLX_CHK(src + src_off[b], src_len[b] < 5u ? src_len[b] : 5u);
     const uint32_t u = preamble(src + src_off[b], src_len[b], ok);
     dst_len[b] = u;
     status[b] = ok ? MTBLX_SNAPPY_OK : MTBLX_SNAPPY_CORRUPT;
@@ -1539,10 +1558,10 @@ extern "C" int mtblx_snappy_dir(const uint8_t* src, const uint64_t* src_off, con
   if (nblk == 0) return MTBLX_OK;
   const uint32_t nwg = (nblk + kDirSpan - 1) / kDirSpan;
   uint64_t* wsum = reinterpret_cast<uint64_t*>(workspace);
-  hipLaunchKernelGGL(k_snap_len, dim3(nwg), dim3(kDirThreads), 0, s, src, src_off, src_len, nblk, dst_len, status,
+  MTBLX_LAUNCH((src, src_off, src_len, dst_len, status, wsum, totals), k_snap_len, dim3(nwg), dim3(kDirThreads), 0, s, src, src_off, src_len, nblk, dst_len, status,
                      wsum, totals);
-  hipLaunchKernelGGL(k_snap_scan, dim3(1), dim3(kDirThreads), 0, s, wsum, nwg, totals);
-  hipLaunchKernelGGL(k_snap_off, dim3(nwg), dim3(kDirThreads), 0, s, dst_len, nblk, wsum, dst_off);
+  MTBLX_LAUNCH((wsum, totals), k_snap_scan, dim3(1), dim3(kDirThreads), 0, s, wsum, nwg, totals);
+  MTBLX_LAUNCH((dst_len, wsum, dst_off), k_snap_off, dim3(nwg), dim3(kDirThreads), 0, s, dst_len, nblk, wsum, dst_off);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
 
@@ -1566,30 +1585,30 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   const bool two_pass = mode == 3 || (mode == 0 && MTBLX_SNAPPY_TWO_DEFAULT);
   const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(2 * lanes::kThreads);
   if (mode == 2) {
-    hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
+    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
                        status, dec_len, 0);
   } else if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
     // k_snappy_lanes costs about one block's serial decode however many blocks run (all are in
     // flight), the quads ~0.19 ms per round of 8 192 blocks: the lanes win from ~50 000 blocks
     // (25 000 compressible blocks: quads 0.66 ms, lanes ~1.0 ms; 100 000: 2.33 vs 1.24 ms)
     const uint32_t lanes_x = ((mode == 0 && nblk >= kLanesMinBlocks) || mode == 3) ? 2u : 0u;
-    hipLaunchKernelGGL(quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
+    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len, lanes_x);
     if (lanes_x && two_pass) {
-      hipLaunchKernelGGL(two::k_snappy_parse, dim3((nblk + two::kParseThreads - 1) / two::kParseThreads),
+      MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), two::k_snappy_parse, dim3((nblk + two::kParseThreads - 1) / two::kParseThreads),
                          dim3(two::kParseThreads), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len,
                          status, dec_len);
-      hipLaunchKernelGGL(two::k_snappy_exec, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
+      MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, status, dec_len), two::k_snappy_exec, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                          dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, status, dec_len);
     } else if (lanes_x) {
-      hipLaunchKernelGGL(lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
+      MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
                          dst_len, status, dec_len, 1);
     }
-    hipLaunchKernelGGL(quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
+    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
                        src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   } else {
-    hipLaunchKernelGGL(k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,
+    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,
                        src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   }
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;

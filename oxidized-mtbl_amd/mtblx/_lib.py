@@ -19,10 +19,10 @@ i32p = C.POINTER(C.c_int32)
 
 MTBLX_OK, MTBLX_E_INVAL, MTBLX_E_HIP, MTBLX_E_NODEV, MTBLX_E_FORMAT, MTBLX_E_TIMEOUT, MTBLX_E_IO = 0, -1, -2, -3, -4, -5, -6
 ST_OK, ST_INVALID_BLOCK, ST_CORRUPT, ST_LOOP, ST_UNSUPPORTED, ST_OVERFLOW, ST_DECOMPRESS = range(7)
-SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL = range(3)
+SNAPPY_OK, SNAPPY_CORRUPT, SNAPPY_TOO_SMALL, SNAPPY_TIMEOUT = range(4)
 CODEC_OK, CODEC_CORRUPT, CODEC_UNSUPPORTED = range(3)
 DIR_OK, DIR_PANIC, DIR_UNSUPPORTED = range(3)
-GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP = range(5)
+GET_FOUND, GET_NONE, GET_PANIC, GET_ERR, GET_LOOP, GET_MISSING = range(6)
 SEEK_OK, SEEK_ERR, SEEK_PANIC, SEEK_LOOP, SEEK_UNSUPPORTED = range(5)
 EMIT_END, EMIT_PANIC, EMIT_LOOP, EMIT_MAX, EMIT_OVERFLOW = range(5)
 

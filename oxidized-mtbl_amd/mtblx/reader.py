@@ -424,6 +424,37 @@ class Reader:
                           t(zst[order], np.int32), int(order.size), torch.from_numpy(buf).to(dev))
         return self._dtab
 
+    def _dtab_add(self, starts, sizes):
+        """decompress stored blocks [start, + size) the table lacks (a get_batch seek landed on
+        them: MTBLX_GET_MISSING) and add them to the table"""
+        ts, tdo, tdl, tst, n, dec = self._dec_table()
+        L = _lib.lib()
+        parts, base = [], int(dec.numel())
+        s0, o0, l0, z0 = [], [], [], []
+        for a, n_ in zip(starts, sizes):
+            raw = self.file[int(a): int(a) + int(n_)].cpu().numpy()
+            out = _lib.u8p()
+            un = C.c_uint64(0)
+            src = raw if raw.size else np.zeros(1, np.uint8)
+            ok = L.mtblx_decompress(self.compression, src.ctypes.data, raw.size, C.byref(out), C.byref(un)) == 0
+            b = np.empty(int(un.value) if ok else 0, np.uint8)
+            if ok:
+                C.memmove(b.ctypes.data, out, int(un.value))
+                L.mtblx_free(out)
+            s0.append(int(a)); o0.append(base); l0.append(b.size); z0.append(0 if ok else 1)
+            parts.append(b)
+            base += b.size
+        dev = self.file.device
+        start = np.concatenate([ts.cpu().numpy(), np.array(s0, np.int64)])
+        doff = np.concatenate([tdo.cpu().numpy(), np.array(o0, np.int64)])
+        dlen = np.concatenate([tdl.cpu().numpy(), np.array(l0, np.int64)])
+        zst = np.concatenate([tst.cpu().numpy(), np.array(z0, np.int32)])
+        order = np.argsort(start, kind="stable")
+        t = lambda a_: torch.from_numpy(np.ascontiguousarray(a_)).to(dev)
+        extra = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, np.uint8)).to(dev)
+        self._dtab = (t(start[order]), t(doff[order]), t(dlen[order]), t(zst[order]), int(order.size),
+                      torch.cat([dec, extra]))
+
     @property
     def value_source(self):
         """the device bytes get_batch's val_off / val_len point into: the file, or for a
@@ -453,13 +484,26 @@ class Reader:
                                       C.c_void_p(vo.data_ptr()), C.c_void_p(vl.data_ptr()),
                                       C.c_void_p(codec._stream_handle(stream)))
         else:
-            ts, tdo, tdl, tst, ntab, dec = self._dec_table()
-            rc = _lib.lib().mtblx_get_decompressed(
-                C.c_void_p(self.file.data_ptr()), self.len, self.version, 1 if self.verify else 0, self.index_off,
-                self.index_len, C.c_void_p(ts.data_ptr()), C.c_void_p(tdo.data_ptr()), C.c_void_p(tdl.data_ptr()),
-                C.c_void_p(tst.data_ptr()), ntab, C.c_void_p(dec.data_ptr()), C.c_void_p(kb.data_ptr()),
-                C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()), C.c_void_p(vo.data_ptr()),
-                C.c_void_p(vl.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
+            # a lookup that reaches a stored block the table lacks (MTBLX_GET_MISSING: only a
+            # corrupt index read with verification off leads there) gets that block decompressed
+            # and added, and the batch runs again; every round adds a block, so this ends
+            for _ in range(1 + 4096):
+                ts, tdo, tdl, tst, ntab, dec = self._dec_table()
+                rc = _lib.lib().mtblx_get_decompressed(
+                    C.c_void_p(self.file.data_ptr()), self.len, self.version, 1 if self.verify else 0,
+                    self.index_off, self.index_len, C.c_void_p(ts.data_ptr()), C.c_void_p(tdo.data_ptr()),
+                    C.c_void_p(tdl.data_ptr()), C.c_void_p(tst.data_ptr()), ntab, C.c_void_p(dec.data_ptr()),
+                    C.c_void_p(kb.data_ptr()), C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()),
+                    C.c_void_p(vo.data_ptr()), C.c_void_p(vl.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
+                if rc != 0 or nq == 0:
+                    break
+                miss = (st[:nq] == _lib.GET_MISSING).cpu().numpy()
+                if not miss.any():
+                    break
+                pairs = sorted(set(zip(vo[:nq].cpu().numpy()[miss].tolist(), vl[:nq].cpu().numpy()[miss].tolist())))
+                self._dtab_add([a for a, _ in pairs], [b for _, b in pairs])
+            else:
+                raise RuntimeError("get_batch: missing blocks did not converge")
         if rc != 0:
             raise RuntimeError(f"mtblx_get failed: {rc}")
         return st[:nq], vo[:nq], vl[:nq]

@@ -36,3 +36,29 @@ def _sync_after_gpu_test(request):
     import torch
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         torch.cuda.synchronize()
+    if os.environ.get("MTBLX_BOUNDS_CHECK") and "mtblx" in sys.modules:
+        _bounds_check(request)
+
+
+_bounds_seen = [0]
+
+
+def _bounds_check(request):
+    """the bounds-checked diagnostic library (oxidized-mtbl_amd/csrc/bounds.h, MTBLX_LIB pointing
+    at build/libmtblx_bounds.so): fail the test whose launches touched memory outside their
+    argument allocations, or faulted"""
+    import ctypes as C
+    import mtblx
+    lib = mtblx.lib()
+    fn = getattr(lib, "mtblx_bounds_report", None)
+    if fn is None:
+        return
+    fn.restype = C.c_longlong
+    fn.argtypes = [C.c_char_p, C.c_size_t]
+    buf = C.create_string_buffer(512)
+    n = int(fn(buf, 512))
+    assert n >= 0, "MTBLX_BOUNDS_CHECK is set but the loaded library is not the bounds-checked build"
+    if n != _bounds_seen[0]:
+        _bounds_seen[0] = n
+        pytest.fail(f"bounds-checked build: {n & 0xFFFFFFFF} out-of-allocation accesses, {n >> 32} faults "
+                    f"so far; first: {buf.value.decode()}")

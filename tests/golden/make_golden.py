@@ -144,6 +144,113 @@ SEEK_KAT = {
 }
 
 
+# --- BlockBuilder's restart cadence and multi-byte varint headers, hand-derived ---
+# One data block of 33 records at restart interval 16 (src/block_builder.rs:49-83): entries 0, 16
+# and 32 start a restart (counter == interval -> push buf.len(), counter = 0, shared = 0,
+# :56-62); every other entry shares the 4-byte prefix "kat-" with its predecessor.
+#   key_i   = "kat-" + chr(0x41 + i)            (5 B; 'A' .. 'a')
+#   key_20  = "kat-U" + "x" * 130               (135 B: non_shared 131 -> 2-byte varint 83 01)
+#   value_i = chr(0x30 + i % 10) * (i % 4)      (0..3 B)
+#   value_10 = 0xa5 * 16500                     (value_length 16500 -> 3-byte varint f4 80 01)
+# Entry sizes (header + non_shared + value_length):
+#   restart entries 0, 16, 32: header 00 05 00, 5 key bytes, no value    -> 8
+#   entry i (other):           header 04 01 0v, 1 key byte, v = i % 4     -> 4 + i % 4
+#   entry 10:                  header 04 01 f4 80 01, 1 key byte, 16500 B -> 16506
+#   entry 20:                  header 04 83 01 00, 131 key bytes         -> 135
+#   restart[1] = 8 + (5+6+7+4+5+6+7+4+5 +7+4+5+6+7 = 78) + 16506          = 16592
+#   restart[2] = 16592 + 8 + (5+6+7 +5+6+7+4+5+6+7+4+5+6+7 = 80) + 135     = 16815
+#   buf = 16815 + 8 = 16823; finish (:85-104): u32 LE 0, 16592, 16815 and n = 3 -> L = 16839
+# write_block (src/writer.rs:203-237): varint64(16839) = c7 83 01 (16384 + 3*128 + 71), crc32c,
+# content -> 3 + 4 + 16839 = 16846 B.  Writer::into_inner: one index entry, key = the last key
+# "kat-a" (no separator: nothing follows, :158-162), value varint64(0) = 00 ->
+# content 000501 6b61742d61 00 | 00000000 | 01000000 (17 B), frame 11 + crc + content = 22 B.
+# Footer (src/metadata.rs:61-79): {16846, 65536, 0, 33, 1, 16846, 22, 295, 16546}, magic at 508.
+# bytes_keys = 32 * 5 + 135 = 295; bytes_values = sum(i % 4, i != 10) + 16500 = 46 + 16500.
+RESTART_KAT = {
+    "block_size": 65536, "restart_interval": 16, "n": 33,
+    "headers": {"restart": "000500", "regular": "0401", "e10": "0401f48001", "e20": "04830100"},
+    "restarts": [0, 16592, 16815],
+    "content_len": 16839,
+    "len_varint": "c78301",
+    "data_frame_len": 16846,
+    "index_block_content": "0005016b61742d61000000000001000000",
+    "file_len": 17380,
+    "metadata": [16846, 65536, 0, 33, 1, 16846, 22, 295, 16546],
+    # computed from the bytes above by this file's own bitwise CRC-32C / hashlib (restart_kat_bytes)
+    "data_block_crc": "3b89ccac",
+    "index_block_crc": "64ce6dc3",
+    "content_sha256": "db586532e85ed44fa77874c1d369a35daba9ef12fc795f16fef6d9255d7f9792",
+    "sha256": "12ed53a371c51f15a4a8a3876251b27790de6d38683816ab2bf9ec2a555119ec",
+}
+
+
+def restart_kat_records():
+    recs = []
+    for i in range(33):
+        k = b"kat-" + bytes([0x41 + i]) + (b"x" * 130 if i == 20 else b"")
+        v = b"\xa5" * 16500 if i == 10 else bytes([0x30 + i % 10]) * (i % 4)
+        recs.append((k, v))
+    return recs
+
+
+def crc32c_bitwise(b: bytes) -> int:
+    """CRC-32C (Castagnoli, reflected 0x82F63B78, init / xorout 0xFFFFFFFF), bit by bit"""
+    c = 0xFFFFFFFF
+    for x in b:
+        c ^= x
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 if c & 1 else 0)
+    return c ^ 0xFFFFFFFF
+
+
+def restart_kat_bytes():
+    """assemble the RESTART_KAT block and file from the hand-derived pieces (no oracle)"""
+    k = RESTART_KAT
+    h = k["headers"]
+    buf = b""
+    starts = []
+    for i, (key, val) in enumerate(restart_kat_records()):
+        starts.append(len(buf))
+        if i % 16 == 0:
+            buf += bytes.fromhex(h["restart"]) + key
+        elif i == 10:
+            buf += bytes.fromhex(h["e10"]) + key[4:] + val
+        elif i == 20:
+            buf += bytes.fromhex(h["e20"]) + key[4:] + val
+        else:
+            buf += bytes.fromhex(h["regular"]) + bytes([i % 4]) + key[4:] + val
+    assert [starts[0], starts[16], starts[32]] == k["restarts"]
+    content = buf + b"".join(r.to_bytes(4, "little") for r in k["restarts"]) + (3).to_bytes(4, "little")
+    assert len(content) == k["content_len"]
+    crc = crc32c_bitwise(content)
+    frame = bytes.fromhex(k["len_varint"]) + crc.to_bytes(4, "little") + content
+    assert len(frame) == k["data_frame_len"]
+    idx = bytes.fromhex(k["index_block_content"])
+    icrc = crc32c_bitwise(idx)
+    footer = b"".join(m.to_bytes(8, "little") for m in k["metadata"])
+    f = frame + bytes([len(idx)]) + icrc.to_bytes(4, "little") + idx + footer + b"\0" * (508 - len(footer)) + \
+        (0x4D54424C).to_bytes(4, "little")
+    assert len(f) == k["file_len"]
+    return content, crc, idx, icrc, f
+
+
+def check_restart_kat():
+    """the hand-assembled bytes carry the recorded checksums / digests, and the oracle Writer and
+    block decoder agree with them"""
+    import pyoracle as o
+    k = RESTART_KAT
+    assert crc32c_bitwise(b"123456789") == int(KAT["crc32c_check"]["crc"], 16)
+    content, crc, idx, icrc, f = restart_kat_bytes()
+    assert f"{crc:08x}" == k["data_block_crc"] and f"{icrc:08x}" == k["index_block_crc"], (hex(crc), hex(icrc))
+    assert hashlib.sha256(content).hexdigest() == k["content_sha256"]
+    assert hashlib.sha256(f).hexdigest() == k["sha256"]
+    recs = restart_kat_records()
+    assert o.write_file(recs, k["block_size"], k["restart_interval"]) == f
+    st, got = o.decode_block(content)
+    assert st == 0 and got == recs
+    return f
+
+
 def seek_kat_records():
     v = SEEK_KAT["value_len"]
     return [(k.encode(), bytes([0x41 + i]) * v) for i, k in enumerate(SEEK_KAT["keys"])]
@@ -205,7 +312,9 @@ def main():
     one, empty = build_files()
     check(one, empty)
     one1, empty1 = check_v1(one, empty)
+    rk = check_restart_kat()
     if "--check" in sys.argv:
+        assert open(os.path.join(HERE, "restart_kat.mtbl"), "rb").read() == rk
         assert open(os.path.join(HERE, "one_key.mtbl"), "rb").read() == one
         assert open(os.path.join(HERE, "empty.mtbl"), "rb").read() == empty
         assert open(os.path.join(HERE, "one_key_v1.mtbl"), "rb").read() == one1
@@ -216,7 +325,8 @@ def main():
     open(os.path.join(HERE, "empty.mtbl"), "wb").write(empty)
     open(os.path.join(HERE, "one_key_v1.mtbl"), "wb").write(one1)
     open(os.path.join(HERE, "empty_v1.mtbl"), "wb").write(empty1)
-    json.dump(dict(KAT, seek_kat=SEEK_KAT), open(os.path.join(HERE, "kat.json"), "w"), indent=1)
+    open(os.path.join(HERE, "restart_kat.mtbl"), "wb").write(rk)
+    json.dump(dict(KAT, seek_kat=SEEK_KAT, restart_kat=RESTART_KAT), open(os.path.join(HERE, "kat.json"), "w"), indent=1)
     json.dump(QUIRKS, open(os.path.join(HERE, "quirk_blocks.json"), "w"), indent=1)
     print("wrote tests/golden/{one_key,empty}{,_v1}.mtbl, kat.json, quirk_blocks.json")
 

@@ -46,6 +46,34 @@ def test_kat_block_contents(oracle):
     assert oracle.crc32c(bytes.fromhex(k["data_block_content"])) == int(k["data_block_crc"], 16)
 
 
+def test_restart_kat_hand_derived(oracle):
+    """BlockBuilder's restart cadence (entries 0 / 16 / 32 restart with
+    shared = 0, src/block_builder.rs:56-62), finish's three-entry restart array (:85-104), a
+    2-byte non_shared varint and a 3-byte value_length varint (:69-73), pinned by the bytes
+    tests/golden/make_golden.py assembles from hand-derived headers and offsets (no oracle)"""
+    k = kat()["restart_kat"]
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_golden
+    recs = make_golden.restart_kat_records()
+    f = oracle.write_file(recs, k["block_size"], k["restart_interval"])
+    assert len(f) == k["file_len"] and hashlib.sha256(f).hexdigest() == k["sha256"]
+    assert f == open(os.path.join(GOLD, "restart_kat.mtbl"), "rb").read()
+    assert f[:3].hex() == k["len_varint"] and f[3:7] == bytes.fromhex(k["data_block_crc"])[::-1]
+    content = f[7: 7 + k["content_len"]]
+    assert hashlib.sha256(content).hexdigest() == k["content_sha256"]
+    n = int.from_bytes(content[-4:], "little")
+    R = len(content) - 4 * (n + 1)
+    assert [int.from_bytes(content[R + 4 * i: R + 4 * i + 4], "little") for i in range(n)] == k["restarts"]
+    for i, hx in ((0, k["headers"]["restart"]), (16, k["headers"]["restart"]), (32, k["headers"]["restart"])):
+        p = k["restarts"][i // 16]
+        assert content[p: p + 3].hex() == hx
+    st, got = oracle.decode_block(content)
+    assert st == 0 and got == recs
+    r = oracle.file_scan(f)
+    assert r["end"] == oracle.END_NONE and r["records"] == recs and r["meta"] == k["metadata"]
+
+
 @pytest.mark.parametrize("name,block,exp", corpus.quirk_blocks(), ids=[q[0] for q in corpus.quirk_blocks()])
 def test_quirk_blocks_hand_derived(oracle, name, block, exp):
     st, recs = oracle.decode_block(block)

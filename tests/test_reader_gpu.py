@@ -165,6 +165,63 @@ def test_get_batch_compressed(oracle, comp):
                 _check_get(oracle, bytes(d), qs[:60] + [keys[-1]], verify=verify)
 
 
+def _index_entry_offsets(data: bytes):
+    """(content start, entry offsets, restart points) of a V2 file's index block, every header a
+    1-byte varint triple (host walk for building corrupt files)"""
+    meta0 = int.from_bytes(data[-512:-504], "little")
+    p, ln, sh = meta0, 0, 0
+    while True:
+        b = data[p]
+        ln |= (b & 0x7F) << sh
+        p += 1
+        sh += 7
+        if b < 0x80:
+            break
+    c0 = p + 4
+    content = data[c0: c0 + ln]
+    n = int.from_bytes(content[-4:], "little")
+    R = ln - 4 * (n + 1)
+    restarts = [int.from_bytes(content[R + 4 * i: R + 4 * i + 4], "little") for i in range(n)]
+    offs, q = [], restarts[0]
+    while q < R:
+        offs.append(q)
+        assert content[q] < 128 and content[q + 1] < 128 and content[q + 2] < 128
+        q += 3 + content[q + 1] + content[q + 2]
+    return c0, offs, restarts
+
+
+@pytest.mark.parametrize("comp", [1, 2, 5])
+def test_get_batch_compressed_seek_past_linear_walk(oracle, comp):
+    """on a compressed file whose index is corrupt mid-chain (read with
+    verification off), the linear walk of the index (the directory, mtblx_block_dir) stops at
+    the corrupt entry, while Reader::get's index seek jumps over it through later restart
+    points and lands on blocks the walk never reached.  The reference reads, decompresses and
+    scans those blocks (src/reader.rs:111-122, :140-172); mtblx_get_decompressed reports them
+    MTBLX_GET_MISSING and get_batch decompresses them and runs the batch again -- the results
+    equal the oracle's, where the earlier library answered Err(Io)."""
+    rng = np.random.default_rng(90 + comp)
+    from mtblx.writer import Writer
+    recs = corpus.random_records(rng, 3000, 8, 40, 40, 120)
+    w = Writer(1024, 16, comp)
+    for k, v in recs:
+        w.insert(k, v)
+    data = w.into_inner()
+    c0, offs, restarts = _index_entry_offsets(data)
+    assert len(restarts) >= 4
+    bad_entry = offs.index(restarts[1]) + 3               # inside the second restart interval
+    d = bytearray(data)
+    d[c0 + offs[bad_entry]] = 0x7F                        # shared 127 > the key Vec's capacity: panic
+    keys = [k for k, _ in recs]
+    qs = [keys[int(i)] for i in rng.integers(0, len(keys), 150)] + [keys[-1], keys[0], keys[-1] + b"\x01"]
+    rd = _reader()
+    r = rd.ReaderBuilder().verify_checksums(False).read(bytes(d))
+    ntab0 = r._dec_table()[4]
+    assert ntab0 <= bad_entry                              # the linear walk stopped at the corruption
+    _check_get(oracle, bytes(d), qs, verify=False)
+    r.get_batch(qs)
+    assert r._dec_table()[4] > ntab0                       # blocks past the corruption were added
+
+
 def test_get_stale_value_when_next_block_invalid(oracle):
     """ADVICE r1: Reader::get whose seek runs past a block while the NEXT block fails Block::init
     returns Ok(Some(value of the last entry the seek parsed in the old block)) -- the crate's

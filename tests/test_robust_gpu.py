@@ -93,6 +93,42 @@ def test_window_past_buffer_is_corrupt(oracle):
         assert vbad.cpu().numpy()[nb - 1:].tolist() == [1, 1]
 
 
+def test_fused_verify_window_far_past_buffer(oracle):
+    """r05: the fused verify kernels read a block's stored checksum (the u32 before its content)
+    from HBM.  For a window starting far past the buffer -- a corrupt index read with
+    verification off points a block anywhere -- that read went to data + off - 4 unguarded (an
+    access tens of MiB or a TiB past the allocation).  Every verify path must flag such blocks
+    bad, decode them CORRUPT and read nothing outside the buffer; in-buffer blocks of the same
+    tiles stay exact.  PipeSmallV (4 KiB blocks) and PipeLargeV (64 KiB blocks)."""
+    codec = _codec()
+    import torch
+    from mtblx import synth
+    for bs, nblk in ((4096, 300), (65536, 60)):
+        data, off, ln = synth.cfg2_file(nblk, block_size=bs)
+        n = off.size
+        far = [len(data) + (8 << 20), 1 << 40, (1 << 40) + 4]
+        o2 = off.astype(np.uint64).copy()
+        l2 = ln.astype(np.uint32).copy()
+        idx = [5, n // 2, n - 1]
+        for i, f in zip(idx, far):
+            o2[i] = f
+        batch = codec.DeviceBatch.from_host(data, o2, l2)
+        for fused in (True, False):
+            out, crc, bad = codec.decode_verify(batch, framed=True, fused=fused)
+            torch.cuda.synchronize()
+            dev = out.to_host()
+            b = bad.cpu().numpy()
+            assert sorted(np.nonzero(b)[0].tolist()) == idx, (bs, fused)
+            assert all(dev.status[i] == 2 and dev.nrec[i] == 0 for i in idx)
+            keep = [i for i in range(n) if i not in idx]
+            orc = oracle.decode_blocks(data, off[keep], ln[keep])
+            assert np.array_equal(dev.status[keep], orc.status) and np.array_equal(dev.nrec[keep], orc.nrec)
+            assert np.array_equal(dev.keys, orc.keys) and np.array_equal(dev.vals, orc.vals)
+            got = crc.cpu().numpy().view(np.uint32)[keep]
+            exp = np.array([oracle.crc32c(bytes(data[int(off[i]): int(off[i]) + int(ln[i])])) for i in keep], np.uint32)
+            assert np.array_equal(got, exp)
+
+
 def test_lookback_timeout_rejected_everywhere(oracle, monkeypatch, tmp_path):
     """no API hands back records from a launch whose look-back timed out."""
     codec = _codec()

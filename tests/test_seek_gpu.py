@@ -398,3 +398,26 @@ def test_keys_over_64kib(oracle):
         keys = _probe_keys(rng, recs, 6)
         ops = [("seek", keys[1]), 3, ("seek", keys[2]), 5, ("seek", keys[0]), 40]
         _script_check(oracle, bad, False, "iter", b"", b"", ops)
+
+
+def test_entry_offsets_zero_progress_entry():
+    """r05: mtblx_entry_offsets' parallel pass walked each restart interval with no progress
+    check, so an entry that does not advance (unterminated varints with non_shared = value_length
+    = 0: the reference's next() yields it forever) spun one thread forever.  Such an interval is
+    irregular now and the serial walk stops on the entry: offsets [0, 5], count 2, not regular."""
+    _mods()
+    import ctypes as C
+
+    import torch
+    from mtblx import _lib, codec
+    blk = bytes.fromhex("0001014142" "8080808080" "00000000" "05000000" "02000000")
+    d = torch.frombuffer(bytearray(blk), dtype=torch.uint8).to("cuda")
+    offs = torch.full((16,), -1, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    reg = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    rc = _lib.lib().mtblx_entry_offsets(C.c_void_p(d.data_ptr()), len(blk), C.c_void_p(offs.data_ptr()), 16,
+                                        C.c_void_p(cnt.data_ptr()), C.c_void_p(reg.data_ptr()),
+                                        C.c_void_p(codec._stream_handle(None)))
+    assert rc == 0
+    assert int(cnt.item()) == 2 and int(reg.item()) == 0
+    assert offs[:2].cpu().tolist() == [0, 5]

@@ -34,6 +34,42 @@ def test_golden_files():
     assert _device_file([(b"hello", b"I'm the one")], 8192, 16) == open(os.path.join(GOLD, "one_key.mtbl"), "rb").read()
 
 
+def test_restart_kat_device():
+    """the hand-derived restart-cadence / multi-byte-header KAT
+    (tests/golden/make_golden.py RESTART_KAT: 33 records at interval 16 -> restarts at entries
+    0 / 16 / 32, a 2-byte non_shared varint, a 3-byte value_length varint) -- written by the
+    device Writer (k_plan + k_encode + the index kernels), encoded unframed by k_encode, and
+    decoded by the device (mtblx_decode_blocks, verified and fused-verified, and the Reader)"""
+    encode = _dev()
+    import json
+    import sys
+
+    import torch
+    from mtblx import codec, reader
+    sys.path.insert(0, GOLD)
+    import make_golden
+    k = json.load(open(os.path.join(GOLD, "kat.json")))["restart_kat"]
+    gold = open(os.path.join(GOLD, "restart_kat.mtbl"), "rb").read()
+    recs = make_golden.restart_kat_records()
+    assert _device_file(recs, k["block_size"], k["restart_interval"]) == gold
+    d = encode.DeviceRecords.from_list(recs)
+    blk = torch.tensor([0, len(recs)], dtype=torch.int64, device="cuda")
+    e = encode.encode_blocks(d, blk, k["restart_interval"], framed=False)
+    content = gold[7: 7 + k["content_len"]]
+    o, n = int(e.blk_off[0].item()), int(e.blk_len[0].item())
+    assert e.out.cpu().numpy()[o: o + n].tobytes() == content
+    f = np.frombuffer(gold, np.uint8)
+    batch = codec.DeviceBatch.from_host(f, np.array([7], np.uint64), np.array([k["content_len"]], np.uint32))
+    h = codec.decode_blocks(batch).to_host()
+    assert int(h.status[0]) == 0 and h.records(0) == recs
+    for fused in (False, True):
+        out, crc, bad = codec.decode_verify(batch, framed=True, fused=fused)
+        torch.cuda.synchronize()
+        assert out.to_host().records(0) == recs
+        assert int(crc.cpu().numpy().view(np.uint32)[0]) == int(k["data_block_crc"], 16) and int(bad[0].item()) == 0
+    assert reader.Reader(f).iter().records() == recs
+
+
 def _append_quirk_records(n, vlen):
     """consecutive pairs (.. j, 0xFF ..) < (.. j+1, 0x00 ..): every block boundary between
     them takes the separator's write_u16 APPEND branch (src/writer.rs:254-262)"""

@@ -2,11 +2,13 @@
 // build/libmtblx_bounds.so; never the product or the measured build).
 //
 // What it checks: every global access a kernel makes through MTBLX_CHK(p, n) must fall inside
-// one of the device allocations its launch was handed (the hipMalloc / caching-allocator
-// segments that contain the launch's pointer arguments, found with hipMemGetAddressRange).  An
-// access outside all of them is exactly the kind that can fault the GPU (hipErrorIllegalAddress)
-// when the next page is unmapped, and that silently reads or corrupts another buffer when it is
-// not.  The first violation of a launch is recorded in a device word (source line, address,
+// one of the ranges its launch was handed: the caller-declared extent of an argument where the
+// entry point knows it (Rng{ptr, bytes}: data_len, capacities, nblk / nq sized arrays), else the
+// device allocation that contains the pointer (the hipMalloc / caching-allocator segment, found
+// with hipMemGetAddressRange).  An access outside every range breaks the entry point's contract;
+// outside every allocation it is exactly the kind that can fault the GPU
+// (hipErrorIllegalAddress) when the next page is unmapped, and that silently reads or corrupts
+// another buffer when it is not.  The first violation of a launch is recorded in a device word (source line, address,
 // size); the host side of every launch (MTBLX_LAUNCH) then synchronizes the stream and prints it
 // with the kernel's name, so a fault or a violation is reported by the launch that caused it,
 // not by whatever API call comes next.  mtblx_bounds_report() (mtblx_api.cpp) returns the
@@ -68,21 +70,35 @@ __device__ __forceinline__ void lcheck(const void* p, uint32_t n, uint32_t line)
   if ((uint64_t)off + n > (uint64_t)__builtin_amdgcn_groupstaticsize()) violation(line | 0x80000000u, off, n);
 }
 
-// host: the allocations behind the launch's pointer arguments -> the table; the whole device is
-// synchronized first, so no kernel of this translation unit still reads the previous table
-// MTBLX_BOUNDS_SELFTEST=1 (tests/test_bounds_gpu.py): the launch's FIRST pointer is left out of
-// the table, so the checker must report that launch's reads of it
-inline void set_ranges(hipStream_t s, std::initializer_list<const void*> ptrs) {
+// one range of a launch: [p, p + n), or (n == 0) the allocation holding p
+struct Rng {
+  const void* p;
+  uint64_t n;
+  Rng(const void* q) : p(q), n(0) {}
+  Rng(const void* q, uint64_t m) : p(q), n(m) {}
+};
+
+// host: the launch's ranges -> the table; the whole device is synchronized first, so no kernel of
+// this translation unit still reads the previous table.  MTBLX_BOUNDS_SELFTEST=1
+// (tests/test_bounds_gpu.py): the launch's FIRST range is left out of the table, so the checker
+// must report that launch's accesses to it.
+inline void set_ranges(hipStream_t s, std::initializer_list<Rng> rs) {
   (void)hipDeviceSynchronize();
   Tab t{};
   const char* st = getenv("MTBLX_BOUNDS_SELFTEST");
   bool skip = st && st[0] == '1';
-  for (const void* p : ptrs) {
+  for (const Rng& r : rs) {
     if (skip) { skip = false; continue; }
-    if (!p || t.n >= (uint32_t)kMaxRanges) continue;
+    if (!r.p || t.n >= (uint32_t)kMaxRanges) continue;
+    if (r.n) {
+      t.lo[t.n] = (uint64_t)(uintptr_t)r.p;
+      t.hi[t.n] = (uint64_t)(uintptr_t)r.p + r.n;
+      ++t.n;
+      continue;
+    }
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess || !base) {
+    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(r.p)) != hipSuccess || !base) {
       (void)hipGetLastError();
       continue;
     }
@@ -116,16 +132,19 @@ inline void after(const char* name, hipStream_t s) {
 
 #define MTBLX_CHK(p, n) mtblx_bounds::check((const void*)(p), (uint64_t)(n), __LINE__)
 #define MTBLX_LCHK(p, n) mtblx_bounds::lcheck((const void*)(p), (uint32_t)(n), __LINE__)
-// MTBLX_LAUNCH((ptr, ptr, ...), kernel, grid, block, shmem, stream, args...)
+// MTBLX_LAUNCH((range, range, ...), kernel, grid, block, shmem, stream, args...): a range is a
+// pointer (its allocation) or MTBLX_R(ptr, bytes) (the caller-declared extent)
 #define MTBLX_PTRS(...) {__VA_ARGS__}
-#define MTBLX_LAUNCH(ptrs, kern, g, b, sh, s, ...)                                   \
-  do {                                                                               \
-    mtblx_bounds::set_ranges((s), std::initializer_list<const void*> MTBLX_PTRS ptrs); \
+#define MTBLX_R(p, n) mtblx_bounds::Rng((const void*)(p), (uint64_t)(n))
+#define MTBLX_LAUNCH(ptrs, kern, g, b, sh, s, ...)                                        \
+  do {                                                                                    \
+    mtblx_bounds::set_ranges((s), std::initializer_list<mtblx_bounds::Rng> MTBLX_PTRS ptrs); \
     hipLaunchKernelGGL(kern, g, b, sh, s, __VA_ARGS__);                              \
     mtblx_bounds::after(#kern, (s));                                                 \
   } while (0)
 #else
 #define MTBLX_CHK(p, n) ((void)0)
 #define MTBLX_LCHK(p, n) ((void)0)
+#define MTBLX_R(p, n) (p)
 #define MTBLX_LAUNCH(ptrs, kern, g, b, sh, s, ...) hipLaunchKernelGGL(kern, g, b, sh, s, __VA_ARGS__)
 #endif

@@ -214,30 +214,6 @@ struct RingSlot {   // one step: its 64 16-byte chunks, lowest address first
 };
 static_assert(kMStep / 16 == kWave, "one LDS-DMA wave-instruction per step");
 
-// The block's first bytes: a step's chunks lie at block positions a = sb + 16 k, 16-byte aligned
-// in memory while the block is not.  A chunk wholly before the block is zeroed (its DMA read
-// the block's first aligned chunk instead); the chunk holding byte 0 keeps bytes >= 0 only; the
-// 0xFFFFFFFF init is folded into bytes 0..3 (one or two chunks, one or two steps).
-__device__ __forceinline__ uint32_t head_dword(uint32_t w, int pos) {
-  if (pos >= 4) return w;
-  const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
-  const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8 * (uint32_t)pos);
-  return (w & keep) ^ fold;
-}
-__device__ __forceinline__ v4u head_chunk(v4u x, int a) {
-  if (a <= -16) return v4u{0u, 0u, 0u, 0u};
-  if (a >= 4) return x;
-  return v4u{head_dword(x.x, a), head_dword(x.y, a + 4), head_dword(x.z, a + 8), head_dword(x.w, a + 12)};
-}
-// the pad after the block's end: t < 16 zero bytes in the last chunk of the block's last step
-__device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
-  const uint32_t k = 16u - t;   // bytes kept
-  const auto m = [&](uint32_t d) {
-    return k >= 4 * d + 4 ? 0xFFFFFFFFu : (k <= 4 * d ? 0u : 0xFFFFFFFFu >> (8 * (4 * d + 4 - k)));
-  };
-  return v4u{y.x & m(0), y.y & m(1), y.z & m(2), y.w & m(3)};
-}
-
 // s_waitcnt vmcnt(k): a step has landed once at most the k DMA instructions of the k steps
 // issued after it are outstanding (the counter retires in issue order).  The steady state waits
 // vmcnt(kRing - 1) inline; this is the drain at the end of the wave's blocks.
@@ -556,7 +532,9 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
     }
     const uint32_t need = (in->nblk + mtblx_crc::kMWaves - 1u) / mtblx_crc::kMWaves;
     const dim3 g(need < (uint32_t)mgrid ? need : (uint32_t)mgrid), t(mtblx_crc::kMThreads);
-    MTBLX_LAUNCH((in->data, in->blk_off, in->blk_len, crc, bad), mtblx_crc::k_crc32c_mfma, g, t, 0,
+    MTBLX_LAUNCH((MTBLX_R(in->data, in->data_len), MTBLX_R(in->blk_off, 8ull * in->nblk),
+                  MTBLX_R(in->blk_len, 4ull * in->nblk), MTBLX_R(crc, 4ull * in->nblk), MTBLX_R(bad, in->nblk)),
+                 mtblx_crc::k_crc32c_mfma, g, t, 0,
                  reinterpret_cast<hipStream_t>(stream), in->data,
                        in->data_len, in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
     return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
@@ -576,7 +554,9 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   const uint32_t wpg = mtblx_crc::kCrcThreads / mtblx_crc::kWave;   // waves (blocks in flight) per workgroup
   const uint32_t need = (in->nblk + wpg - 1u) / wpg;
   const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);
-  MTBLX_LAUNCH((in->data, in->blk_off, in->blk_len, crc, bad), mtblx_crc::k_crc32c_blocks, g, t, 0,
+  MTBLX_LAUNCH((MTBLX_R(in->data, in->data_len), MTBLX_R(in->blk_off, 8ull * in->nblk),
+                MTBLX_R(in->blk_len, 4ull * in->nblk), MTBLX_R(crc, 4ull * in->nblk), MTBLX_R(bad, in->nblk)),
+               mtblx_crc::k_crc32c_blocks, g, t, 0,
                reinterpret_cast<hipStream_t>(stream), in->data, in->data_len,
                      in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;

@@ -130,4 +130,23 @@ struct MfmaTabs {
   }
 };
 
+// nibble tables of the super-window shifts x^(8·8192·S), S < N (a super-window's raw CRC moved to
+// its place in a block of N super-windows at most): encode.hip (blocks assembled in LDS) and the
+// fused verify of decode.hip (blocks staged in LDS)
+template <int N>
+struct SwTabs {
+  uint32_t t[N][8][16];
+  constexpr SwTabs() : t() {
+    static_assert(kMStep * kMSup == 8192, "8 KiB super-windows");
+    uint32_t K = 0x80000000u;   // x^8, squared 13 times: x^(8·8192)
+    for (int k = 0; k < 8; ++k) K = (K & 1u) ? (K >> 1) ^ kPoly : K >> 1;
+    for (int q = 0; q < 13; ++q) K = multmodp(K, K);
+    uint32_t P = 0x80000000u;
+    for (int S = 0; S < N; ++S) {
+      MulTabs::fill(t[S], P);
+      P = multmodp(K, P);
+    }
+  }
+};
+
 }  // namespace mtblx_crc

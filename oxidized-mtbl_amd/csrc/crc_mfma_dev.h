@@ -64,4 +64,46 @@ __device__ __forceinline__ void mfma_step(const v4i (&A)[kMKs][2], v4u x, v4i a2
   c2b = mfma_f16(a2hi, b2, c2b);
 }
 
+// mfma_step with the stage-1 operand A read from memory (pa: lane's entry of MfmaTabs::a, as v4i,
+// k-step k half h at pa[(2 k + h) 64]) instead of registers: 8 VGPRs live instead of 32
+__device__ __forceinline__ void mfma_step_ld(const v4i* pa, v4u x, v4i a2lo, v4i a2hi, v4f& c2a, v4f& c2b) {
+  const uint32_t w[kMKs] = {x.x, x.y, x.z, x.w};
+  v4f c1a = {0.f, 0.f, 0.f, 0.f}, c1b = c1a;
+#pragma unroll
+  for (int k = 0; k < kMKs; ++k) {
+    const uint32_t v = w[k];
+    const v4i b = {(int)(v & 0x11111111u), (int)(v & 0x22222222u), (int)(v & 0x44444444u),
+                   (int)((v >> 1) & 0x44444444u)};
+    c1a = mfma_fp4(pa[(2 * k) * 64], b, c1a);
+    c1b = mfma_fp4(pa[(2 * k + 1) * 64], b, c1b);
+  }
+  const v4i b2 = {pk16(c1a.x, c1a.y), pk16(c1a.z, c1a.w), pk16(c1b.x, c1b.y), pk16(c1b.z, c1b.w)};
+  c2a = mfma_f16(a2lo, b2, c2a);
+  c2b = mfma_f16(a2hi, b2, c2b);
+}
+
+// The block's first bytes: a step's chunks lie at block positions a = sb + 16 k, 16-byte aligned
+// in memory while the block is not.  A chunk wholly before the block is zeroed (its DMA read
+// the block's first aligned chunk instead); the chunk holding byte 0 keeps bytes >= 0 only; the
+// 0xFFFFFFFF init is folded into bytes 0..3 (one or two chunks, one or two steps).
+__device__ __forceinline__ uint32_t head_dword(uint32_t w, int pos) {
+  if (pos >= 4) return w;
+  const uint32_t keep = pos <= -4 ? 0u : (pos < 0 ? 0xFFFFFFFFu << (8 * (uint32_t)(-pos)) : 0xFFFFFFFFu);
+  const uint32_t fold = pos < 0 ? keep : 0xFFFFFFFFu >> (8 * (uint32_t)pos);
+  return (w & keep) ^ fold;
+}
+__device__ __forceinline__ v4u head_chunk(v4u x, int a) {
+  if (a <= -16) return v4u{0u, 0u, 0u, 0u};
+  if (a >= 4) return x;
+  return v4u{head_dword(x.x, a), head_dword(x.y, a + 4), head_dword(x.z, a + 8), head_dword(x.w, a + 12)};
+}
+// the pad after the block's end: t < 16 zero bytes in the last chunk of the block's last step
+__device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
+  const uint32_t k = 16u - t;   // bytes kept
+  const auto m = [&](uint32_t d) {
+    return k >= 4 * d + 4 ? 0xFFFFFFFFu : (k <= 4 * d ? 0u : 0xFFFFFFFFu >> (8 * (4 * d + 4 - k)));
+  };
+  return v4u{y.x & m(0), y.y & m(1), y.z & m(2), y.w & m(3)};
+}
+
 }  // namespace mtblx_crc

@@ -19,6 +19,8 @@
 
 #include "bounds.h"
 #include "crc_dev.h"
+#include "crc_mfma.h"
+#include "crc_mfma_dev.h"
 #include "mtblx.h"
 
 // Ablations (outputs incomplete by construction) and the spilling variant build only through the
@@ -2153,6 +2155,79 @@ __device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileAr
   }
 }
 
+// The fused checksum on the matrix cores (MTBLX_FUSED_MFMA, default): the staged blocks' CRC-32C
+// by the method of k_crc32c_mfma (crc_mfma.h) read straight from the tile's LDS stage.  Work unit
+// = (block j, super-window sw: 8 steps of 1 KiB counted from the block's 16-byte aligned end in
+// the stage); copy wave cw takes units cw, cw + NC, ... of the tile after its copy.  Per step a
+// lane reads its aligned 16-byte chunk (ds_read_b128), masks the bytes before the block start
+// and folds the init into bytes 0..3 (head_chunk), masks the pad after the block end
+// (tail_chunk), then 8 fp4 + 2 f16 MFMAs (mfma_step); per unit the column parities, the column
+// and super-window shifts and the pad removal x^(-8t) (nibble tables), XORed into the block's
+// accumulator.  Round 4's VALU window loop (slicing-by-4, MTBLX_FUSED_MFMA=0) stays for A/B.
+#ifndef MTBLX_FUSED_MFMA
+#define MTBLX_FUSED_MFMA 0
+#endif
+constexpr int kDecSup = (65664 + mtblx_crc::kMStep * mtblx_crc::kMSup - 1) / (mtblx_crc::kMStep * mtblx_crc::kMSup) + 1;
+static __constant__ mtblx_crc::MfmaTabs kDecMfma = mtblx_crc::MfmaTabs();
+static __constant__ mtblx_crc::SwTabs<kDecSup> kDecSw = mtblx_crc::SwTabs<kDecSup>();
+
+template <class P>
+__device__ __forceinline__ void pipe_crc_mfma(const PipeBuf<P>& B, PipeLds<P>& S, uint32_t cw, int lane, uint32_t par) {
+  using namespace mtblx_crc;
+  constexpr uint32_t NC = (uint32_t)P::NCOPY;
+  const uint32_t nb = B.nb;
+  const int g = lane >> 4, n = lane & 15;
+  const int32_t kx16 = 16 * (60 - 4 * n + g);   // the lane's chunk of a step
+  uint32_t u = 0;   // running unit number over the tile's blocks
+  for (uint32_t j = 0; j < nb; ++j) {
+    const uint32_t L = B.blen[j], bo = B.boff[j];
+    if (bo >= kOutOfBounds || L < 4u) continue;   // pipe_crc_final: from HBM / byte-wise
+    const uint32_t t = (16u - ((bo + L) & 15u)) & 15u, Lp = L + t;
+    const uint32_t steps = (Lp + kMStep - 1) / kMStep, nsup = (steps + kMSup - 1) / kMSup;
+    // this wave's units of block j: sw with (u + sw) % NC == cw
+    uint32_t sw = (cw + NC - u % NC) % NC;
+    u += nsup;
+    for (; sw < nsup; sw += NC) {
+      v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
+#pragma unroll 1
+      for (int tt = kMSup - 1; tt >= 0; --tt) {   // from the super-window's start
+        const uint32_t s = sw * kMSup + (uint32_t)tt;
+        if (s < steps) {
+          const int32_t pos = (int32_t)Lp - (int32_t)(kMStep * (s + 1)) + kx16;   // block position, 16-aligned in LDS
+          v4u x = {0u, 0u, 0u, 0u};
+          if (pos > -16) {
+            MTBLX_LCHK(B.stage + (int32_t)bo + pos, 16);
+            const uint4 w = *reinterpret_cast<const uint4*>(B.stage + (int32_t)bo + pos);
+            x = v4u{w.x, w.y, w.z, w.w};
+            if (pos < 4) x = head_chunk(x, pos);
+          }
+          if (s == 0 && t != 0 && lane == 48) x = tail_chunk(x, t);   // lane (g 3, n 0): the step's last chunk
+          // the stage-1 operands are read per step (L1 / L2 hits): held in registers through the
+          // tile loop they pushed the fused-verify kernels past 128 VGPRs into scratch
+          const v4i* pa = reinterpret_cast<const v4i*>(&kDecMfma.a[0][0][0][0]) + lane;
+          const v4i a2lo = reinterpret_cast<const v4i*>(&kDecMfma.a2[tt][0][0][0])[lane];
+          const v4i a2hi = reinterpret_cast<const v4i*>(&kDecMfma.a2[tt][1][0][0])[lane];
+          mfma_step_ld(pa, x, a2lo, a2hi, c2a, c2b);
+        }
+      }
+      uint32_t c = kDecMfma.col[n][g][par_nib(c2a)] ^ kDecMfma.col[n][4 + g][par_nib(c2b)];
+      c = row_xor(c);
+      uint32_t C = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 16) ^
+                   (uint32_t)__builtin_amdgcn_readlane((int)c, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
+      const uint32_t jl = (uint32_t)lane & 15u;
+      if (sw) {   // x^(8·8192·sw)
+        const uint32_t v = jl < 8u ? kDecSw.t[sw][jl][(C >> (4 * jl)) & 15u] : 0u;
+        C = (uint32_t)__builtin_amdgcn_readlane((int)row_xor(v), 0);
+      }
+      if (t) {    // x^(-8t): the pad removed (linear: per unit, before the XOR of the units)
+        const uint32_t v = jl < 8u ? kDecMfma.inv[t][jl][(C >> (4 * jl)) & 15u] : 0u;
+        C = (uint32_t)__builtin_amdgcn_readlane((int)row_xor(v), 0);
+      }
+      if (lane == 0) __hip_atomic_fetch_xor(&S.cacc[par][j], C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+
 // copy wave cw (of NC) after its copy of tile B: its share of the windows, then the count; the
 // last of the NC waves finalises the tile
 template <class P>
@@ -2190,7 +2265,8 @@ __device__ MTBLX_PIPE_CRC_INLINE void pipe_crc_copy(const PipeBuf<P>& B, const T
   const uint32_t* st32 = reinterpret_cast<const uint32_t*>(B.stage);
   const uint32_t g = nb >= NC ? 1u : NC / nb;           // waves per block
   const uint32_t jstep = nb >= NC ? NC : nb;            // (nb < NC: one block per wave, then done)
-  if constexpr ((MTBLX_ABL_CRC & 1) == 0)
+  if constexpr ((MTBLX_ABL_CRC & 1) == 0 && MTBLX_FUSED_MFMA) pipe_crc_mfma(B, S, cw, lane, par);
+  if constexpr ((MTBLX_ABL_CRC & 1) == 0 && !MTBLX_FUSED_MFMA)
   for (uint32_t j = nb >= NC ? cw : cw / g; j < nb; j += jstep) {
     const uint32_t s = nb >= NC ? 0u : cw % g;
     const uint32_t L = B.blen[j], bo = B.boff[j];
@@ -2705,8 +2781,12 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
              wscap,        0,             0,            debug_flags()};
   a.wait_ticks = debug_ms("MTBLX_DEBUG_WAIT_MS", kWaitTicks);
   a.dbg_delay0 = debug_ms("MTBLX_DEBUG_DELAY0_MS", 0);
-#define MTBLX_DECODE_PTRS (in->data, in->blk_off, in->blk_len, out->nrec, out->rec_base, out->key_base, out->val_base, \
-                           out->status, out->key_end, out->val_end, out->keys, out->vals, out->totals, ws, crc, crc_bad)
+#define MTBLX_DECODE_PTRS                                                                                        \
+  (MTBLX_R(in->data, in->data_len), MTBLX_R(in->blk_off, 8ull * nblk), MTBLX_R(in->blk_len, 4ull * nblk),         \
+   MTBLX_R(out->nrec, 4ull * nblk), MTBLX_R(out->rec_base, 8ull * nblk), MTBLX_R(out->key_base, 8ull * nblk),      \
+   MTBLX_R(out->val_base, 8ull * nblk), MTBLX_R(out->status, 4ull * nblk), MTBLX_R(out->key_end, 4 * out->rec_cap), \
+   MTBLX_R(out->val_end, 4 * out->rec_cap), MTBLX_R(out->keys, out->keys_cap), MTBLX_R(out->vals, out->vals_cap),   \
+   MTBLX_R(out->totals, 32), MTBLX_R(ws, ws_bytes), MTBLX_R(crc, 4ull * nblk), MTBLX_R(crc_bad, nblk))
   if (p.kind == 0) {
     if (verify)
       MTBLX_LAUNCH(MTBLX_DECODE_PTRS, k_decode_pipe<PipeSmallV>, dim3(pipe_grid(p.ntiles)), dim3(kPipeThreads), 0, s, a);

@@ -236,20 +236,7 @@ static __constant__ X8Tab kX8 = X8Tab();
 #define MTBLX_ENC_CRC_UNROLL 4
 #endif
 constexpr int kEncSup = (kLdsBlock + mtblx_crc::kMStep * mtblx_crc::kMSup - 1) / (mtblx_crc::kMStep * mtblx_crc::kMSup);
-struct EncSw {
-  uint32_t t[kEncSup][8][16];
-  constexpr EncSw() : t() {
-    uint32_t K = 0x80000000u;   // x^8, squared 13 times: x^(8·8192)
-    for (int k = 0; k < 8; ++k) K = (K & 1u) ? (K >> 1) ^ mtblx_crc::kPoly : K >> 1;
-    for (int q = 0; q < 13; ++q) K = mtblx_crc::multmodp(K, K);
-    uint32_t P = 0x80000000u;
-    for (int S = 0; S < kEncSup; ++S) {
-      mtblx_crc::MulTabs::fill(t[S], P);
-      P = mtblx_crc::multmodp(K, P);
-    }
-  }
-};
-static_assert(mtblx_crc::kMStep * mtblx_crc::kMSup == 8192, "EncSw: 8 KiB super-windows");
+using EncSw = mtblx_crc::SwTabs<kEncSup>;
 static __constant__ mtblx_crc::MfmaTabs kEncMfma = mtblx_crc::MfmaTabs();
 static __constant__ EncSw kEncSw = EncSw();
 

@@ -867,7 +867,9 @@ extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t 
   if (nent == 0) return MTBLX_OK;
   if (!file || !vals || !val_end || !blk_off || !blk_len || !dir_st || version > 1) return MTBLX_E_INVAL;
   const uint32_t threads = 256;
-  MTBLX_LAUNCH((file, vals, val_end, blk_off, blk_len, dir_st), mtblx_rd::k_block_dir,
+  MTBLX_LAUNCH((MTBLX_R(file, file_len), vals, MTBLX_R(val_end, 4ull * nent), MTBLX_R(blk_off, 8ull * nent),
+                MTBLX_R(blk_len, 4ull * nent), MTBLX_R(dir_st, 4ull * nent)),
+               mtblx_rd::k_block_dir,
                dim3((nent + threads - 1) / threads), dim3(threads), 0, reinterpret_cast<hipStream_t>(stream), file, file_len, version, vals, val_end, val_base, nent,
                      blk_off, blk_len, dir_st);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
@@ -886,7 +888,9 @@ extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t versio
     grid = (ncu > 0 ? ncu : 256) * 8;
   }
   const uint32_t need = (nq + 3u) / 4u;
-  MTBLX_LAUNCH((file, keys, key_end, status, val_off, val_len), mtblx_rd::k_get,
+  MTBLX_LAUNCH((MTBLX_R(file, file_len), keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(status, 4ull * nq),
+                MTBLX_R(val_off, 8ull * nq), MTBLX_R(val_len, 8ull * nq)),
+               mtblx_rd::k_get,
                dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
                      mtblx_rd::DecTab{nullptr, nullptr, nullptr, nullptr, 0u, nullptr}, keys, key_end, nq, status,
@@ -911,7 +915,9 @@ extern "C" int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, ui
     grid = (ncu > 0 ? ncu : 256) * 8;
   }
   const uint32_t need = (nq + 3u) / 4u;
-  MTBLX_LAUNCH((file, tab_start, tab_doff, tab_dlen, tab_st, dec, keys, key_end, status, val_off, val_len),
+  MTBLX_LAUNCH((MTBLX_R(file, file_len), MTBLX_R(tab_start, 8ull * ntab), MTBLX_R(tab_doff, 8ull * ntab),
+                MTBLX_R(tab_dlen, 8ull * ntab), MTBLX_R(tab_st, 4ull * ntab), dec, keys, MTBLX_R(key_end, 8ull * nq),
+                MTBLX_R(status, 4ull * nq), MTBLX_R(val_off, 8ull * nq), MTBLX_R(val_len, 8ull * nq)),
                mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
                      mtblx_rd::DecTab{tab_start, tab_doff, tab_dlen, tab_st, ntab, dec}, keys, key_end, nq, status,
@@ -925,7 +931,8 @@ extern "C" int mtblx_index_seek_batch(const uint8_t* file, uint64_t file_len, ui
   if (nq == 0) return MTBLX_OK;
   if (!file || !keys || !key_end || !out || version > 1) return MTBLX_E_INVAL;
   const uint32_t need = (nq + 3u) / 4u;
-  MTBLX_LAUNCH((file, keys, key_end, out), mtblx_rd::k_index_seek, dim3(need < 2048u ? need : 2048u), dim3(256), 0,
+  MTBLX_LAUNCH((MTBLX_R(file, file_len), keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(out, sizeof(*out) * nq)),
+               mtblx_rd::k_index_seek, dim3(need < 2048u ? need : 2048u), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
                      keys, key_end, nq, out);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
@@ -937,7 +944,9 @@ extern "C" int mtblx_block_seek_batch(const uint8_t* data, const uint8_t* keys, 
                                       uint64_t* kcap_out, uint64_t rec_cap, void* stream) {
   if (nq == 0) return MTBLX_OK;
   if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out) return MTBLX_E_INVAL;
-  MTBLX_LAUNCH((data, keys, key_end, q, out_keys, out_vals, key_end_out, val_end_out, kcap_out),
+  MTBLX_LAUNCH((data, keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(q, sizeof(*q) * nq), MTBLX_R(out_keys, keys_cap * nq),
+                MTBLX_R(out_vals, vals_cap * nq), MTBLX_R(key_end_out, 8 * rec_cap * nq),
+                MTBLX_R(val_end_out, 8 * rec_cap * nq), MTBLX_R(kcap_out, 8 * rec_cap * nq)),
                mtblx_rd::k_block_seek<false>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
                      vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, nullptr, 0);
@@ -953,7 +962,10 @@ extern "C" int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* k
   if (!data || !keys || !key_end || !q || !out_keys || !out_vals || !key_end_out || !val_end_out || !key_buf ||
       key_buf_cap == 0)
     return MTBLX_E_INVAL;
-  MTBLX_LAUNCH((data, keys, key_end, q, out_keys, out_vals, key_end_out, val_end_out, kcap_out, key_buf),
+  MTBLX_LAUNCH((data, keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(q, sizeof(*q) * nq), MTBLX_R(out_keys, keys_cap * nq),
+                MTBLX_R(out_vals, vals_cap * nq), MTBLX_R(key_end_out, 8 * rec_cap * nq),
+                MTBLX_R(val_end_out, 8 * rec_cap * nq), MTBLX_R(kcap_out, 8 * rec_cap * nq),
+                MTBLX_R(key_buf, key_buf_cap * nq)),
                mtblx_rd::k_block_seek<true>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
                      vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, key_buf, key_buf_cap);
@@ -970,7 +982,8 @@ extern "C" int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t*
   // Reader; r05: no stream-ordered pool allocations next to the caller's caching allocator)
   uint64_t* scratch = nullptr;
   if (hipMalloc(reinterpret_cast<void**>(&scratch), nr * sizeof(uint64_t)) != hipSuccess) return MTBLX_E_HIP;
-  MTBLX_LAUNCH((block, offs, count, scratch, regular), mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch,
+  MTBLX_LAUNCH((MTBLX_R(block, len), MTBLX_R(offs, 8 * cap), MTBLX_R(count, 8), MTBLX_R(scratch, 8 * nr),
+                MTBLX_R(regular, 4)), mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch,
                      regular);
   const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
   (void)hipFree(scratch);
@@ -983,7 +996,7 @@ extern "C" int mtblx_key_filter(const uint8_t* keys, const uint64_t* key_end, ui
   if (!keys || !key_end || !first_fail || (klen && !k) || type < 1 || type > 3) return MTBLX_E_INVAL;
   const uint64_t blocks = (n + 255) / 256;
   if (blocks > 0x7FFFFFFFull) return MTBLX_E_INVAL;
-  MTBLX_LAUNCH((keys, key_end, k, first_fail), mtblx_rd::k_key_filter, dim3((uint32_t)blocks), dim3(256), 0,
+  MTBLX_LAUNCH((keys, MTBLX_R(key_end, 8 * n), MTBLX_R(k, klen), MTBLX_R(first_fail, 8)), mtblx_rd::k_key_filter, dim3((uint32_t)blocks), dim3(256), 0,
                reinterpret_cast<hipStream_t>(stream),
                      keys, key_end, n, type, k, klen, reinterpret_cast<unsigned long long*>(first_fail));
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;

@@ -1585,30 +1585,30 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   const bool two_pass = mode == 3 || (mode == 0 && MTBLX_SNAPPY_TWO_DEFAULT);
   const dim3 glanes((nblk + lanes::kThreads - 1) / lanes::kThreads), tlanes(2 * lanes::kThreads);
   if (mode == 2) {
-    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
+    MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len,
                        status, dec_len, 0);
   } else if (max_dst_len != 0 && max_dst_len <= (uint32_t)quad::OUT) {
     // k_snappy_lanes costs about one block's serial decode however many blocks run (all are in
     // flight), the quads ~0.19 ms per round of 8 192 blocks: the lanes win from ~50 000 blocks
     // (25 000 compressible blocks: quads 0.66 ms, lanes ~1.0 ms; 100 000: 2.33 vs 1.24 ms)
     const uint32_t lanes_x = ((mode == 0 && nblk >= kLanesMinBlocks) || mode == 3) ? 2u : 0u;
-    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
+    MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len, lanes_x);
     if (lanes_x && two_pass) {
-      MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), two::k_snappy_parse, dim3((nblk + two::kParseThreads - 1) / two::kParseThreads),
+      MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), two::k_snappy_parse, dim3((nblk + two::kParseThreads - 1) / two::kParseThreads),
                          dim3(two::kParseThreads), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len,
                          status, dec_len);
-      MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, status, dec_len), two::k_snappy_exec, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
+      MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), two::k_snappy_exec, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                          dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, status, dec_len);
     } else if (lanes_x) {
-      MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
+      MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
                          dst_len, status, dec_len, 1);
     }
-    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
+    MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), quad::k_snappy_deferred, dim3(grid_for(2, (nblk + kWave - 1) / kWave)), dim3(kWave), 0, s,
                        src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   } else {
-    MTBLX_LAUNCH((src, src_off, src_len, dst, dst_off, dst_len, status, dec_len), k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,
+    MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), k_snappy_blocks<Large>, dim3(grid_for(2, nblk)), dim3(Large::WAVES * kWave), 0, s, src,
                        src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len);
   }
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;

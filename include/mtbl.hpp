@@ -111,12 +111,18 @@ struct DevBuf {
 };
 // one query of mtblx_block_seek_batch, or -- kbuf allocated: the iterator's key past 64 KiB --
 // of mtblx_block_seek_batch_kbuf with the key in kbuf
+// (vsrc allocated: mtblx_block_seek_batch_ex, the value bytes left to mtblx_copy_ranges)
 inline int block_seek_call(const uint8_t* base, const DevBuf& key, const DevBuf& kend, const DevBuf& q, const DevBuf& k,
                            uint64_t keys_cap, const DevBuf& v, uint64_t vals_cap, const DevBuf& ke, const DevBuf& ve,
-                           const DevBuf& kc, uint64_t rec_cap, const DevBuf& kbuf) {
+                           const DevBuf& kc, uint64_t rec_cap, const DevBuf& kbuf, const DevBuf& vsrc) {
   const auto* kk = static_cast<const uint8_t*>(key.p);
   const auto* kn = static_cast<const uint64_t*>(kend.p);
   auto* qq = static_cast<mtblx_block_seek*>(q.p);
+  if (vsrc.p)
+    return mtblx_block_seek_batch_ex(base, kk, kn, 1, qq, k.as<uint8_t>(), keys_cap, v.as<uint8_t>(), vals_cap,
+                                     ke.as<uint64_t>(), ve.as<uint64_t>(), kc.as<uint64_t>(), rec_cap,
+                                     kbuf.p ? kbuf.as<uint8_t>() : nullptr, kbuf.p ? kbuf.n : 0, vsrc.as<uint64_t>(),
+                                     nullptr);
   if (kbuf.p)
     return mtblx_block_seek_batch_kbuf(base, kk, kn, 1, qq, k.as<uint8_t>(), keys_cap, v.as<uint8_t>(), vals_cap,
                                        ke.as<uint64_t>(), ve.as<uint64_t>(), kc.as<uint64_t>(), rec_cap,
@@ -796,7 +802,9 @@ inline ReaderIntoIter::EmitResult ReaderIntoIter::emit(const Content& c, const B
   for (int attempt = 0; attempt < 4; ++attempt) {
     DevBuf d_q = upload(&q, 1), d_k(keys_cap + 1), d_v(vals_cap + 1), d_ke(8 * rec_cap + 8), d_ve(8 * rec_cap + 8),
         d_kc(8 * rec_cap + 8);
-    abi_check(block_seek_call(c.base, d_key, d_kend, d_q, d_k, keys_cap, d_v, vals_cap, d_ke, d_ve, d_kc, rec_cap, kbuf),
+    DevBuf d_vs = big ? DevBuf(8 * rec_cap + 8) : DevBuf();   // big blocks: values moved by the whole grid
+    abi_check(block_seek_call(c.base, d_key, d_kend, d_q, d_k, keys_cap, d_v, vals_cap, d_ke, d_ve, d_kc, rec_cap, kbuf,
+                              d_vs),
               "mtblx_block_seek_batch");
     hip_check(hipDeviceSynchronize(), "sync");
     EmitResult r;
@@ -820,6 +828,25 @@ inline ReaderIntoIter::EmitResult ReaderIntoIter::emit(const Content& c, const B
     b.kcaps_known = true;
     b.kcap_end = r.res.kcap;
     b.keys = download<uint8_t>(d_k.p, r.res.key_bytes);
+    if (big && r.res.nrec) {   // the values: mtblx_copy_ranges from the block content
+      const std::vector<uint64_t> vs = download<uint64_t>(d_vs.p, r.res.nrec);
+      std::vector<uint64_t> so(r.res.nrec), dofs(r.res.nrec), ln(r.res.nrec), cb(r.res.nrec);
+      uint64_t prev = 0, chunks = 0;
+      for (uint64_t i = 0; i < r.res.nrec; ++i) {
+        so[i] = c.off + vs[i];
+        dofs[i] = prev;
+        ln[i] = b.ve[i] - prev;
+        cb[i] = chunks;
+        chunks += (ln[i] + 15) / 16;
+        prev = b.ve[i];
+      }
+      DevBuf d_so = upload(so.data(), so.size()), d_do = upload(dofs.data(), dofs.size()),
+             d_ln = upload(ln.data(), ln.size()), d_cb = upload(cb.data(), cb.size());
+      abi_check(mtblx_copy_ranges(c.base, d_so.as<uint64_t>(), d_v.as<uint8_t>(), d_do.as<uint64_t>(),
+                                  d_ln.as<uint64_t>(), d_cb.as<uint64_t>(), (uint32_t)r.res.nrec, chunks, nullptr),
+                "mtblx_copy_ranges");
+      hip_check(hipDeviceSynchronize(), "sync");
+    }
     b.vals = download<uint8_t>(d_v.p, r.res.val_bytes);
     if (r.res.has_val) b.last_val = download<uint8_t>(c.base + c.off + r.res.last_voff, r.res.last_vlen);
     return r;
@@ -849,11 +876,13 @@ inline uint64_t ReaderIntoIter::kcap_now(Bi& b) {
     const uint64_t kend = 0;
     const uint8_t z = 0;
     DevBuf d_key = upload(&z, 1), d_kend = upload(&kend, 1), d_q = upload(&q, 1);
-    DevBuf d_k(2 * b.c.len + 65), d_v(b.c.len + 17), d_ke(8 * b.n() + 8), d_ve(8 * b.n() + 8), d_kc(8 * b.n() + 8);
+    // only the key capacities are needed: the value bytes are deferred (vsrc) and never moved
+    DevBuf d_k(2 * b.c.len + 65), d_v, d_ke(8 * b.n() + 8), d_ve(8 * b.n() + 8), d_kc(8 * b.n() + 8),
+        d_vs(8 * b.n() + 8);
     DevBuf kbuf;
     for (int attempt = 0; attempt < 2; ++attempt) {
       abi_check(block_seek_call(b.c.base, d_key, d_kend, d_q, d_k, 2 * b.c.len + 64, d_v, b.c.len + 16, d_ke, d_ve, d_kc,
-                                b.n(), kbuf),
+                                b.n(), kbuf, d_vs),
                 "mtblx_block_seek_batch");
       hip_check(hipDeviceSynchronize(), "sync");
       if (download<mtblx_block_seek>(d_q.p, 1)[0].status != MTBLX_SEEK_UNSUPPORTED || kbuf.p) break;

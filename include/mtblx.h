@@ -303,6 +303,16 @@ int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* keys, const 
                                 mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
                                 uint64_t vals_cap, uint64_t* key_end_out, uint64_t* val_end_out, uint64_t* kcap_out,
                                 uint64_t rec_cap, uint8_t* key_buf, uint64_t key_buf_cap, void* stream);
+/* (2'') the same with the value bytes left to the caller (blocks >= 4 GiB hold values of GiBs):
+ *      record r of query q gets val_end_out as above and val_src_out[q * rec_cap + r] = its value's
+ *      offset in the block content; out_vals is not written (may be NULL) and vals_cap only sizes
+ *      the emission.  The caller then moves the bytes with mtblx_copy_ranges (the whole grid).
+ *      key_buf == NULL: the key in LDS as mtblx_block_seek_batch; else as _kbuf. */
+int mtblx_block_seek_batch_ex(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end, uint32_t nq,
+                              mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap, uint8_t* out_vals,
+                              uint64_t vals_cap, uint64_t* key_end_out, uint64_t* val_end_out, uint64_t* kcap_out,
+                              uint64_t rec_cap, uint8_t* key_buf, uint64_t key_buf_cap, uint64_t* val_src_out,
+                              void* stream);
 
 /* (3) the offsets of the entries seek_to_first + next visit in a block (the index block: entry
  *     i <-> index record i <-> directory entry i), so a seek's landed entry maps to its index
@@ -468,6 +478,13 @@ int mtblx_host_unregister(void* p);
 #define MTBLX_COPY_NT_STORES 4
 #define MTBLX_COPY_NT_LOADS 8
 int mtblx_stream_copy(void* dst, const void* src, uint64_t bytes, int variant, void* stream);
+
+/* n byte ranges src + src_off[i] -> dst + dst_off[i] (len[i] bytes each, device arrays) by the
+ * whole grid: chunk_base[i] = the exclusive prefix of ceil(len / 16) over the ranges, nchunks its
+ * total.  Asynchronous on `stream`.  Used with mtblx_block_seek_batch_ex for the values of blocks
+ * >= 4 GiB (one wave would copy their GiBs at a few GB/s). */
+int mtblx_copy_ranges(const uint8_t* src, const uint64_t* src_off, uint8_t* dst, const uint64_t* dst_off,
+                      const uint64_t* len, const uint64_t* chunk_base, uint32_t n, uint64_t nchunks, void* stream);
 
 #ifdef __cplusplus
 }

@@ -45,7 +45,82 @@ void launch(int variant, dim3 g, hipStream_t s, const v4u* src, v4u* dst, uint64
   }
 }
 
+// n byte ranges src + src_off[i] -> dst + dst_off[i], len[i] bytes, by the whole grid: the
+// ranges' 16-byte destination chunks are numbered across all ranges (exclusive prefix in
+// chunk_base, host-computed) and every thread takes chunks grid-stride, U in flight: an unaligned
+// 16-byte load and store per whole chunk, bytes at each range's ragged ends.  For the values of
+// blocks >= 4 GiB (mtblx_block_seek_batch_ex).
+typedef uint32_t v4uu __attribute__((ext_vector_type(4), aligned(1)));
+__global__ void __launch_bounds__(256) k_copy_ranges(const uint8_t* __restrict__ src, const uint64_t* src_off,
+                                                     uint8_t* __restrict__ dst, const uint64_t* dst_off,
+                                                     const uint64_t* len, const uint64_t* chunk_base, uint32_t n,
+                                                     uint64_t nchunks) {
+  constexpr int U = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  for (; c < nchunks; c += stride * U) {
+    v4uu v[U];
+    uint8_t* dp[U];
+    uint32_t m[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t cc = c + stride * (uint64_t)u;
+      m[u] = 0;
+      if (cc >= nchunks) continue;
+      uint32_t lo = 0, hi = n;   // the range holding chunk cc: last i with chunk_base[i] <= cc
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (chunk_base[mid] <= cc) lo = mid; else hi = mid;
+      }
+      const uint64_t k = 16 * (cc - chunk_base[lo]), L = len[lo];
+      const uint8_t* sp = src + src_off[lo] + k;
+      dp[u] = dst + dst_off[lo] + k;
+      m[u] = L - k < 16 ? (uint32_t)(L - k) : 16u;
+      MTBLX_CHK(sp, m[u]);
+      if (m[u] == 16) {
+        v[u] = *reinterpret_cast<const v4uu*>(sp);
+      } else {
+        uint32_t t[4] = {0, 0, 0, 0};
+        for (uint32_t b = 0; b < m[u]; ++b) t[b >> 2] |= (uint32_t)sp[b] << (8 * (b & 3));
+        v[u] = v4uu{t[0], t[1], t[2], t[3]};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (m[u] == 0) continue;
+      MTBLX_CHK(dp[u], m[u]);
+      if (m[u] == 16) {
+        *reinterpret_cast<v4uu*>(dp[u]) = v[u];
+      } else {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        for (uint32_t b = 0; b < m[u]; ++b) dp[u][b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int mtblx_copy_ranges(const uint8_t* src, const uint64_t* src_off, uint8_t* dst, const uint64_t* dst_off,
+                                 const uint64_t* len, const uint64_t* chunk_base, uint32_t n, uint64_t nchunks,
+                                 void* stream) {
+  if (n == 0 || nchunks == 0) return MTBLX_OK;
+  if (!src || !src_off || !dst || !dst_off || !len || !chunk_base) return MTBLX_E_INVAL;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const uint64_t want = (nchunks + 4 * 256 - 1) / (4 * 256);
+  const dim3 g((unsigned)(want < (uint64_t)ncu * 8u ? want : (uint64_t)ncu * 8u));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * n), dst, MTBLX_R(dst_off, 8ull * n), MTBLX_R(len, 8ull * n),
+                MTBLX_R(chunk_base, 8ull * n)),
+               k_copy_ranges, g, dim3(256), 0, s, src, src_off, dst, dst_off, len, chunk_base, n, nchunks);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
 
 extern "C" int mtblx_stream_copy(void* dst, const void* src, uint64_t bytes, int variant, void* stream) {
   if (!dst || !src || (bytes & 15u) || ((uintptr_t)dst & 15u) || ((uintptr_t)src & 15u)) return MTBLX_E_INVAL;

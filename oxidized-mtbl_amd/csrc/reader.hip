@@ -577,13 +577,16 @@ __device__ __forceinline__ int s_seek(const Blk& b, SIt& it, uint8_t* K, uint64_
 }
 
 // GK: the key lives in the caller's buffer (kbuf + q * kbuf_cap) instead of LDS -- keys longer
-// than 64 KiB (mtblx_block_seek_batch_kbuf)
-template <bool GK>
+// than 64 KiB (mtblx_block_seek_batch_kbuf).  DEFER: value bytes are not copied by the wave;
+// record r's value source (content offset) goes to vsrc[q * rec_cap + r] and the caller moves
+// the bytes with the whole grid (mtblx_block_seek_batch_ex + mtblx_copy_ranges: blocks >= 4 GiB
+// hold values of GiBs, which one wave copies at a few GB/s)
+template <bool GK, bool DEFER = false>
 __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const uint8_t* qkeys, const uint64_t* qend,
                                                    uint32_t nq, mtblx_block_seek* qs, uint8_t* okeys,
                                                    uint64_t keys_cap, uint8_t* ovals, uint64_t vals_cap,
                                                    uint64_t* oke, uint64_t* ove, uint64_t* okcap, uint64_t rec_cap,
-                                                   uint8_t* kbuf, uint64_t kbuf_cap) {
+                                                   uint8_t* kbuf, uint64_t kbuf_cap, uint64_t* vsrc = nullptr) {
   __shared__ uint8_t stage[kSeekStage];
   __shared__ uint8_t Klds[GK ? 1 : kSeekKey];
   const int lane = threadIdx.x;
@@ -673,7 +676,11 @@ __global__ void __launch_bounds__(64) k_block_seek(const uint8_t* data, const ui
             kd[Q.key_bytes + j] = K[j];
           }
           uint64_t j0 = 0;
-          if (it.vlen >= 4096) {   // big values (blocks >= 4 GiB hold values of GiBs): 16 B per lane
+          if (DEFER) {
+            j0 = it.vlen;   // the caller copies the value (vsrc)
+            MTBLX_CHK(vsrc + (uint64_t)q * rec_cap + Q.nrec, 8);
+            if (lane == 0) vsrc[(uint64_t)q * rec_cap + Q.nrec] = it.voff;
+          } else if (it.vlen >= 4096) {   // big values (blocks >= 4 GiB hold values of GiBs): 16 B per lane
             typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
             const uint64_t nv = it.vlen / 16;
             const uint8_t* vs = d + it.voff;
@@ -969,6 +976,34 @@ extern "C" int mtblx_block_seek_batch_kbuf(const uint8_t* data, const uint8_t* k
                mtblx_rd::k_block_seek<true>, dim3(nq < 1024u ? nq : 1024u), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), data, keys, key_end, nq, q, out_keys, keys_cap, out_vals,
                      vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, key_buf, key_buf_cap);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_block_seek_batch_ex(const uint8_t* data, const uint8_t* keys, const uint64_t* key_end,
+                                         uint32_t nq, mtblx_block_seek* q, uint8_t* out_keys, uint64_t keys_cap,
+                                         uint8_t* out_vals, uint64_t vals_cap, uint64_t* key_end_out,
+                                         uint64_t* val_end_out, uint64_t* kcap_out, uint64_t rec_cap, uint8_t* key_buf,
+                                         uint64_t key_buf_cap, uint64_t* val_src_out, void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!data || !keys || !key_end || !q || !out_keys || !key_end_out || !val_end_out || !val_src_out ||
+      (key_buf && key_buf_cap == 0))
+    return MTBLX_E_INVAL;
+  const dim3 g(nq < 1024u ? nq : 1024u);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (key_buf)
+    MTBLX_LAUNCH((data, keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(q, sizeof(*q) * nq), MTBLX_R(out_keys, keys_cap * nq),
+                  MTBLX_R(key_end_out, 8 * rec_cap * nq), MTBLX_R(val_end_out, 8 * rec_cap * nq),
+                  MTBLX_R(kcap_out, 8 * rec_cap * nq), MTBLX_R(key_buf, key_buf_cap * nq),
+                  MTBLX_R(val_src_out, 8 * rec_cap * nq)),
+                 (mtblx_rd::k_block_seek<true, true>), g, dim3(64), 0, s, data, keys, key_end, nq, q, out_keys,
+                 keys_cap, out_vals, vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, key_buf, key_buf_cap,
+                 val_src_out);
+  else
+    MTBLX_LAUNCH((data, keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(q, sizeof(*q) * nq), MTBLX_R(out_keys, keys_cap * nq),
+                  MTBLX_R(key_end_out, 8 * rec_cap * nq), MTBLX_R(val_end_out, 8 * rec_cap * nq),
+                  MTBLX_R(kcap_out, 8 * rec_cap * nq), MTBLX_R(val_src_out, 8 * rec_cap * nq)),
+                 (mtblx_rd::k_block_seek<false, true>), g, dim3(64), 0, s, data, keys, key_end, nq, q, out_keys,
+                 keys_cap, out_vals, vals_cap, key_end_out, val_end_out, kcap_out, rec_cap, nullptr, 0, val_src_out);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
 

@@ -38,7 +38,7 @@ EXPORTS = [
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
     "mtblx_codec_available", "mtblx_decompress", "mtblx_compress", "mtblx_decompress_blocks", "mtblx_writer_set_level",
-    "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_block_seek_batch_kbuf", "mtblx_entry_offsets",
+    "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_block_seek_batch_kbuf", "mtblx_block_seek_batch_ex", "mtblx_copy_ranges", "mtblx_entry_offsets",
     "mtblx_key_filter",
 ]
 PLAN_OUT_OF_ORDER, PLAN_PANIC, PLAN_TOO_LONG = 1, 2, 4
@@ -211,6 +211,11 @@ def lib() -> C.CDLL:
         L.mtblx_block_seek_batch_kbuf.argtypes = L.mtblx_block_seek_batch.argtypes[:-1] + [C.c_void_p, C.c_uint64,
                                                                                           C.c_void_p]
         L.mtblx_block_seek_batch_kbuf.restype = C.c_int
+        L.mtblx_block_seek_batch_ex.argtypes = L.mtblx_block_seek_batch_kbuf.argtypes[:-1] + [C.c_void_p, C.c_void_p]
+        L.mtblx_block_seek_batch_ex.restype = C.c_int
+        L.mtblx_copy_ranges.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_uint32, C.c_uint64, C.c_void_p]
+        L.mtblx_copy_ranges.restype = C.c_int
         L.mtblx_entry_offsets.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                            C.c_void_p]
         L.mtblx_entry_offsets.restype = C.c_int

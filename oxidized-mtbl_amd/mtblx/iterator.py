@@ -93,13 +93,19 @@ class Emitted:
         return out
 
 
+_BIG_BLOCK = 64 << 20   # past this, the values move with the whole grid whatever the caller asks
+
+
 def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 << 62,
-               small_caps: bool = False, resume_off: int | None = None) -> Emitted:
+               small_caps: bool = False, resume_off: int | None = None, values: bool = True) -> Emitted:
     """BlockIter::seek(key) (key None: seek_to_first) on content = (tensor, off, len) with the
     given key capacity, then the records it yields until get() is None.  resume_off: instead
     of seeking, an iterator holding key bytes `key` and capacity kcap calls next(), which
     parses the entry at resume_off.  small_caps: start from small output buffers and size them
-    exactly from the first pass's counts (blocks of GiBs)."""
+    exactly from the first pass's counts, and move the value bytes with the whole grid
+    (mtblx_block_seek_batch_ex + mtblx_copy_ranges) instead of the seeking wave (blocks of GiBs).
+    values=False: the value bytes are not moved at all (the emission's key capacities only)."""
+    defer = small_caps or not values or content[2] > _BIG_BLOCK
     data, off, ln = content
     dev = data.device
     kb = _dev_bytes(key or b"", dev)
@@ -119,10 +125,15 @@ def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 <
         oke = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev)
         ove = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev)
         okc = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev)
+        vsrc = torch.empty(max(rec_cap, 1), dtype=torch.int64, device=dev) if defer else None
         args = [C.c_void_p(data.data_ptr()), C.c_void_p(kb.data_ptr()), C.c_void_p(ke.data_ptr()), 1,
                 C.c_void_p(qt.data_ptr()), C.c_void_p(okeys.data_ptr()), keys_cap, C.c_void_p(ovals.data_ptr()),
                 vals_cap, C.c_void_p(oke.data_ptr()), C.c_void_p(ove.data_ptr()), C.c_void_p(okc.data_ptr()), rec_cap]
-        if kbuf is None:
+        if defer:
+            rc = _lib.lib().mtblx_block_seek_batch_ex(*args, C.c_void_p(kbuf.data_ptr() if kbuf is not None else 0),
+                                                      kbuf.numel() if kbuf is not None else 0,
+                                                      C.c_void_p(vsrc.data_ptr()), C.c_void_p(codec._stream_handle(None)))
+        elif kbuf is None:
             rc = _lib.lib().mtblx_block_seek_batch(*args, C.c_void_p(codec._stream_handle(None)))
         else:
             rc = _lib.lib().mtblx_block_seek_batch_kbuf(*args, C.c_void_p(kbuf.data_ptr()), kbuf.numel(),
@@ -137,9 +148,28 @@ def block_seek(content, key: bytes | None, kcap: int = 0, max_records: int = 1 <
             continue
         if res.end != _lib.EMIT_OVERFLOW:
             n = int(res.nrec)
+            if defer and values and n:
+                _copy_values(data, off, vsrc[:n], ove[:n], ovals)
             return Emitted(res, okeys[: int(res.key_bytes)], ovals[: int(res.val_bytes)], oke[:n], ove[:n], okc[:n])
         rec_cap, keys_cap, vals_cap = int(res.nrec), int(res.key_bytes), int(res.val_bytes)
     raise RuntimeError("mtblx_block_seek_batch: output sizes did not converge")
+
+
+def _copy_values(data, off: int, vsrc, vend, ovals):
+    """the emitted records' values, block content offsets vsrc -> ovals at their END offsets vend
+    (mtblx_copy_ranges: every CU moves the GiBs)"""
+    start = torch.cat([torch.zeros(1, dtype=torch.int64, device=vend.device), vend[:-1]])
+    ln = vend - start
+    chunks = (ln + 15) // 16
+    base = torch.cumsum(chunks, 0) - chunks
+    total = int(chunks.sum().item())
+    src_off = (vsrc + off).contiguous()
+    rc = _lib.lib().mtblx_copy_ranges(C.c_void_p(data.data_ptr()), C.c_void_p(src_off.data_ptr()),
+                                      C.c_void_p(ovals.data_ptr()), C.c_void_p(start.data_ptr()),
+                                      C.c_void_p(ln.data_ptr()), C.c_void_p(base.data_ptr()), int(vend.numel()),
+                                      total, C.c_void_p(codec._stream_handle(None)))
+    if rc != 0:
+        raise RuntimeError(f"mtblx_copy_ranges failed: {rc}")
 
 
 def key_filter(keys: torch.Tensor, key_end: torch.Tensor, n: int, typ: int, k: bytes) -> int:
@@ -345,7 +375,7 @@ class _Bi:
         if not self.recs:
             return self.kcap_end
         if self.kcaps is None:   # records came from the bulk decoder: replay seek_to_first + next
-            em = block_seek(self.content, None, 0, len(self.recs))
+            em = block_seek(self.content, None, 0, len(self.recs), values=False)
             self.kcaps = em.kcaps.cpu().numpy().tolist()
         return int(self.kcaps[min(self.pos, len(self.recs) - 1)])
 

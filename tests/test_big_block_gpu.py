@@ -130,3 +130,49 @@ def test_compressed_blocks_over_4gib(oracle):
     exp2 = oracle.iter_script(data, "from", b"c", b"", [1, ("seek", b"e"), 1], verify=True)
     assert nxt == exp2["records"][1]
     note("get / seek ok")
+
+
+def test_copy_ranges_and_deferred_values(oracle):
+    """r05: the values of blocks >= 4 GiB are moved by the whole grid (mtblx_block_seek_batch_ex
+    leaves them to mtblx_copy_ranges) instead of the seeking wave.  mtblx_copy_ranges on ragged,
+    unaligned ranges (0..40 B and MiBs) equals the host copy; the deferred emission (small_caps,
+    and values=False for key capacities) equals the wave-copied one on ordinary blocks."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+    import corpus
+    from mtblx import _lib, codec, iterator
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 256, 12 << 20, dtype=np.uint8)
+    lens = [int(x) for x in rng.integers(0, 41, 200)] + [3 << 20, (1 << 20) + 7, 17, 0, 4099]
+    so = [int(rng.integers(0, src.size - n + 1)) for n in lens]
+    do, acc = [], 5
+    for n in lens:
+        do.append(acc)
+        acc += n + int(rng.integers(0, 3))
+    dst = np.zeros(acc + 16, np.uint8)
+    ch = [(n + 15) // 16 for n in lens]
+    cb = np.concatenate([[0], np.cumsum(ch)[:-1]]).astype(np.int64)
+    t = lambda a: torch.tensor(np.asarray(a, np.int64), device="cuda")   # noqa: E731
+    ds, dd = torch.from_numpy(src).to("cuda"), torch.from_numpy(dst).to("cuda")
+    args = [t(so), t(do), t(lens), t(cb)]
+    rc = _lib.lib().mtblx_copy_ranges(C.c_void_p(ds.data_ptr()), C.c_void_p(args[0].data_ptr()),
+                                      C.c_void_p(dd.data_ptr()), C.c_void_p(args[1].data_ptr()),
+                                      C.c_void_p(args[2].data_ptr()), C.c_void_p(args[3].data_ptr()), len(lens),
+                                      int(sum(ch)), C.c_void_p(codec._stream_handle(None)))
+    assert rc == 0
+    for a, b, n in zip(so, do, lens):
+        dst[b: b + n] = src[a: a + n]
+    assert np.array_equal(dd.cpu().numpy(), dst)
+    # deferred emission == the wave's own copies
+    for seed in (1, 2):
+        recs = corpus.random_records(np.random.default_rng(seed), 300, 0, 40, 0, 5000)
+        blk = oracle.build_block(recs, restart_interval=16)
+        d = torch.frombuffer(bytearray(b"\x00" * 3 + blk), dtype=torch.uint8).to("cuda")
+        content = (d, 3, len(blk))
+        a = iterator.block_seek(content, None)
+        b = iterator.block_seek(content, None, small_caps=True)
+        c = iterator.block_seek(content, None, values=False)
+        assert a.host_records() == b.host_records() == recs
+        assert torch.equal(a.kcaps, c.kcaps) and torch.equal(a.key_end, c.key_end) and torch.equal(a.val_end, c.val_end)

@@ -281,6 +281,54 @@ def test_fused_verify_decode(oracle):
 
 
 
+def _block_of_len(oracle, rng, L, iv, n, kmax):
+    """a BlockBuilder block of exactly L bytes: n records, keys 4..kmax B, the value bytes spread
+    so the content reaches L (the last value absorbs the varint-length steps)"""
+    recs = corpus.random_records(rng, n, 4, kmax, 0, 0)
+    need = L - len(oracle.build_block(recs, restart_interval=iv))
+    assert need >= 0
+    vl = [need // n] * n
+    for _ in range(8):
+        vl[-1] = max(0, vl[-1])
+        cur = [(k, bytes(rng.integers(0, 256, v, dtype=np.uint8))) for (k, _), v in zip(recs, vl)]
+        b = oracle.build_block(cur, restart_interval=iv)
+        if len(b) == L:
+            return b
+        vl[-1] += L - len(b)
+    raise AssertionError("block length not reached")
+
+
+def test_pipelarge_max_shapes(oracle):
+    """PipeLarge / PipeLargeV at their largest tile and block shapes, fused verify and
+    decode + CRC against the oracle: blocks of exactly the largest PipeLarge slot (65 601 B: one
+    per 65 664 B tile) with 64 restart intervals (the tile's interval capacity), 65 (one past),
+    one restart per entry, and a few long values; then blocks of 32 785 B (the largest two per
+    tile) with 32 intervals each (64 per tile)."""
+    codec = _dev()
+    import torch
+    rng = np.random.default_rng(2026)
+    batches = [
+        [_block_of_len(oracle, rng, 65601, 16, 1024, 24), _block_of_len(oracle, rng, 65601, 16, 1025, 24),
+         _block_of_len(oracle, rng, 65601, 1, 200, 40), _block_of_len(oracle, rng, 65601, 16, 40, 60),
+         _block_of_len(oracle, rng, 65601, 16, 300, 300), _block_of_len(oracle, rng, 60000, 7, 900, 30)],
+        [_block_of_len(oracle, rng, 32785, 16, 512, 24) for _ in range(5)] + [_block_of_len(oracle, rng, 32785, 1, 100, 40)],
+    ]
+    for blocks in batches:
+        blocks = blocks * 3
+        d, o, l = corpus.pack(blocks, rng=rng, lead=5)
+        for fused in (True, False):
+            batch = codec.DeviceBatch.from_host(d, o, l)
+            out, crc, bad = codec.decode_verify(batch, framed=False, fused=fused)
+            torch.cuda.synchronize()
+            dev = out.to_host()
+            orc = oracle.decode_blocks(d, o, l)
+            assert (orc.status == 0).all()
+            assert_same(dev, orc, o.size)
+            exp = np.array([oracle.crc32c(b) for b in blocks], np.uint32)
+            assert np.array_equal(crc.cpu().numpy().view(np.uint32), exp)
+            assert not bad.cpu().numpy().any()
+
+
 def _tail_records(rng, n, mode):
     """n strictly increasing keys for the copy waves' key-tail paths, random 0..64 B values.
     "counter": be64 counter with random gaps (shared ~5 B) + a random tail of 0..292 B, so every

@@ -49,6 +49,13 @@ if [ "$MODE" = fab ]; then   # fused verify A/B: the product vs build/libmtblx_$
   step fab_var64 300 env MTBLX_AB_CRC=1 $BB --block-size 65536 --blocks 6000 --lib $V
   grep -h -o '"decode_blocks_verify".*"vs_decode' $O/fab_*.log || true
 fi
+if [ "$MODE" = encab ]; then   # k_encode A/B on one cfg3 chunk: product vs build/libmtblx_<v>.so for v in $ENCV
+  B="python bench.py --config cfg3 --cfg3-blocks 100000 --steps 1 --warmup 0"
+  step encab_prod1 300 $B
+  for v in ${ENCV:-}; do step encab_$v 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
+  step encab_prod2 300 $B
+  grep -h -o '"encode_GiB_per_s": [0-9.]*' $O/encab_*.log || true
+fi
 if [ "$MODE" = spill ]; then
   step spill 700 python -u -m pytest tests/test_spill_gpu.py -v --timeout 650 --timeout-method thread
 fi

@@ -579,7 +579,9 @@ def run_cfg3(args, dist, world, rank):
         "decode_records_per_s": round(acc["records"] * world / (dec_ms * 1e-3), 1),
         "encode_GiB_per_s": round(bb / (enc_ms * 1e-3) / 2**30, 2),
         "encode_records_per_s": round(acc["records"] * world / (enc_ms * 1e-3), 1),
-        "plan_ms_total": round(acc["plan_ms"], 1), "scaling": "weak", "dtype": "u8",
+        "plan_ms_total": round(acc["plan_ms"], 1),
+        # the device Writer end to end: block cut (mtblx_encode_plan, wall clock per chunk) + encode
+        "writer_GiB_per_s": round(bb / ((enc_ms + _max_over_ranks(acc["plan_ms"], dist)) * 1e-3) / 2**30, 2), "scaling": "weak", "dtype": "u8",
         "data": "synthetic (device generator: Zipf 8..256 B keys = be64(counter) || random tail, 64 B random values)",
         "config": {"workload": "cfg3: 64 KiB blocks, restart_interval=16, compression=none, encode (framed) + decode",
                    "blocks_per_gpu": acc["blocks"], "records_per_gpu": acc["records"],

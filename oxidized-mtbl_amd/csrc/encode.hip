@@ -737,8 +737,10 @@ using namespace mtblx_enc;
 
 extern "C" size_t mtblx_encode_workspace_bytes(uint32_t nblk) { return 256u + 8ull * (uint64_t)nblk; }
 
-extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
-                                 uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
+// the round-1..4 block cut: one wave per shard walking the Writer's chain (plan.hip dispatches here
+// for MTBLX_PLAN=serial and record ranges of 2^32 or more)
+extern "C" int mtblx_encode_plan_serial(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
+                                        uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
                                  uint64_t* nblk_out, uint32_t* flags_out, void* stream) {
   if (!rec || !shard_rec || !nblk_out || nshard == 0) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

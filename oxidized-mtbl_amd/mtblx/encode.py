@@ -65,19 +65,16 @@ def plan(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16
     nb = C.c_uint64(0)
     fl = C.c_uint32(0)
     st = C.c_void_p(codec._stream_handle(stream))
+    # one call: every block holds >= 1 record, so the shards' record count + 1 always suffices
+    cap = max(recs.n, 0) + 1
+    blk = torch.empty(cap, dtype=torch.int64, device=dev)
     rc = L.mtblx_encode_plan(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size),
-                             int(restart_interval), None, 0, C.byref(nb), C.byref(fl), st)
+                             int(restart_interval), C.c_void_p(blk.data_ptr()), cap, C.byref(nb), C.byref(fl), st)
     if rc == _lib.MTBLX_E_FORMAT:
         raise WriterPanic(int(fl.value))
     if rc != 0:
-        raise RuntimeError(f"mtblx_encode_plan (count) failed: {rc}")
-    blk = torch.empty(int(nb.value) + 1, dtype=torch.int64, device=dev)
-    rc = L.mtblx_encode_plan(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size),
-                             int(restart_interval), C.c_void_p(blk.data_ptr()), blk.numel(), C.byref(nb), C.byref(fl),
-                             st)
-    if rc != 0:
         raise RuntimeError(f"mtblx_encode_plan failed: {rc}")
-    return blk
+    return blk[: int(nb.value) + 1]
 
 
 @dataclass

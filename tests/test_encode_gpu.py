@@ -120,6 +120,57 @@ def test_shards_are_independent_writers():
     assert np.array_equal(blk[:-1], np.concatenate(exp)) and blk[-1] == 4000
 
 
+def _plan_serial(recs, shard_rec, bs, iv, cap):
+    """the round-1..4 block cut (one wave per shard walking the Writer's chain), exported as
+    mtblx_encode_plan_serial: the parallel planner must cut exactly where it does"""
+    import ctypes as C
+    import torch
+    from mtblx import _lib, codec
+    L = _lib.lib()
+    f = L.mtblx_encode_plan_serial
+    f.argtypes = L.mtblx_encode_plan.argtypes
+    f.restype = C.c_int
+    blk = torch.empty(cap, dtype=torch.int64, device="cuda")
+    nb, fl = C.c_uint64(0), C.c_uint32(0)
+    rc_ = recs.cstruct()
+    rc = f(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), int(shard_rec.numel()) - 1, bs, iv, C.c_void_p(blk.data_ptr()),
+           cap, C.byref(nb), C.byref(fl), C.c_void_p(codec._stream_handle(None)))
+    return rc, int(fl.value), blk[: int(nb.value) + 1].cpu().numpy()
+
+
+def test_parallel_plan_equals_writer_chain():
+    """mtblx_encode_plan (r05: next(j) for every record from prefix sums + pointer doubling) cuts
+    exactly where the Writer does (src/writer.rs:125-130, src/block_builder.rs:40-62): against
+    the host Writer on small shapes, and against the serial device walk on large ones -- intervals
+    1..5000, block sizes 1 KiB..1 MiB, values far larger than the block (a record alone past the
+    size: one-record blocks), empty keys and values, empty and one-record shards, a shard of
+    more than 4096 blocks (the next^4096 level), many shards."""
+    enc = _enc()
+    import torch
+    from mtblx import synth
+    rng = np.random.default_rng(64)
+    for bs, iv, n, kmin, kmax, vmin, vmax in [(1024, 1, 500, 0, 30, 0, 40), (1024, 16, 600, 1, 20, 0, 3000),
+                                              (4096, 7, 2000, 0, 80, 0, 200), (9000, 100, 3000, 0, 40, 0, 60),
+                                              (1 << 20, 5000, 9000, 4, 60, 0, 300), (2048, 2, 1500, 0, 8, 0, 0),
+                                              (1500, 16, 800, 1, 30, 900, 2500)]:
+        recs = corpus.random_records(rng, n, kmin, kmax, vmin, vmax)
+        _, _, _, nrec = _writer_file(recs, bs, iv)
+        blk = enc.plan(enc.DeviceRecords.from_list(recs), bs, iv).cpu().numpy()
+        assert np.array_equal(np.diff(blk), nrec.astype(np.int64)), (bs, iv)
+    recs, _ = synth.cfg3_records_device(400_000, seed=9)
+    dev = recs.key_end.device
+    for bs, iv, cuts in [(65536, 16, [0, 400_000]), (1024, 16, [0, 400_000]), (4096, 3, [0, 1, 1, 2, 150_000, 150_000, 400_000]),
+                         (30000, 40, list(np.linspace(0, 400_000, 101).astype(int))), (2048, 1, [0, 123_457, 400_000])]:
+        sr = torch.tensor(cuts, dtype=torch.int64, device=dev)
+        got = enc.plan(recs, bs, iv, shard_rec=sr).cpu().numpy()
+        rc, fl, exp = _plan_serial(recs, sr, bs, iv, 400_002)
+        assert rc == 0 and fl == 0
+        assert np.array_equal(got, exp), (bs, iv, got.size, exp.size)
+    # interval 0: only one-record blocks are legal; the parallel walk reports the panic too
+    big = [(bytes([1, i]), bytes(3000)) for i in range(40)]
+    blk = enc.plan(enc.DeviceRecords.from_list(big), 2048, 0).cpu().numpy()
+    assert np.array_equal(blk, np.arange(41))
+
 def test_cfg3_roundtrip_sample(oracle):
     """cfg3 scheme on the device: plan -> encode -> decode == the generated records; a sample of
     blocks against the oracle builder and decoder"""

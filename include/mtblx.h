@@ -363,6 +363,16 @@ int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint3
                       uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
                       uint32_t* flags_out, void* stream);
 
+/* The same block cut, keeping what the encode needs (round 5): `plan` (device, 256-byte aligned,
+ * mtblx_plan_keep_bytes(number of records in the shards) bytes) receives every record's entry size
+ * summed in order, the bytes a restart entry loses by not sharing summed along residue classes
+ * mod restart_interval, and every record's shared-prefix length with its predecessor.
+ * restart_interval must be >= 1.  Returns like mtblx_encode_plan. */
+size_t mtblx_plan_keep_bytes(uint64_t nrec);
+int mtblx_encode_plan_keep(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
+                           uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
+                           uint32_t* flags_out, void* plan, size_t plan_bytes, void* stream);
+
 /* BlockBuilder::add for every record of a block, then finish (src/block_builder.rs:49-104),
  * for every block b of blk_rec at once.  framed != 0 adds write_block's framing before each
  * content (varint64 len | crc32c | content, src/writer.rs:203-237, CompressionType::None):
@@ -376,6 +386,15 @@ size_t mtblx_encode_workspace_bytes(uint32_t nblk);
 int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk_rec, uint32_t nblk, uint32_t restart_interval,
                         int framed, uint8_t* out, uint64_t out_cap, uint64_t* blk_off, uint32_t* blk_len,
                         int32_t* status, uint64_t* totals, void* workspace, size_t ws_bytes, void* stream);
+/* mtblx_encode_blocks reading a kept plan (mtblx_encode_plan_keep over the same records and
+ * restart_interval; blk_rec may be any cut of records inside it): every block's length and file
+ * offset come from the kept sums and one scan, so no block waits on its predecessors, and no
+ * entry's shared prefix is recomputed.  Output identical to mtblx_encode_blocks.  Asynchronous
+ * after one small synchronous read of the plan's header. */
+int mtblx_encode_blocks_planned(const mtblx_records* rec, const uint64_t* blk_rec, uint32_t nblk,
+                                uint32_t restart_interval, int framed, uint8_t* out, uint64_t out_cap,
+                                uint64_t* blk_off, uint32_t* blk_len, int32_t* status, uint64_t* totals,
+                                void* workspace, size_t ws_bytes, const void* plan, void* stream);
 
 /* Writer::into_inner's tail on the device (src/writer.rs:132-138, :155-181, :239-265;
  * src/metadata.rs:61-79) for ONE file whose data blocks mtblx_encode_blocks wrote framed:

@@ -81,7 +81,7 @@ __device__ __forceinline__ void rec_of(const Recs& R, uint64_t r, uint64_t& k0, 
 }
 
 // common prefix length of a[0..al) and b[0..bl); cmp = sign of a <=> b (lexicographic, Ord for [u8])
-__device__ uint64_t lcp_cmp(const uint8_t* a, uint64_t al, const uint8_t* b, uint64_t bl, int& cmp) {
+__device__ __forceinline__ uint64_t lcp_cmp(const uint8_t* a, uint64_t al, const uint8_t* b, uint64_t bl, int& cmp) {
   const uint64_t m = al < bl ? al : bl;
   uint64_t i = 0;
   while (i + 8 <= m) {
@@ -254,7 +254,22 @@ struct EncArgs {
   uint64_t* totals;          // [2]: bytes written, flags
   uint32_t* ticket;
   uint64_t* lbw;             // [nblk] look-back words
+  // planned mode (mtblx_encode_blocks_planned): the block cut's kept sums, local to record plo
+  const uint64_t* PA;        // inclusive prefix of the entry sizes with sharing
+  const uint64_t* Q;         // inclusive prefix of the restart savings along residue classes mod interval
+  const uint32_t* SH;        // shared-prefix length with the previous record
+  uint64_t plo, pm;          // the plan's first record and record count
+  const uint64_t* fincl;     // [nblk] inclusive prefix of the framed block sizes (the file offsets)
 };
+
+// planned mode: the byte offset of entry i (0 <= i <= n) in a block whose first record is local
+// record j0 (src/block_builder.rs:49-83: entries before i, restart entries without sharing)
+__device__ __forceinline__ uint64_t planned_off(const EncArgs& a, uint64_t j0, uint64_t i, uint32_t iv) {
+  if (i == 0) return 0;
+  const uint64_t last = j0 + (uint64_t)iv * ((i - 1) / iv);
+  MTBLX_CHK(a.PA + j0 + i - 1, 8), MTBLX_CHK(a.Q + last, 8);
+  return a.PA[j0 + i - 1] - (j0 ? a.PA[j0 - 1] : 0) + a.Q[last] - (j0 >= iv ? a.Q[j0 - iv] : 0);
+}
 
 struct alignas(16) EncLds {
   uint8_t ob[kLdsBlock];
@@ -335,7 +350,7 @@ __device__ __forceinline__ uint32_t crc_word(const EncLds& S, uint32_t c, uint32
   return S.T[3][c & 0xffu] ^ S.T[2][(c >> 8) & 0xffu] ^ S.T[1][(c >> 16) & 0xffu] ^ S.T[0][c >> 24];
 }
 
-__device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
+__device__ __forceinline__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t acc = 0;
   if (L >= 4) {
@@ -386,7 +401,7 @@ __device__ uint32_t wg_crc32c(EncLds& S, const uint8_t* d, uint64_t L) {
 // (crc_mfma_part, no barrier: wave 0 runs the look-back first); after a barrier the waves'
 // parts are XOR-combined and the pad is removed by x^(-8t) (crc_mfma_final).  The operands come
 // from constant memory.
-__device__ void crc_mfma_part(EncLds& S, uint32_t L) {
+__device__ __forceinline__ void crc_mfma_part(EncLds& S, uint32_t L) {
   using namespace mtblx_crc;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, n = lane & 15;
   const uint32_t t = (16u - (L & 15u)) & 15u, Lp = L + t;
@@ -431,7 +446,7 @@ __device__ void crc_mfma_part(EncLds& S, uint32_t L) {
   if (lane == 0) S.redf[w] = C;
 }
 // after a barrier that follows every wave's crc_mfma_part
-__device__ uint32_t crc_mfma_final(const EncLds& S, uint32_t L) {
+__device__ __forceinline__ uint32_t crc_mfma_final(const EncLds& S, uint32_t L) {
   const int lane = threadIdx.x & 63;
   const uint32_t t = (16u - (L & 15u)) & 15u;
   uint32_t r = 0;
@@ -450,11 +465,16 @@ struct Ent {
   uint64_t k0, kl, v0, vl, sh;
 };
 __device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, uint32_t iv,
-                                        const uint16_t* shc = nullptr) {
+                                        const uint16_t* shc = nullptr, const uint32_t* SH = nullptr) {
   Ent e;
   rec_of(R, r0 + i, e.k0, e.kl, e.v0, e.vl);
   e.sh = 0;
-  if (shc && i < kShCache && shc[i] != 0xFFFFu) {
+  if (SH) {   // planned: the block cut kept every record's shared-prefix length
+    if (shares(i, iv)) {
+      MTBLX_CHK(SH + i, 4);
+      e.sh = SH[i];
+    }
+  } else if (shc && i < kShCache && shc[i] != 0xFFFFu) {
     e.sh = shc[i];
   } else if (shares(i, iv)) {
     uint64_t pk0, pkl, pv0, pvl;
@@ -497,7 +517,7 @@ __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent
   copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys);
   copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl, R.vals);
 }
-__device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
+__device__ __forceinline__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
   uint64_t excl = 0;
   int64_t j = (int64_t)b - 1;
   while (j >= 0) {
@@ -537,6 +557,7 @@ __device__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeo
 #define ESTAMP(k) do { } while (0)
 #endif
 
+template <bool PL>   // PL: planned mode (sizes and offsets from the block cut's sums; no look-back)
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MTBLX_ENC_WPE))) k_encode(EncArgs a) {   // 2 per CU
   __shared__ EncLds S;
 #ifdef MTBLX_ENC_STAMPS
@@ -559,9 +580,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 #if !MTBLX_ENC_LAZY_T
   build_tables();
 #endif
-  if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
-  __syncthreads();
-  const uint32_t b = S.sh_u32[0];
+  uint32_t b = blockIdx.x;
+  if constexpr (!PL) {   // ticket order: every earlier block is running or done (the look-back)
+    if (tid == 0) S.sh_u32[0] = atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    b = S.sh_u32[0];
+  }
   if (b >= a.nblk) return;
   const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
   const uint32_t iv = a.interval;
@@ -569,6 +593,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 
   // ---- phase A: the content length (entries + restart array + count) ----
   uint64_t part = 0;
+  // planned mode: the block's record range must lie in the plan
+  const bool pl_ok = !PL || (r0 >= a.plo && r0 + n <= a.plo + a.pm);
+  const uint64_t j0 = PL ? r0 - a.plo : 0;
 #if MTBLX_ENC_CONTIG
   // thread t owns the contiguous entries [i0, i1) (balanced: floor(n / threads) or one more
   // each): the scan of its byte total is the offset of its first entry, so phase B runs through
@@ -576,8 +603,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   // for the longest entry (Zipf keys).  (Phase A reading coalesced, entry i on thread i mod
   // threads, and handing the sizes over in LDS measured slower: 1043 vs 1069 GiB/s.)
   const uint64_t i0 = n * (uint64_t)tid / kThreads, i1 = n * (uint64_t)(tid + 1) / kThreads;
-  for (uint64_t i = i0; i < i1; ++i) {
+  for (uint64_t i = i0; i < i1 && !PL; ++i) {
 #else
+  static_assert(!PL, "planned mode needs MTBLX_ENC_CONTIG");
   for (uint64_t i = tid; i < n; i += kThreads) {
 #endif
     const Ent e = entry_of(a.R, r0, i, iv);
@@ -585,17 +613,27 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     if (i < kShCache)
       S.shc[i] = e.sh < 0xFFFFu ? (uint16_t)e.sh : (uint16_t)0xFFFFu;
   }
-  uint64_t entries = 0;
-  const uint64_t tbase = wg_excl_scan(S, part, entries);
+  uint64_t entries = 0, tbase = 0;
+  if constexpr (PL) {   // the sums give every offset: no size pass, no scan
+    if (pl_ok) {
+      entries = planned_off(a, j0, n, iv);
+#if MTBLX_ENC_CONTIG
+      tbase = planned_off(a, j0, i0, iv);
+#endif
+    }
+  } else {
+    tbase = wg_excl_scan(S, part, entries);
+  }
   (void)tbase;
   // restarts: [0] + one push per restart entry (src/block_builder.rs:21, :60)
   const uint64_t nrest = n == 0 ? 1 : (iv == 0 ? 2 : 1 + (n - 1) / iv);
   int32_t st = MTBLX_ST_OK;
+  if (!pl_ok) st = MTBLX_ST_UNSUPPORTED;                   // planned mode: records outside the plan
   if (iv == 0 && n > 1) st = MTBLX_ST_CORRUPT;            // assert!(counter <= interval) (:50)
   if (entries > 0xFFFFFFFFull) st = MTBLX_ST_UNSUPPORTED;  // u64 restart arrays: blocks >= 4 GiB
   const uint64_t L = entries + 4 * nrest + 4;
   const uint64_t F = a.framed ? vlen64(L) + 4 + L : L;
-  if (tid == 0) {   // publish this block's framed size as early as possible
+  if (!PL && tid == 0) {   // publish this block's framed size as early as possible
     __hip_atomic_store(a.lbw + b, (b == 0 ? kIncl : kAgg) | F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const bool in_lds = L <= kLdsBlock && st == MTBLX_ST_OK;
@@ -608,10 +646,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 #if MTBLX_ENC_CONTIG
     uint64_t eo = tbase;
     Ent en{};   // the next entry's fields are loaded before this entry's bytes move
-    if (i0 < i1) en = entry_of(a.R, r0, i0, iv, S.shc);
+    const uint32_t* SHb = PL ? a.SH + j0 : nullptr;
+    if (i0 < i1) en = entry_of(a.R, r0, i0, iv, S.shc, SHb);
     for (uint64_t i = i0; i < i1; ++i) {
       const Ent e = en;
-      if (i + 1 < i1) en = entry_of(a.R, r0, i + 1, iv, S.shc);
+      if (i + 1 < i1) en = entry_of(a.R, r0, i + 1, iv, S.shc, SHb);
       const uint64_t sz = entry_bytes(e.sh, e.kl, e.vl);
       {
 #else
@@ -661,9 +700,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   const bool crc_mfma = MTBLX_ENC_CRC_MFMA && a.framed && in_lds && L >= 4;
   if (crc_mfma) {
     __syncthreads();   // the assembled block (entries, restarts, count, pad) before its CRC
-    if (w != 0) crc_mfma_part(S, (uint32_t)L);
+    if (w != 0 || PL) crc_mfma_part(S, (uint32_t)L);
   }
-  if (w == 0) {
+  if constexpr (PL) {   // the file offset: the scan of the framed sizes
+    if (tid == 0) S.sh_u64[0] = pl_ok ? a.fincl[b] - F : 0;
+  } else if (w == 0) {
     bool to = false;
     const uint64_t excl = b == 0 ? 0 : lookback(a, b, lane, to);
     if (lane == 0) {
@@ -735,7 +776,37 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 
 using namespace mtblx_enc;
 
-extern "C" size_t mtblx_encode_workspace_bytes(uint32_t nblk) { return 256u + 8ull * (uint64_t)nblk; }
+namespace mtblx_plan {   // plan.hip
+uint64_t sscan_words(uint64_t m, uint64_t w);
+int sscan(uint64_t* X, uint64_t m, uint64_t w, uint64_t* S, hipStream_t s);
+}
+
+namespace mtblx_enc {
+// planned mode: every block's framed size from the kept sums (the same formula k_encode applies)
+__global__ void __launch_bounds__(256) k_enc_fsize(EncArgs a, uint64_t* F) {
+  const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nblk) return;
+  MTBLX_CHK(a.blk_rec + b, 16);
+  const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
+  const uint32_t iv = a.interval;
+  uint64_t f = 0;
+  if (r0 >= a.plo && r0 + n <= a.plo + a.pm) {
+    const uint64_t entries = planned_off(a, r0 - a.plo, n, iv);
+    const uint64_t nrest = n == 0 ? 1 : 1 + (n - 1) / iv;
+    const uint64_t L = entries + 4 * nrest + 4;
+    f = a.framed ? vlen64(L) + 4 + L : L;
+  }
+  MTBLX_CHK(F + b, 8);
+  F[b] = f;
+}
+}  // namespace mtblx_enc
+
+extern "C" size_t mtblx_encode_workspace_bytes(uint32_t nblk) {
+  // look-back words (mtblx_encode_blocks) or the framed sizes + their scan (..._planned)
+  const uint64_t lb = 256u + 8ull * (uint64_t)nblk;
+  const uint64_t pl = 256u + 8ull * (uint64_t)nblk + 8ull * mtblx_plan::sscan_words(nblk, 1) + 256u;
+  return lb > pl ? lb : pl;
+}
 
 // the round-1..4 block cut: one wave per shard walking the Writer's chain (plan.hip dispatches here
 // for MTBLX_PLAN=serial and record ranges of 2^32 or more)
@@ -814,6 +885,42 @@ extern "C" int mtblx_encode_blocks(const mtblx_records* rec, const uint64_t* blk
             totals,
             reinterpret_cast<uint32_t*>(ws),
             reinterpret_cast<uint64_t*>(ws + 256)};
-  MTBLX_LAUNCH((rec->keys, rec->key_end, rec->vals, rec->val_end, blk_rec, out, blk_off, blk_len, status, totals, workspace), k_encode, dim3(nblk), dim3(kThreads), 0, s, a);
+  MTBLX_LAUNCH((rec->keys, rec->key_end, rec->vals, rec->val_end, blk_rec, out, blk_off, blk_len, status, totals, workspace), k_encode<false>, dim3(nblk), dim3(kThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
+
+extern "C" int mtblx_encode_blocks_planned(const mtblx_records* rec, const uint64_t* blk_rec, uint32_t nblk,
+                                           uint32_t restart_interval, int framed, uint8_t* out, uint64_t out_cap,
+                                           uint64_t* blk_off, uint32_t* blk_len, int32_t* status, uint64_t* totals,
+                                           void* workspace, size_t ws_bytes, const void* plan, void* stream) {
+  if (!rec || !blk_rec || !totals || !plan) return MTBLX_E_INVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint64_t h[4] = {0, 0, 0, 0};   // magic, first record, records, interval (plan.hip KeepHdr)
+  if (hipMemcpyAsync(h, plan, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return MTBLX_E_HIP;
+  if (h[0] != 0x4e414c5058544d31ull || h[3] != restart_interval || restart_interval == 0) return MTBLX_E_INVAL;
+  if (hipMemsetAsync(totals, 0, 16, s) != hipSuccess) return MTBLX_E_HIP;
+  if (nblk == 0) return MTBLX_OK;
+  if (!out || !blk_off || !blk_len || !status || !workspace || ws_bytes < mtblx_encode_workspace_bytes(nblk) ||
+      (reinterpret_cast<uintptr_t>(workspace) & 7u))
+    return MTBLX_E_INVAL;
+  const uint64_t m = h[2];
+  const uint8_t* kp = static_cast<const uint8_t*>(plan) + 256;
+  const uint64_t* PA = reinterpret_cast<const uint64_t*>(kp);
+  const uint64_t* Q = PA + (m + 1);
+  const uint32_t* SH = reinterpret_cast<const uint32_t*>(Q + (m + 1));
+  uint64_t* F = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(workspace) + 256);
+  uint64_t* scr = F + nblk;
+  EncArgs a{{rec->keys, rec->key_end, rec->vals, rec->val_end},
+            blk_rec, nblk, restart_interval, framed ? 1 : 0, out, out_cap, blk_off, blk_len, status, totals,
+            nullptr, nullptr, PA, Q, SH, h[1], m, F};
+  MTBLX_LAUNCH((MTBLX_R(blk_rec, 8ull * (nblk + 1)), MTBLX_R(PA, 8 * m), MTBLX_R(Q, 8 * m), MTBLX_R(F, 8ull * nblk)),
+               k_enc_fsize, dim3((nblk + 255) / 256), dim3(256), 0, s, a, F);
+  if (hipGetLastError() != hipSuccess) return MTBLX_E_HIP;
+  const int rc = mtblx_plan::sscan(F, nblk, 1, scr, s);
+  if (rc != MTBLX_OK) return rc;
+  MTBLX_LAUNCH((rec->keys, rec->key_end, rec->vals, rec->val_end, MTBLX_R(blk_rec, 8ull * (nblk + 1)), out, blk_off, blk_len,
+                status, totals, MTBLX_R(PA, 8 * m), MTBLX_R(Q, 8 * m), MTBLX_R(SH, 4 * m), MTBLX_R(F, 8ull * nblk)),
+               k_encode<true>, dim3(nblk), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }

@@ -89,6 +89,7 @@ struct RecArgs {
   uint64_t* G;          // [m] 15 + |key| + |value|: the flush test's record term
   uint64_t* GM;         // [ceil(m / 64)] max G per 64-record chunk
   uint32_t* flags;
+  uint32_t* SH;         // nullable: [m] the shared-prefix length with the previous record (kept for the encode)
 };
 
 // per record: sizes, the order check (key > predecessor within the shard) and the length limit
@@ -139,6 +140,10 @@ __global__ void __launch_bounds__(kT) k_plan_rec(RecArgs a) {
       a.A[j] = A;
       a.D[j] = Z - A;
       a.G[j] = g;
+      if (a.SH) {
+        MTBLX_CHK(a.SH + j, 4);
+        a.SH[j] = (uint32_t)(sh < 0xFFFFFFFFull ? sh : 0xFFFFFFFFull);
+      }
     }
     // the chunk's largest record term (a wave = one aligned 64-record chunk)
     uint64_t mx = g;
@@ -585,9 +590,16 @@ int sscan(uint64_t* X, uint64_t m, uint64_t w, uint64_t* S, hipStream_t s) {
 
 using namespace mtblx_plan;
 
-extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
-                                 uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
-                                 uint64_t* nblk_out, uint32_t* flags_out, void* stream) {
+// the kept plan (mtblx_encode_plan_keep): header, then PA [m] u64, Q [m] u64, SH [m] u32
+struct KeepHdr {
+  uint64_t magic, lo, m, iv;
+};
+constexpr uint64_t kKeepMagic = 0x4e414c5058544d31ull;   // "1MTXPLAN"
+inline size_t keep_bytes(uint64_t n) { return 256 + 16 * (n + 1) + 4 * (n + 1) + 256; }
+
+static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
+                     uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
+                     uint32_t* flags_out, void* keep, size_t keep_cap, void* stream) {
   if (!rec || !shard_rec || !nblk_out || nshard == 0) return MTBLX_E_INVAL;
   static const int serial = [] {
     const char* e = getenv("MTBLX_PLAN");
@@ -613,7 +625,9 @@ extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard
     if (sh[i + 1] < sh[i]) return MTBLX_E_INVAL;
   if (hi > rec->n) return MTBLX_E_INVAL;
   const uint64_t m = hi - lo;
-  if (serial || m >= 0xFFFFFFF0ull)
+  if (keep && (keep_cap < keep_bytes(m) || (reinterpret_cast<uintptr_t>(keep) & 255u) || restart_interval == 0))
+    return MTBLX_E_INVAL;
+  if (!keep && (serial || m >= 0xFFFFFFF0ull))
     return mtblx_encode_plan_serial(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out,
                                     flags_out, stream);
   if (block_size < 1024) block_size = 1024;   // WriterBuilder::block_size clamp (src/writer.rs:43-46)
@@ -651,7 +665,8 @@ extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard
   if (hipMalloc(reinterpret_cast<void**>(&ws), off) != hipSuccess) return MTBLX_E_HIP;
   auto p64 = [&](size_t o) { return reinterpret_cast<uint64_t*>(ws + o); };
   auto p32 = [&](size_t o) { return reinterpret_cast<uint32_t*>(ws + o); };
-  uint64_t *A = p64(oA), *D = p64(oD), *G = p64(oG), *GM = p64(oGM), *S = p64(oS), *dsb = p64(oSB), *db12 = p64(oB12),
+  uint64_t *A = keep ? reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(keep) + 256) : p64(oA),
+           *D = keep ? A + (m + 1) : p64(oD), *G = p64(oG), *GM = p64(oGM), *S = p64(oS), *dsb = p64(oSB), *db12 = p64(oB12),
            *dnb = p64(oNB), *dbb = p64(oBB), *mx = p64(oMX);
   uint32_t *fl = p32(oFL), *bnd = p32(oE), *J0 = p32(oJ0), *T1 = p32(oT1), *T2 = p32(oT2), *J6 = p32(oJ6),
            *J12 = p32(oJ12), *n12 = p32(oN12), *W12 = p32(oW12), *n6 = p32(oN6), *W6 = p32(oW6);
@@ -666,9 +681,11 @@ extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard
     if (!ok(hipMemcpyAsync(db12, base12.data(), 8ull * (nshard + 1), hipMemcpyHostToDevice, s))) break;
     if (!ok(hipMemsetAsync(ws + oFL, 0, 4, s))) break;   // flags
     if (m) {
-      RecArgs ra{{rec->keys, rec->key_end, rec->vals, rec->val_end}, lo, m, dsb, nshard, A, D, G, GM, fl};
+      uint32_t* SH = keep ? reinterpret_cast<uint32_t*>(D + (m + 1)) : nullptr;
+      RecArgs ra{{rec->keys, rec->key_end, rec->vals, rec->val_end}, lo, m, dsb, nshard, A, D, G, GM, fl, SH};
       MTBLX_LAUNCH((MTBLX_R(rec->key_end, 8 * hi), MTBLX_R(rec->val_end, 8 * hi), rec->keys, MTBLX_R(dsb, 8 * (nshard + 1)),
-                    MTBLX_R(A, 8 * m), MTBLX_R(D, 8 * m), MTBLX_R(G, 8 * m), MTBLX_R(GM, 8 * nchunk), MTBLX_R(fl, 4)),
+                    MTBLX_R(A, 8 * m), MTBLX_R(D, 8 * m), MTBLX_R(G, 8 * m), MTBLX_R(GM, 8 * nchunk), MTBLX_R(fl, 4),
+                    SH ? MTBLX_R(SH, 4 * m) : MTBLX_R(nullptr, 0)),
                    k_plan_rec, dim3((unsigned)std::min<uint64_t>(grid_of(m), 8192)), dim3(kT), 0, s, ra);
       if (!ok(hipMemsetAsync(mx, 0, 8, s))) break;
       MTBLX_LAUNCH((MTBLX_R(GM, 8 * nchunk), MTBLX_R(mx, 8)), k_plan_gmax,
@@ -731,10 +748,32 @@ extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard
     if (!ok(hipMemcpyAsync(&flags, fl, 4, hipMemcpyDeviceToHost, s))) break;
     ok(hipStreamSynchronize(s));
   } while (false);
+  if (rc == MTBLX_OK && keep) {
+    const KeepHdr h{kKeepMagic, lo, m, restart_interval};
+    if (hipMemcpyAsync(keep, &h, sizeof(h), hipMemcpyHostToDevice, s) != hipSuccess) rc = MTBLX_E_HIP;
+  }
   if (hipStreamSynchronize(s) != hipSuccess && rc == MTBLX_OK) rc = MTBLX_E_HIP;
   (void)hipFree(ws);
   *nblk_out = total;
   if (flags_out) *flags_out = flags;
   if (rc == MTBLX_OK && (flags & (MTBLX_PLAN_OUT_OF_ORDER | MTBLX_PLAN_PANIC | MTBLX_PLAN_TOO_LONG))) rc = MTBLX_E_FORMAT;
   return rc;
+}
+
+extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
+                                 uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
+                                 uint64_t* nblk_out, uint32_t* flags_out, void* stream) {
+  return plan_impl(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out, flags_out, nullptr,
+                   0, stream);
+}
+
+extern "C" size_t mtblx_plan_keep_bytes(uint64_t nrec) { return keep_bytes(nrec); }
+
+extern "C" int mtblx_encode_plan_keep(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
+                                      uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
+                                      uint64_t* nblk_out, uint32_t* flags_out, void* plan, size_t plan_bytes,
+                                      void* stream) {
+  if (!plan) return MTBLX_E_INVAL;
+  return plan_impl(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out, flags_out, plan,
+                   plan_bytes, stream);
 }

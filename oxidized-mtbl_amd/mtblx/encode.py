@@ -53,9 +53,10 @@ class DeviceRecords:
 
 
 def plan(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16, shard_rec=None,
-         stream=None) -> torch.Tensor:
+         stream=None, keep: bool = False):
     """-> blk_rec (device int64 [nblk + 1]): block b = records [blk_rec[b], blk_rec[b+1]).
-    shard_rec: record boundaries of independent Writers (default: one Writer over all)."""
+    shard_rec: record boundaries of independent Writers (default: one Writer over all).
+    keep=True (restart_interval >= 1): -> (blk_rec, Plan), the cut's sums kept for encode_into."""
     L = codec._require_device()
     dev = recs.key_end.device
     if shard_rec is None:
@@ -68,13 +69,29 @@ def plan(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16
     # one call: every block holds >= 1 record, so the shards' record count + 1 always suffices
     cap = max(recs.n, 0) + 1
     blk = torch.empty(cap, dtype=torch.int64, device=dev)
-    rc = L.mtblx_encode_plan(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size),
-                             int(restart_interval), C.c_void_p(blk.data_ptr()), cap, C.byref(nb), C.byref(fl), st)
+    args = [C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size), int(restart_interval),
+            C.c_void_p(blk.data_ptr()), cap, C.byref(nb), C.byref(fl)]
+    kept = None
+    if keep:
+        kb = int(L.mtblx_plan_keep_bytes(recs.n))
+        kept = Plan(torch.empty(kb, dtype=torch.uint8, device=dev), int(restart_interval))
+        rc = L.mtblx_encode_plan_keep(*args, C.c_void_p(kept.buf.data_ptr()), kb, st)
+    else:
+        rc = L.mtblx_encode_plan(*args, st)
     if rc == _lib.MTBLX_E_FORMAT:
         raise WriterPanic(int(fl.value))
     if rc != 0:
         raise RuntimeError(f"mtblx_encode_plan failed: {rc}")
-    return blk[: int(nb.value) + 1]
+    blk = blk[: int(nb.value) + 1]
+    return (blk, kept) if keep else blk
+
+
+@dataclass
+class Plan:
+    """the block cut's kept sums (mtblx_encode_plan_keep): lets encode_into skip the size pass and
+    the look-back (mtblx_encode_blocks_planned)"""
+    buf: torch.Tensor
+    restart_interval: int
 
 
 @dataclass
@@ -116,24 +133,28 @@ class EncodeBuffers:
 
 
 def encode_into(recs: DeviceRecords, blk_rec: torch.Tensor, bufs: EncodeBuffers, restart_interval: int = 16,
-                framed: bool = True, stream=None) -> Encoded:
+                framed: bool = True, stream=None, plan: "Plan | None" = None) -> Encoded:
+    """mtblx_encode_blocks; with a kept plan (plan(..., keep=True)) mtblx_encode_blocks_planned"""
     L = codec._require_device()
     nblk = int(blk_rec.numel()) - 1
     rc_ = recs.cstruct()
-    rc = L.mtblx_encode_blocks(C.byref(rc_), C.c_void_p(blk_rec.data_ptr()), nblk, int(restart_interval),
-                               1 if framed else 0, C.c_void_p(bufs.out.data_ptr()), bufs.out.numel(),
-                               C.c_void_p(bufs.blk_off.data_ptr()), C.c_void_p(bufs.blk_len.data_ptr()),
-                               C.c_void_p(bufs.status.data_ptr()), C.c_void_p(bufs.totals.data_ptr()),
-                               C.c_void_p(bufs.ws.data_ptr()), bufs.ws_bytes, C.c_void_p(codec._stream_handle(stream)))
+    args = [C.byref(rc_), C.c_void_p(blk_rec.data_ptr()), nblk, int(restart_interval), 1 if framed else 0,
+            C.c_void_p(bufs.out.data_ptr()), bufs.out.numel(), C.c_void_p(bufs.blk_off.data_ptr()),
+            C.c_void_p(bufs.blk_len.data_ptr()), C.c_void_p(bufs.status.data_ptr()), C.c_void_p(bufs.totals.data_ptr()),
+            C.c_void_p(bufs.ws.data_ptr()), bufs.ws_bytes]
+    if plan is not None:
+        rc = L.mtblx_encode_blocks_planned(*args, C.c_void_p(plan.buf.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
+    else:
+        rc = L.mtblx_encode_blocks(*args, C.c_void_p(codec._stream_handle(stream)))
     if rc != 0:
         raise RuntimeError(f"mtblx_encode_blocks failed: {rc}")
     return Encoded(bufs.out, bufs.blk_off[:nblk], bufs.blk_len[:nblk], bufs.status[:nblk], bufs.totals)
 
 
 def encode_blocks(recs: DeviceRecords, blk_rec: torch.Tensor, restart_interval: int = 16, framed: bool = True,
-                  stream=None) -> Encoded:
+                  stream=None, plan: "Plan | None" = None) -> Encoded:
     bufs = EncodeBuffers(recs, int(blk_rec.numel()) - 1, device=recs.key_end.device)
-    return encode_into(recs, blk_rec, bufs, restart_interval, framed, stream)
+    return encode_into(recs, blk_rec, bufs, restart_interval, framed, stream, plan)
 
 
 def write_file(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16, stream=None) -> torch.Tensor:
@@ -143,11 +164,15 @@ def write_file(recs: DeviceRecords, block_size: int = 8192, restart_interval: in
     to Writer::into_inner for the same records (CompressionType::None)."""
     L = codec._require_device()
     dev = recs.key_end.device
-    blk = plan(recs, block_size, restart_interval, stream=stream)
+    kept = None
+    if restart_interval >= 1:   # the cut's sums drive the encode (no size pass, no look-back)
+        blk, kept = plan(recs, block_size, restart_interval, stream=stream, keep=True)
+    else:
+        blk = plan(recs, block_size, restart_interval, stream=stream)
     nblk = int(blk.numel()) - 1
     kbytes = int(recs.key_end[-1].item()) if recs.n else 0
     if nblk:
-        e = encode_blocks(recs, blk, restart_interval, framed=True, stream=stream)
+        e = encode_blocks(recs, blk, restart_interval, framed=True, stream=stream, plan=kept)
         torch.cuda.synchronize()
         e.check()
         if int(e.totals[1].item()) & 1:

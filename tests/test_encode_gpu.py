@@ -171,6 +171,51 @@ def test_parallel_plan_equals_writer_chain():
     blk = enc.plan(enc.DeviceRecords.from_list(big), 2048, 0).cpu().numpy()
     assert np.array_equal(blk, np.arange(41))
 
+
+def test_planned_encode_equals_encode():
+    """mtblx_encode_blocks_planned (the block cut's kept sums: no size pass, no look-back) writes
+    exactly what mtblx_encode_blocks writes -- framed and unframed, the Writer's cut and arbitrary
+    cuts inside the plan (0-record blocks included), intervals 1..40, blocks past the LDS buffer
+    (assembled in HBM), cfg3 shards; a cut outside the plan is rejected per block."""
+    enc = _enc()
+    import torch
+    from mtblx import synth
+    rng = np.random.default_rng(65)
+
+    def same(a, b, nb):
+        for x, y in ((a.blk_off, b.blk_off), (a.blk_len, b.blk_len), (a.status, b.status)):
+            assert torch.equal(x[:nb], y[:nb])
+        assert torch.equal(a.totals, b.totals)
+        t = int(a.totals[0].item())
+        assert torch.equal(a.out[:t], b.out[:t])
+
+    for bs, iv, n, kmax, vmax in [(4096, 16, 3000, 80, 200), (1024, 1, 800, 20, 10), (8192, 3, 2000, 300, 50),
+                                  (65536, 40, 4000, 60, 120), (200_000, 16, 3000, 40, 150)]:
+        recs = corpus.random_records(rng, n, 0, kmax, 0, vmax)
+        d = enc.DeviceRecords.from_list(recs)
+        blk, kept = enc.plan(d, bs, iv, keep=True)
+        assert torch.equal(blk, enc.plan(d, bs, iv))
+        for framed in (True, False):
+            a = enc.encode_blocks(d, blk, iv, framed=framed)
+            b = enc.encode_blocks(d, blk, iv, framed=framed, plan=kept)
+            same(a, b, blk.numel() - 1)
+        cuts = np.sort(rng.integers(0, n + 1, 30))
+        arb = torch.tensor(np.concatenate([[0], cuts, [n]]), dtype=torch.int64, device="cuda")
+        a = enc.encode_blocks(d, arb, iv, framed=True)
+        b = enc.encode_blocks(d, arb, iv, framed=True, plan=kept)
+        same(a, b, arb.numel() - 1)
+    recs, _ = synth.cfg3_records_device(200_000, seed=4)
+    sr = torch.tensor([0, 70_000, 200_000], dtype=torch.int64, device="cuda")
+    blk, kept = enc.plan(recs, 65536, 16, shard_rec=sr, keep=True)
+    same(enc.encode_blocks(recs, blk, 16), enc.encode_blocks(recs, blk, 16, plan=kept), blk.numel() - 1)
+    # a plan over the second shard only: blocks outside it are refused (UNSUPPORTED), the rest exact
+    sr2 = torch.tensor([70_000, 200_000], dtype=torch.int64, device="cuda")
+    blk2, kept2 = enc.plan(recs, 65536, 16, shard_rec=sr2, keep=True)
+    mix = torch.cat([blk[:3], blk2])
+    e = enc.encode_blocks(recs, mix, 16, plan=kept2)
+    st = e.status.cpu().numpy()
+    assert (st[:3] == 4).all() and (st[3:] == 0).all()
+
 def test_cfg3_roundtrip_sample(oracle):
     """cfg3 scheme on the device: plan -> encode -> decode == the generated records; a sample of
     blocks against the oracle builder and decoder"""

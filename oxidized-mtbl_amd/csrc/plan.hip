@@ -662,7 +662,13 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
                oN12 = take(4 * nshard), oW12 = take(4 * std::max<uint64_t>(slots, 1)), oN6 = take(4 * std::max<uint64_t>(slots, 1)),
                oW6 = take(4 * std::max<uint64_t>(slots, 1) * mid), oPAN = take(iv == 0 ? m1 : 1);
   uint8_t* ws = nullptr;
-  if (hipMalloc(reinterpret_cast<void**>(&ws), off) != hipSuccess) return MTBLX_E_HIP;
+  if (hipMalloc(reinterpret_cast<void**>(&ws), off) != hipSuccess) {
+    (void)hipGetLastError();
+    if (keep) return MTBLX_E_HIP;
+    // ~50 B of scratch per record did not fit: the serial walk needs none
+    return mtblx_encode_plan_serial(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out,
+                                    flags_out, stream);
+  }
   auto p64 = [&](size_t o) { return reinterpret_cast<uint64_t*>(ws + o); };
   auto p32 = [&](size_t o) { return reinterpret_cast<uint32_t*>(ws + o); };
   uint64_t *A = keep ? reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(keep) + 256) : p64(oA),

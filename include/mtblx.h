@@ -369,6 +369,9 @@ int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint3
  * mod restart_interval, and every record's shared-prefix length with its predecessor.
  * restart_interval must be >= 1.  Returns like mtblx_encode_plan. */
 size_t mtblx_plan_keep_bytes(uint64_t nrec);
+/* mtblx_encode_plan / _keep cache their device scratch (~50 B per record) across calls; this
+ * frees it (the next call allocates again). */
+void mtblx_plan_release(void);
 int mtblx_encode_plan_keep(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
                            uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
                            uint32_t* flags_out, void* plan, size_t plan_bytes, void* stream);

@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "bounds.h"
@@ -590,6 +591,22 @@ int sscan(uint64_t* X, uint64_t m, uint64_t w, uint64_t* S, hipStream_t s) {
 
 using namespace mtblx_plan;
 
+static std::mutex g_ws_mu;   // the planner's cached scratch
+static uint8_t* g_ws = nullptr;
+static size_t g_ws_bytes = 0;
+static int g_ws_dev = -1;
+
+extern "C" void mtblx_plan_release(void) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  if (g_ws) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_ws);
+  }
+  g_ws = nullptr;
+  g_ws_bytes = 0;
+  g_ws_dev = -1;
+}
+
 // the kept plan (mtblx_encode_plan_keep): header, then PA [m] u64, Q [m] u64, SH [m] u32
 struct KeepHdr {
   uint64_t magic, lo, m, iv;
@@ -661,8 +678,23 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
                oJ0 = take(4 * m1), oT1 = take(4 * m1), oT2 = take(4 * m1), oJ6 = take(4 * m1), oJ12 = take(4 * m1),
                oN12 = take(4 * nshard), oW12 = take(4 * std::max<uint64_t>(slots, 1)), oN6 = take(4 * std::max<uint64_t>(slots, 1)),
                oW6 = take(4 * std::max<uint64_t>(slots, 1) * mid), oPAN = take(iv == 0 ? m1 : 1);
-  uint8_t* ws = nullptr;
-  if (hipMalloc(reinterpret_cast<void**>(&ws), off) != hipSuccess) {
+  // the scratch is cached across calls (grow-only; mtblx_plan_release frees it): a 66 M-record
+  // cut needs ~3 GB, and mapping that afresh each call cost more than the cut's kernels
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (g_ws && (g_ws_bytes < off || g_ws_dev != dev)) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_ws);
+    g_ws = nullptr;
+    g_ws_bytes = 0;
+  }
+  if (!g_ws && hipMalloc(reinterpret_cast<void**>(&g_ws), off) == hipSuccess) {
+    g_ws_bytes = off;
+    g_ws_dev = dev;
+  }
+  uint8_t* ws = g_ws;
+  if (!ws) {
     (void)hipGetLastError();
     if (keep) return MTBLX_E_HIP;
     // ~50 B of scratch per record did not fit: the serial walk needs none
@@ -759,7 +791,6 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
     if (hipMemcpyAsync(keep, &h, sizeof(h), hipMemcpyHostToDevice, s) != hipSuccess) rc = MTBLX_E_HIP;
   }
   if (hipStreamSynchronize(s) != hipSuccess && rc == MTBLX_OK) rc = MTBLX_E_HIP;
-  (void)hipFree(ws);
   *nblk_out = total;
   if (flags_out) *flags_out = flags;
   if (rc == MTBLX_OK && (flags & (MTBLX_PLAN_OUT_OF_ORDER | MTBLX_PLAN_PANIC | MTBLX_PLAN_TOO_LONG))) rc = MTBLX_E_FORMAT;

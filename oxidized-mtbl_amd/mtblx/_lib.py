@@ -36,7 +36,7 @@ EXPORTS = [
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
     "mtblx_pipe_decode", "mtblx_pipe_set", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks", "mtblx_plan_keep_bytes",
-    "mtblx_encode_plan_keep", "mtblx_encode_blocks_planned",
+    "mtblx_encode_plan_keep", "mtblx_encode_blocks_planned", "mtblx_plan_release",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
     "mtblx_codec_available", "mtblx_decompress", "mtblx_compress", "mtblx_decompress_blocks", "mtblx_writer_set_level",
     "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_block_seek_batch_kbuf", "mtblx_block_seek_batch_ex", "mtblx_copy_ranges", "mtblx_entry_offsets",

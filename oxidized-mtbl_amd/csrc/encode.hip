@@ -464,19 +464,21 @@ __device__ __forceinline__ uint32_t crc_mfma_final(const EncLds& S, uint32_t L) 
 struct Ent {
   uint64_t k0, kl, v0, vl, sh;
 };
-__device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, uint32_t iv,
+// share: the entry shares a prefix with its predecessor (shares(i, interval), tracked by the
+// callers as a running restart phase: a 64-bit modulo per entry was ~100 vector instructions)
+__device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, bool share,
                                         const uint16_t* shc = nullptr, const uint32_t* SH = nullptr) {
   Ent e;
   rec_of(R, r0 + i, e.k0, e.kl, e.v0, e.vl);
   e.sh = 0;
   if (SH) {   // planned: the block cut kept every record's shared-prefix length
-    if (shares(i, iv)) {
+    if (share) {
       MTBLX_CHK(SH + i, 4);
       e.sh = SH[i];
     }
   } else if (shc && i < kShCache && shc[i] != 0xFFFFu) {
     e.sh = shc[i];
-  } else if (shares(i, iv)) {
+  } else if (share) {
     uint64_t pk0, pkl, pv0, pvl;
     rec_of(R, r0 + i - 1, pk0, pkl, pv0, pvl);
     int c;
@@ -603,12 +605,18 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   // for the longest entry (Zipf keys).  (Phase A reading coalesced, entry i on thread i mod
   // threads, and handing the sizes over in LDS measured slower: 1043 vs 1069 GiB/s.)
   const uint64_t i0 = n * (uint64_t)tid / kThreads, i1 = n * (uint64_t)(tid + 1) / kThreads;
+  // the restart phase of entry i0 (i0 mod interval), then advanced per entry
+  const uint32_t ph0 = iv ? (uint32_t)(i0 % iv) : 0u;
+  uint32_t ph = ph0;
   for (uint64_t i = i0; i < i1 && !PL; ++i) {
+    const bool share = iv ? (i > 0 && ph != 0) : (i > 0);
+    if (iv && ++ph == iv) ph = 0;
 #else
   static_assert(!PL, "planned mode needs MTBLX_ENC_CONTIG");
   for (uint64_t i = tid; i < n; i += kThreads) {
+    const bool share = shares(i, iv);
 #endif
-    const Ent e = entry_of(a.R, r0, i, iv);
+    const Ent e = entry_of(a.R, r0, i, share);
     part += entry_bytes(e.sh, e.kl, e.vl);
     if (i < kShCache)
       S.shc[i] = e.sh < 0xFFFFu ? (uint16_t)e.sh : (uint16_t)0xFFFFu;
@@ -647,10 +655,15 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     uint64_t eo = tbase;
     Ent en{};   // the next entry's fields are loaded before this entry's bytes move
     const uint32_t* SHb = PL ? a.SH + j0 : nullptr;
-    if (i0 < i1) en = entry_of(a.R, r0, i0, iv, S.shc, SHb);
+    // restart phase of the entry and the number of restarts before it (multiples of the interval)
+    uint32_t rp = ph0;
+    uint64_t ri = iv ? (i0 + iv - 1) / iv : 0;
+    const auto share_at = [&](uint64_t i, uint32_t p) { return iv ? (i > 0 && p != 0) : (i > 0); };
+    if (i0 < i1) en = entry_of(a.R, r0, i0, share_at(i0, rp), S.shc, SHb);
     for (uint64_t i = i0; i < i1; ++i) {
       const Ent e = en;
-      if (i + 1 < i1) en = entry_of(a.R, r0, i + 1, iv, S.shc, SHb);
+      const uint32_t rp1 = iv ? (rp + 1 == iv ? 0u : rp + 1) : 0u;
+      if (i + 1 < i1) en = entry_of(a.R, r0, i + 1, share_at(i + 1, rp1), S.shc, SHb);
       const uint64_t sz = entry_bytes(e.sh, e.kl, e.vl);
       {
 #else
@@ -660,7 +673,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       Ent e{};
       uint64_t sz = 0;
       if (i < n) {
-        e = entry_of(a.R, r0, i, iv, S.shc);
+        e = entry_of(a.R, r0, i, shares(i, iv), S.shc);
         sz = entry_bytes(e.sh, e.kl, e.vl);
       }
       uint64_t tot = 0;
@@ -676,7 +689,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
 #else
         put_entry(dst + eo, a.R, e);
 #endif
+#if MTBLX_ENC_CONTIG
+        if (iv > 0 && rp == 0) put32(dst + R + 4 * ri++, (uint32_t)eo);
+        rp = rp1;
+#else
         if (iv > 0 && i % iv == 0) put32(dst + R + 4 * (i / iv), (uint32_t)eo);
+#endif
       }
 #if MTBLX_ENC_CONTIG
       eo += sz;

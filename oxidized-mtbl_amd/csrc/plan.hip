@@ -226,6 +226,27 @@ __global__ void __launch_bounds__(kT) k_sscan_down(uint64_t* X, uint64_t m, uint
   }
 }
 
+// n / d for 32-bit n and a divisor fixed per launch (Granlund-Montgomery: multiply-high + shift);
+// a 64-bit division per probe was most of k_plan_next's vector instructions
+struct FastDiv {
+  uint32_t d, m, s;
+  static FastDiv make(uint32_t d) {
+    FastDiv f{d, 0, 0};
+    if (d > 1) {
+      uint32_t l = 0;
+      while ((1ull << l) < d) ++l;
+      f.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+      f.s = l - 1;
+    }
+    return f;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    if (d == 1) return n;
+    const uint32_t t = __umulhi(m, n);
+    return (t + ((n - t) >> 1)) >> s;
+  }
+};
+
 struct NextArgs {
   uint64_t m;
   uint32_t iv;
@@ -239,17 +260,75 @@ struct NextArgs {
   uint32_t nsh;
   uint32_t* next;       // [m] local index of the record that starts the next block (or the shard end)
   uint8_t* pan;         // [m] iv == 0: a second entry would be added (assert, src/block_builder.rs:50)
+  FastDiv div;          // by iv
 };
 
 // current_size_estimate() of a block holding entries [j, k) (src/block_builder.rs:40-47)
 __device__ __forceinline__ uint64_t est(const NextArgs& a, uint64_t j, uint64_t base_a, uint64_t base_q, uint64_t k) {
-  const uint64_t nr = 1 + (k - 1 - j) / a.iv;
-  const uint64_t last = j + (nr - 1) * (uint64_t)a.iv;
+  const uint64_t q = a.div.div((uint32_t)(k - 1 - j));   // < 2^32: the plan has fewer records
+  const uint64_t nr = 1 + q;
+  const uint64_t last = j + q * (uint64_t)a.iv;
   MTBLX_CHK(a.PA + k - 1, 8), MTBLX_CHK(a.Q + last, 8);
   const uint64_t buf = a.PA[k - 1] - base_a + a.Q[last] - base_q;
   return buf + nr * (buf > 0xFFFFFFFFull ? 8u : 4u) + 4u;
 }
 
+// next(j) for a start j of a shard ending at e (j + 1 < e, interval >= 1).  The first k with
+// est(k) + gmax >= B (est grows with k) is bracketed by a gallop from `guess` (first step d) and
+// bisected -- ka, returned for the next start's guess; from there the flushing record is found
+// chunk by chunk (a 64-record chunk is skipped while est at its last record + its largest record
+// term stays below the block size).
+__device__ __forceinline__ uint64_t find_next(const NextArgs& a, uint64_t j, uint64_t e, uint64_t guess, uint64_t d,
+                                              uint64_t gm, uint64_t& ka) {
+  const uint64_t base_a = j ? a.PA[j - 1] : 0;
+  const uint64_t base_q = j >= a.iv ? a.Q[j - a.iv] : 0;
+  const uint64_t e1 = e - 1;
+  const uint64_t k0 = guess < j + 1 ? j + 1 : (guess > e1 ? e1 : guess);
+  uint64_t lo = j, hi = 0;   // lo: a k known false (j: none yet); hi: a k known true (0: none)
+  if (est(a, j, base_a, base_q, k0) + gm >= a.B) {
+    hi = k0;
+    while (hi > j + 1) {   // downwards: a false k below hi
+      const uint64_t k = hi - j - 1 > d ? hi - d : j + 1;
+      if (est(a, j, base_a, base_q, k) + gm < a.B) { lo = k; break; }
+      hi = k;
+      d <<= 1;
+    }
+  } else {
+    lo = k0;
+    while (lo < e1) {   // upwards: a true k above lo
+      const uint64_t k = e1 - lo > d ? lo + d : e1;
+      if (est(a, j, base_a, base_q, k) + gm >= a.B) { hi = k; break; }
+      lo = k;
+      d <<= 1;
+    }
+  }
+  if (!hi) {
+    ka = e;
+    return e;
+  }
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + ((hi - lo) >> 1);
+    if (est(a, j, base_a, base_q, mid) + gm >= a.B) hi = mid; else lo = mid;
+  }
+  ka = hi;
+  uint64_t k = hi;
+  while (k <= e1) {
+    const uint64_t cl = std::min<uint64_t>((k | 63u), e1);
+    MTBLX_CHK(a.GM + (k >> 6), 8);
+    if (est(a, j, base_a, base_q, cl) + a.GM[k >> 6] < a.B) { k = cl + 1; continue; }
+    for (; k <= cl; ++k) {
+      MTBLX_CHK(a.G + k, 8);
+      if (est(a, j, base_a, base_q, k) + a.G[k] >= a.B) return k;
+    }
+  }
+  return e;
+}
+
+// kSweep starts per thread, kT apart (neighbouring threads take neighbouring starts: their probes
+// coalesce): the first from a probe at the typical block length, each next one from the previous
+// one's threshold + kT, which moves by about as much as the start did -- a few probes instead of
+// a full search
+constexpr uint32_t kSweep = 8;
 __global__ void __launch_bounds__(kT) k_plan_next(NextArgs a) {
   // the shard starts in LDS when they fit (the shard search is on every thread's chain)
   constexpr uint32_t kLsb = 1024;
@@ -262,78 +341,39 @@ __global__ void __launch_bounds__(kT) k_plan_next(NextArgs a) {
     }
     __syncthreads();
   }
-  const uint64_t j = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (j >= a.m) return;
   const uint64_t* sbp = in_lds ? lsb : a.sb;
-  const uint64_t e = sbp[shard_of(sbp, a.nsh, j) + 1];
-  uint64_t nx = e;
-  if (a.pan) {
-    MTBLX_CHK(a.pan + j, 1);
-    a.pan[j] = 0;
-  }
-  if (j + 1 < e) {
-    if (a.iv == 0) {   // the first add pushes a second restart (restarts = [0, 0]); a second add panics
-      MTBLX_CHK(a.Q + j, 8), MTBLX_CHK(a.G + j + 1, 8), MTBLX_CHK(a.pan + j, 1);
-      const uint64_t z = a.PA[j] - (j ? a.PA[j - 1] : 0) + a.Q[j];
-      const uint64_t es = z + 2 * (z > 0xFFFFFFFFull ? 8u : 4u) + 4u;
-      a.pan[j] = es + a.G[j + 1] >= a.B ? 0 : 1;
-      nx = j + 1;
-    } else {
-      const uint64_t base_a = j ? a.PA[j - 1] : 0;
-      const uint64_t base_q = j >= a.iv ? a.Q[j - a.iv] : 0;
-      const uint64_t gm = *a.gmax;
-      // first k in [j + 1, e - 1] with est(k) + gmax >= B (est grows with k): a probe at the
-      // typical block length (block size / mean entry size), a gallop from there to bracket it,
-      // then bisection.  lo: a k known false (j: none yet); hi: a k known true (0: none)
-      const uint64_t e1 = e - 1;
-      // typical records per block: block size / mean entry size (a heuristic: only where to probe first)
-      const double tot = (double)a.PA[a.m - 1];
-      const double hd = tot > 0.0 ? (double)a.B * (double)a.m / tot : 1.0;
-      const uint64_t hint = hd < 1.0 ? 1u : hd > 1e12 ? (uint64_t)1e12 : (uint64_t)hd;
-      uint64_t k0 = j + hint;
-      k0 = k0 < j + 1 ? j + 1 : (k0 > e1 ? e1 : k0);
-      uint64_t lo = j, hi = 0, d = hint / 16 + 1;
-      if (est(a, j, base_a, base_q, k0) + gm >= a.B) {
-        hi = k0;
-        while (hi > j + 1) {   // downwards: find a false k below hi
-          const uint64_t k = hi - j - 1 > d ? hi - d : j + 1;
-          if (est(a, j, base_a, base_q, k) + gm < a.B) { lo = k; break; }
-          hi = k;
-          d <<= 1;
-        }
+  const uint64_t gm = *a.gmax;
+  // typical records per block: block size / mean entry size (a heuristic: only where to probe first)
+  const double tot = (double)a.PA[a.m - 1];
+  const double hd = tot > 0.0 ? (double)a.B * (double)a.m / tot : 1.0;
+  const uint64_t hint = hd < 1.0 ? 1u : hd > 1e12 ? (uint64_t)1e12 : (uint64_t)hd;
+  uint64_t pe = 0, pka = 0;   // the previous start's shard end and threshold (pe == 0: none)
+  for (uint32_t q = 0; q < kSweep; ++q) {
+    const uint64_t j = ((uint64_t)blockIdx.x * kSweep + q) * kT + threadIdx.x;
+    if (j >= a.m) break;
+    const uint64_t e = j < pe ? pe : sbp[shard_of(sbp, a.nsh, j) + 1];
+    uint64_t nx = e;
+    if (a.pan) {
+      MTBLX_CHK(a.pan + j, 1);
+      a.pan[j] = 0;
+    }
+    if (j + 1 < e) {
+      if (a.iv == 0) {   // the first add pushes a second restart (restarts = [0, 0]); a second add panics
+        MTBLX_CHK(a.Q + j, 8), MTBLX_CHK(a.G + j + 1, 8), MTBLX_CHK(a.pan + j, 1);
+        const uint64_t z = a.PA[j] - (j ? a.PA[j - 1] : 0) + a.Q[j];
+        const uint64_t es = z + 2 * (z > 0xFFFFFFFFull ? 8u : 4u) + 4u;
+        a.pan[j] = es + a.G[j + 1] >= a.B ? 0 : 1;
+        nx = j + 1;
+      } else if (e == pe && pka < pe) {   // the same shard: from the previous threshold
+        nx = find_next(a, j, e, pka + kT, 1, gm, pka);
       } else {
-        lo = k0;
-        while (lo < e1) {   // upwards: find a true k above lo
-          const uint64_t k = e1 - lo > d ? lo + d : e1;
-          if (est(a, j, base_a, base_q, k) + gm >= a.B) { hi = k; break; }
-          lo = k;
-          d <<= 1;
-        }
-      }
-      if (hi) {
-        while (hi - lo > 1) {
-          const uint64_t mid = lo + ((hi - lo) >> 1);
-          if (est(a, j, base_a, base_q, mid) + gm >= a.B) hi = mid; else lo = mid;
-        }
-        // the flushing record: chunks skipped while est at the chunk's last record + the chunk's
-        // largest record term stays below the block size
-        uint64_t k = hi;
-        bool found = false;
-        while (k <= e - 1 && !found) {
-          const uint64_t cl = std::min<uint64_t>((k | 63u), e - 1);
-          MTBLX_CHK(a.GM + (k >> 6), 8);
-          if (est(a, j, base_a, base_q, cl) + a.GM[k >> 6] < a.B) { k = cl + 1; continue; }
-          for (; k <= cl; ++k) {
-            MTBLX_CHK(a.G + k, 8);
-            if (est(a, j, base_a, base_q, k) + a.G[k] >= a.B) { found = true; break; }
-          }
-        }
-        if (found) nx = k;
+        nx = find_next(a, j, e, j + hint, hint / 16 + 1, gm, pka);
       }
     }
+    pe = e;
+    MTBLX_CHK(a.next + j, 4);
+    a.next[j] = (uint32_t)nx;
   }
-  MTBLX_CHK(a.next + j, 4);
-  a.next[j] = (uint32_t)nx;
 }
 
 // the shard ends (local), one bit each: bit x set <=> x ends a shard (x <= m)
@@ -735,10 +775,10 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
       if (!ok(hipGetLastError())) break;
       if ((rc = sscan(A, m, 1, S, s)) != MTBLX_OK) break;
       if (iv && (rc = sscan(D, m, iv, S, s)) != MTBLX_OK) break;
-      NextArgs na{m, iv, block_size, A, D, G, GM, mx, dsb, nshard, J0, pan};
+      NextArgs na{m, iv, block_size, A, D, G, GM, mx, dsb, nshard, J0, pan, FastDiv::make(iv ? iv : 1)};
       MTBLX_LAUNCH((MTBLX_R(A, 8 * m), MTBLX_R(D, 8 * m), MTBLX_R(G, 8 * m), MTBLX_R(GM, 8 * nchunk), MTBLX_R(mx, 8),
                     MTBLX_R(dsb, 8 * (nshard + 1)), MTBLX_R(J0, 4 * m), pan ? MTBLX_R(pan, m) : MTBLX_R(nullptr, 0)),
-                   k_plan_next, dim3(grid_of(m)), dim3(kT), 0, s, na);
+                   k_plan_next, dim3(grid_of(m, (uint64_t)kT * kSweep)), dim3(kT), 0, s, na);
       // next^8 and next^512 by doubling
       const uint32_t* src = J0;
       for (int t = 1; t <= lvHi; ++t) {

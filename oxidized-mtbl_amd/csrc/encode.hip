@@ -305,6 +305,9 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
 // in unaligned access mode).  A tail of 1..15 bytes is read as the 16-byte window ending at n
 // when the record is at least 16 bytes long (never before `base`, the blob's start), else
 // byte by byte.
+#ifndef MTBLX_ENC_TAILV   // tails of 1..15 bytes as 8/4/2/1-byte pieces (0: byte stores, the A/B base)
+#define MTBLX_ENC_TAILV 1
+#endif
 #ifndef MTBLX_ENC_NT_STORES
 #define MTBLX_ENC_NT_STORES 1
 #endif
@@ -326,6 +329,39 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   const uint64_t to = 16 * nfull;
   if (src + n >= base + 16) {   // the 16-byte window ending at n holds the tail in its last t bytes
     const v4u w = *reinterpret_cast<const v4u*>(src + n - 16);
+#if MTBLX_ENC_TAILV
+    // the window shifted right by r = 16 - t bytes (funnel shifts), then stored as pieces of 8,
+    // 4, 2 and 1 bytes (the bits of t) instead of t byte stores: a wave paid for its longest tail
+    const uint32_t r = 16u - t, dq = r >> 2, bs = r & 3u;
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    uint32_t o[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t lo = dq + i < 4 ? (dq + i == 0 ? ws[0] : dq + i == 1 ? ws[1] : dq + i == 2 ? ws[2] : ws[3]) : 0u;
+      const uint32_t hi = dq + i + 1 < 4 ? (dq + i + 1 == 1 ? ws[1] : dq + i + 1 == 2 ? ws[2] : ws[3]) : 0u;
+      o[i] = __builtin_amdgcn_alignbyte(hi, lo, bs);
+    }
+    typedef uint64_t __attribute__((aligned(1))) u64t;
+    typedef uint32_t __attribute__((aligned(1))) u32t;
+    typedef uint16_t __attribute__((aligned(1))) u16t;
+    uint8_t* d = dst + to;
+    uint32_t off = 0;
+    if (t & 8u) {
+      *reinterpret_cast<u64t*>(d) = (uint64_t)o[0] | ((uint64_t)o[1] << 32);
+      off = 8;
+    }
+    if (t & 4u) {
+      *reinterpret_cast<u32t*>(d + off) = off ? o[2] : o[0];
+      off += 4;
+    }
+    const auto word = [&](uint32_t q) { return q == 0 ? o[0] : q == 1 ? o[1] : q == 2 ? o[2] : o[3]; };
+    if (t & 2u) {
+      *reinterpret_cast<u16t*>(d + off) = (uint16_t)(word(off >> 2) >> (8 * (off & 3u)));
+      off += 2;
+    }
+    if (t & 1u) d[off] = (uint8_t)(word(off >> 2) >> (8 * (off & 3u)));
+    return;
+#endif
     for (uint32_t k = 0; k < t; ++k) {
       const uint32_t q = 16 - t + k;
       const uint32_t d = q < 4 ? w.x : q < 8 ? w.y : q < 12 ? w.z : w.w;

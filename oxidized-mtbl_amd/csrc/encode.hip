@@ -305,6 +305,9 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
 // in unaligned access mode).  A tail of 1..15 bytes is read as the 16-byte window ending at n
 // when the record is at least 16 bytes long (never before `base`, the blob's start), else
 // byte by byte.
+#ifndef MTBLX_ENC_CARRY   // the next entry's offsets carried from this one (A/B: 0 = reload both ends)
+#define MTBLX_ENC_CARRY 1
+#endif
 #ifndef MTBLX_ENC_TAILV   // tails of 1..15 bytes as 8/4/2/1-byte pieces (0: byte stores, the A/B base)
 #define MTBLX_ENC_TAILV 1
 #endif
@@ -523,6 +526,33 @@ __device__ __forceinline__ Ent entry_of(const Recs& R, uint64_t r0, uint64_t i, 
   return e;
 }
 
+// entry i + 1 after entry p = entry i: its key and value start where p's end (the END offsets
+// are cumulative), so only record r0 + i + 1's two END offsets are loaded, and its shared prefix
+// (when not cached) is the LCP with p's key
+__device__ __forceinline__ Ent entry_after(const Recs& R, uint64_t r0, uint64_t i1, const Ent& p, bool share,
+                                           const uint16_t* shc = nullptr, const uint32_t* SH = nullptr) {
+  Ent e;
+  const uint64_t r = r0 + i1;
+  MTBLX_CHK(R.key_end + r, 8), MTBLX_CHK(R.val_end + r, 8);
+  e.k0 = p.k0 + p.kl;
+  e.kl = R.key_end[r] - e.k0;
+  e.v0 = p.v0 + p.vl;
+  e.vl = R.val_end[r] - e.v0;
+  e.sh = 0;
+  if (SH) {
+    if (share) {
+      MTBLX_CHK(SH + i1, 4);
+      e.sh = SH[i1];
+    }
+  } else if (shc && i1 < kShCache && shc[i1] != 0xFFFFu) {
+    e.sh = shc[i1];
+  } else if (share) {
+    int c;
+    e.sh = lcp_cmp(R.keys + p.k0, p.kl, R.keys + e.k0, e.kl, c);
+  }
+  return e;
+}
+
 // varint32 bytes of v packed little-endian in a register (<= 5 bytes), *len = their count
 // (src/varint.rs:12-42)
 __device__ __forceinline__ uint64_t vpack(uint64_t v, uint32_t& len) {
@@ -644,15 +674,23 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   // the restart phase of entry i0 (i0 mod interval), then advanced per entry
   const uint32_t ph0 = iv ? (uint32_t)(i0 % iv) : 0u;
   uint32_t ph = ph0;
+  Ent pe{};   // the previous entry (MTBLX_ENC_CARRY)
+  (void)pe;
   for (uint64_t i = i0; i < i1 && !PL; ++i) {
     const bool share = iv ? (i > 0 && ph != 0) : (i > 0);
     if (iv && ++ph == iv) ph = 0;
+#if MTBLX_ENC_CARRY
+    const Ent e = i == i0 ? entry_of(a.R, r0, i, share) : entry_after(a.R, r0, i, pe, share);
+    pe = e;
+#else
+    const Ent e = entry_of(a.R, r0, i, share);
+#endif
 #else
   static_assert(!PL, "planned mode needs MTBLX_ENC_CONTIG");
   for (uint64_t i = tid; i < n; i += kThreads) {
     const bool share = shares(i, iv);
-#endif
     const Ent e = entry_of(a.R, r0, i, share);
+#endif
     part += entry_bytes(e.sh, e.kl, e.vl);
     if (i < kShCache)
       S.shc[i] = e.sh < 0xFFFFu ? (uint16_t)e.sh : (uint16_t)0xFFFFu;
@@ -699,7 +737,11 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     for (uint64_t i = i0; i < i1; ++i) {
       const Ent e = en;
       const uint32_t rp1 = iv ? (rp + 1 == iv ? 0u : rp + 1) : 0u;
+#if MTBLX_ENC_CARRY
+      if (i + 1 < i1) en = entry_after(a.R, r0, i + 1, e, share_at(i + 1, rp1), S.shc, SHb);
+#else
       if (i + 1 < i1) en = entry_of(a.R, r0, i + 1, share_at(i + 1, rp1), S.shc, SHb);
+#endif
       const uint64_t sz = entry_bytes(e.sh, e.kl, e.vl);
       {
 #else

@@ -479,6 +479,48 @@ def rank_totals(block_bytes: int, nrec: int, elapsed: float, dist, device="cuda"
             _max_over_ranks(elapsed, dist, device))
 
 
+def get_leg(data, nblocks, rank, nq=1 << 20, reps=10):
+    """f2, Reader::get batched on the device (mtblx_get, src/reader.rs:111-122): nq queries on the
+    bench's cfg2 file, half of them keys the file holds (random records), half absent (a present
+    key with one tail byte changed: its counter prefix is unique, so the key is not in the file),
+    keys already in HBM; checksums on (the reference default: every landed block's CRC) and off.
+    Device time per batch by HIP events; every found value must be the record's 64 bytes."""
+    import ctypes as C
+    from mtblx import _lib as mlib, codec, reader, synth
+    nrec = synth.cfg2_file_nrec(nblocks)
+    keys = synth.cfg2_keys(nrec, seed=synth.SEED_CFG2 + rank, c0=rank << synth.SHARD_KEY_BITS)
+    rng = np.random.default_rng(0x6765740)
+    q = keys[rng.integers(0, nrec, nq)].copy()
+    q[nq // 2:, 15] ^= 0x5A
+    r = reader.Reader(data, verify_checksums=True)
+    dev = r.file.device
+    kb = torch.from_numpy(q.reshape(-1)).to(dev)
+    ke = torch.arange(1, nq + 1, dtype=torch.int64, device=dev) * 16
+    st = torch.empty(nq, dtype=torch.int32, device=dev)
+    vo = torch.empty(nq, dtype=torch.int64, device=dev)
+    vl = torch.empty(nq, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream()
+    L = mlib.lib()
+    out = {"queries": nq, "present": nq // 2}
+    for verify in (1, 0):
+        def call():
+            if L.mtblx_get(C.c_void_p(r.file.data_ptr()), r.len, r.version, verify, r.index_off, r.index_len,
+                           C.c_void_p(kb.data_ptr()), C.c_void_p(ke.data_ptr()), nq, C.c_void_p(st.data_ptr()),
+                           C.c_void_p(vo.data_ptr()), C.c_void_p(vl.data_ptr()), C.c_void_p(s.cuda_stream)) != 0:
+                raise RuntimeError("mtblx_get failed")
+        with torch.cuda.stream(s):
+            call()
+            call()
+            ms = _timed(call, s, reps)
+        torch.cuda.synchronize()
+        found = int((st == mlib.GET_FOUND).sum().item())
+        ok = found == nq // 2 and bool((vl[st == mlib.GET_FOUND] == 64).all().item())
+        out["checksums_on" if verify else "checksums_off"] = {
+            "ms": round(ms, 3), "gets_per_s": round(nq / (ms * 1e-3), 1), "found": found, "checked": ok}
+    del r
+    return out
+
+
 def run_cfg3(args, dist, world, rank):
     """BASELINE configs[2]: 1 M blocks x 64 KiB per GPU, Zipf 8..256 B keys, 64 B values,
     restart interval 16 -- device encode (Writer block cut + BlockBuilder + framing, src/writer.rs,
@@ -755,6 +797,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-ceiling", action="store_true", help="skip the stream-copy ceiling measurement")
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32C verify measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host in, host out) measurement")
+    ap.add_argument("--no-get", action="store_true", help="skip the batched Reader::get leg (f2)")
     ap.add_argument("--e2e-passes", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4"],
                     help="cfg2 (default, BASELINE configs[1]: the metric's workload); cfg3 / cfg4 print their own line")
@@ -1028,6 +1071,8 @@ def main():
     }
     if crc_info is not None:
         res["crc32c_verify"] = crc_info
+    if not args.no_get and args.block_size == 4096 and not args.lib and not args.stamps:
+        res["get_batch"] = get_leg(data, int(batch.nblk), rank)
     if not args.no_e2e and args.block_size == 4096 and not args.lib and not args.stamps:
         del out, ws
         torch.cuda.empty_cache()

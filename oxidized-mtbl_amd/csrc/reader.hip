@@ -12,6 +12,7 @@
 // the decode kernel's per-block status, over the directory this kernel writes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "bounds.h"
 #include "crc_dev.h"
@@ -196,6 +197,21 @@ __device__ __forceinline__ int decode_entry(const Blk& b, uint64_t p, uint64_t l
   return R_OK;
 }
 
+// the number of equal leading bytes of a[0..n) and b[0..n): 8-byte loads (never past n), the
+// first difference by the lowest set byte of the XOR; then the last < 8 bytes one at a time
+typedef uint64_t __attribute__((aligned(1))) u64u;
+__device__ __forceinline__ uint64_t match_len(const uint8_t* a, const uint8_t* b, uint64_t n) {
+  uint64_t c = 0;
+  while (c + 8 <= n) {
+    MTBLX_CHK(a + c, 8), MTBLX_CHK(b + c, 8);
+    const uint64_t x = *reinterpret_cast<const u64u*>(a + c) ^ *reinterpret_cast<const u64u*>(b + c);
+    if (x) return c + (uint64_t)(__builtin_ctzll(x) >> 3);
+    c += 8;
+  }
+  while (c < n && (MTBLX_CHK(a + c, 1), MTBLX_CHK(b + c, 1), a[c] == b[c])) ++c;
+  return c;
+}
+
 __device__ __forceinline__ int cmp_key(const It& it, uint64_t tlen) {   // Ord of key vs target
   if (it.cmp) return it.cmp;
   return it.klen < tlen ? -1 : (it.klen > tlen ? 1 : 0);
@@ -226,8 +242,9 @@ __device__ int parse_next_key(const Blk& b, It& it, const uint8_t* t, uint64_t t
     it.kcap = c;
   }
   if (m <= it.c) {            // the kept prefix matches the target: compare the suffix
-    uint64_t c = m, j = 0;
-    while (j < ns && c < tlen && (MTBLX_CHK(b.d + p + j, 1), MTBLX_CHK(t + c, 1), b.d[p + j] == t[c])) { ++j; ++c; }
+    const uint64_t lim = ns < tlen - (tlen < m ? tlen : m) ? ns : tlen - (tlen < m ? tlen : m);
+    const uint64_t j = m < tlen ? match_len(b.d + p, t + m, lim) : 0;
+    const uint64_t c = m + j;
     it.cmp = (j < ns && c < tlen) ? (b.d[p + j] < t[c] ? -1 : 1) : 0;
     it.c = c;
   }                           // else: the first difference lies in the kept prefix
@@ -251,8 +268,7 @@ __device__ int seek(const Blk& b, It& it, const uint8_t* t, uint64_t tlen) {
     if (decode_entry(b, restart_point(b, mid), b.R, sh, ns, vl, ko) != R_OK) return R_PANIC;
     if (sh != 0) return R_OK;                                 // "corruption": early return
     if (ko + ns > b.L) return R_PANIC;
-    uint64_t c = 0;
-    while (c < ns && c < tlen && (MTBLX_CHK(b.d + ko + c, 1), MTBLX_CHK(t + c, 1), b.d[ko + c] == t[c])) ++c;
+    const uint64_t c = match_len(b.d + ko, t, ns < tlen ? ns : tlen);
     const int r = (c < ns && c < tlen) ? (b.d[ko + c] < t[c] ? -1 : 1) : (ns < tlen ? -1 : (ns > tlen ? 1 : 0));
     if (r < 0) left = mid;
     else right = mid - 1;
@@ -297,17 +313,17 @@ struct FileCtx {
   DecTab tab;          // tab.dec == nullptr: the file is not compressed
 };
 
-// block_at_index + Reader::block (src/reader.rs:177-186, :139-174):
-// 1 = Some(block), 0 = None, R_PANIC, 2 = Err(InvalidBlock), 3 = a compressed block the caller's
-// table does not hold (its stored content [mstart, + msz) passed framing and the checksum)
-__device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk& out, uint64_t& mstart,
-                              uint64_t& msz) {
+// block_at_index + Reader::block (src/reader.rs:177-186, :139-174), in two halves around the
+// checksum.  frame_at_index: the landed index entry's offset and the block's framing ->
+// 0 = None (get() -> None), R_PANIC, 1 = framed: content [start, start + sz), stored checksum crc.
+__device__ __forceinline__ int frame_at_index(const FileCtx& f, const Blk& ib, const It& ii, uint64_t& start,
+                                              uint64_t& sz, uint32_t& crc) {
   if (!valid(ib, ii)) return 0;                                // get() -> None
   if (ii.voff + ii.vlen > ib.L) return R_PANIC;
   uint64_t off = 0;
   if (dec64(ib.d + ii.voff, ii.vlen, off) < 0) return R_PANIC;
   if (!(off < f.len)) return R_PANIC;
-  uint64_t ll, sz;
+  uint64_t ll;
   if (f.version == 0) {
     if (off + 4 > f.len) return R_PANIC;
     ll = 4; sz = rd32g(f.file + off);
@@ -316,9 +332,16 @@ __device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk
     if (k < 0) return R_PANIC;
     ll = (uint64_t)k;
   }
-  const uint64_t start = off + ll + 4;
+  start = off + ll + 4;
   if (start > f.len || sz > f.len - start) return R_PANIC;
-  if (f.verify && mtblx_crc::wave_crc32c(f.file + start, sz, f.T, f.lane) != rd32g(f.file + off + ll)) return R_PANIC;
+  crc = rd32g(f.file + off + ll);
+  return 1;
+}
+// after the checksum (when verified): decompression (the caller's table) and Block::init ->
+// 1 = Some(block), R_PANIC, 2 = Err(InvalidBlock), 3 = a compressed block the caller's table does
+// not hold (its stored content [mstart, + msz) passed framing and the checksum)
+__device__ __forceinline__ int block_after_crc(const FileCtx& f, uint64_t start, uint64_t sz, Blk& out,
+                                               uint64_t& mstart, uint64_t& msz) {
   const uint8_t* content = f.file + start;
   if (f.tab.dec) {   // decompress (src/reader.rs:166-170): the caller's decompressed copy
     uint32_t lo = 0, hi = f.tab.n;
@@ -343,6 +366,16 @@ __device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk
   if (bi == 1) return 2;
   if (bi < 0) return R_PANIC;
   return 1;
+}
+// the whole of it, for a wave-uniform caller (the checksum shared by the wave's lanes)
+__device__ int block_at_index(const FileCtx& f, const Blk& ib, const It& ii, Blk& out, uint64_t& mstart,
+                              uint64_t& msz) {
+  uint64_t start = 0, sz = 0;
+  uint32_t crc = 0;
+  const int fr = frame_at_index(f, ib, ii, start, sz, crc);
+  if (fr != 1) return fr;
+  if (f.verify && mtblx_crc::wave_crc32c(f.file + start, sz, f.T, f.lane) != crc) return R_PANIC;
+  return block_after_crc(f, start, sz, out, mstart, msz);
 }
 
 __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
@@ -418,6 +451,132 @@ __global__ void __launch_bounds__(256) k_get(const uint8_t* file, uint64_t file_
     MTBLX_CHK(voff + q, 8);
     MTBLX_CHK(vlen + q, 8);
     if (lane == 0) { st[q] = res; voff[q] = ro; vlen[q] = rl; }
+  }
+}
+
+// The same lookups, one LANE per query (round 5): the seeks run per lane -- 64 queries in flight
+// per wave instead of one -- and only the checksums are shared: after each stage the wave
+// computes, one block at a time, the CRC-32C of every block a lane landed on (its lanes
+// cooperating), and each lane goes on with its own result.  The stages follow k_get's control
+// flow exactly: A = index seek + framing of the landed block; B = its Block::init, the block
+// seek, and when the seek runs past the block's end the next index entry's framing; C = that
+// block's Block::init and its first record.
+__device__ __forceinline__ void lanes_crc(const FileCtx& f, bool need, uint64_t start, uint64_t sz, uint32_t stored,
+                                          bool& ok) {
+  uint64_t m = __ballot(need);
+  ok = true;
+  while (m) {
+    const int j = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t st = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(start >> 32), j) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)start, j);
+    const uint64_t n = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sz >> 32), j) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sz, j);
+    const uint32_t c = mtblx_crc::wave_crc32c(f.file + st, n, f.T, f.lane);
+    if (f.lane == j) ok = c == stored;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_get_lanes(const uint8_t* file, uint64_t file_len, uint32_t version,
+                                                   int verify, uint64_t idx_off, uint64_t idx_len, DecTab tab,
+                                                   const uint8_t* qkeys, const uint64_t* qend, uint32_t nq, int32_t* st,
+                                                   uint64_t* voff, uint64_t* vlen) {
+  __shared__ uint32_t T[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = mtblx_crc::kTab.byte[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const FileCtx f{file, file_len, version, verify, T, lane, tab};
+  const uint8_t* vbase = tab.dec ? tab.dec : file;   // values are offsets into the scanned bytes
+  const uint64_t all = (uint64_t)gridDim.x * blockDim.x;
+  // wave-uniform trip count: the whole wave runs every stage and every checksum pass
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < nq; base += all) {
+    const uint64_t q = base + (uint64_t)lane;
+    bool live = q < nq;
+    int32_t res = MTBLX_GET_NONE;
+    uint64_t ro = 0, rl = 0, tl = 0, start = 0, sz = 0, ms = 0, ml = 0;
+    uint32_t crc = 0;
+    const uint8_t* t = qkeys;
+    Blk ib{}, db{};
+    It ii{}, di{};
+    bool need = false, ok = true;
+    // ---- stage A ----
+    if (live) {
+      MTBLX_CHK(qend + q, 8);
+      const uint64_t k0 = q ? qend[q - 1] : 0, k1 = qend[q];
+      t = qkeys + k0;
+      tl = k1 - k0;
+      do {
+        const int ibi = block_init(file + idx_off, idx_len, ib);   // the Reader's index block
+        if (ibi != 0) { res = ibi == 1 ? MTBLX_GET_ERR : MTBLX_GET_PANIC; live = false; break; }
+        if (iter_init(ib, ii) != R_OK) { res = MTBLX_GET_PANIC; live = false; break; }
+        const int r = seek(ib, ii, t, tl);                          // new_from: index_iter.seek(key)
+        if (r != R_OK) { res = r == R_LOOP ? MTBLX_GET_LOOP : MTBLX_GET_PANIC; live = false; break; }
+        const int fr = frame_at_index(f, ib, ii, start, sz, crc);
+        if (fr == R_PANIC) { res = MTBLX_GET_PANIC; live = false; break; }
+        if (fr == 0) { live = false; break; }                       // no block: next() -> None
+        need = verify != 0;
+      } while (false);
+    }
+    lanes_crc(f, live && need, start, sz, crc, ok);
+    // ---- stage B ----
+    need = false;
+    if (live) {
+      do {
+        if (!ok) { res = MTBLX_GET_PANIC; live = false; break; }   // Reader::block's assert_eq
+        const int b = block_after_crc(f, start, sz, db, ms, ml);
+        if (b == R_PANIC) { res = MTBLX_GET_PANIC; live = false; break; }
+        if (b == 3) { res = MTBLX_GET_MISSING; ro = ms; rl = ml; live = false; break; }
+        if (b == 2) { res = MTBLX_GET_ERR; live = false; break; }   // Err at open (new_get)
+        if (iter_init(db, di) != R_OK) { res = MTBLX_GET_PANIC; live = false; break; }
+        int r = seek(db, di, t, tl);                                  // bi.seek(key)
+        if (r != R_OK) { res = r == R_LOOP ? MTBLX_GET_LOOP : MTBLX_GET_PANIC; live = false; break; }
+        if (valid(db, di)) {                                          // next() (first call, Get)
+          if (di.voff + di.vlen > db.L) res = MTBLX_GET_PANIC;
+          else if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
+          live = false;
+          break;
+        }
+        // the seek ran past the end of the block: the next index entry's first record
+        if (!valid(ib, ii)) { live = false; break; }
+        r = parse_next_key(ib, ii, t, tl);
+        if (r == R_PANIC) { res = MTBLX_GET_PANIC; live = false; break; }
+        if (r == R_LOOP) { res = MTBLX_GET_LOOP; live = false; break; }
+        if (!valid(ib, ii)) { live = false; break; }
+        const int fr = frame_at_index(f, ib, ii, start, sz, crc);
+        if (fr == R_PANIC) { res = MTBLX_GET_PANIC; live = false; break; }
+        if (fr == 0) { live = false; break; }
+        need = verify != 0;
+      } while (false);
+    }
+    lanes_crc(f, live && need, start, sz, crc, ok);
+    // ---- stage C ----
+    if (live) {
+      do {
+        if (!ok) { res = MTBLX_GET_PANIC; break; }
+        const int b = block_after_crc(f, start, sz, db, ms, ml);
+        if (b == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+        if (b == 3) { res = MTBLX_GET_MISSING; ro = ms; rl = ml; break; }
+        if (b == 2) {
+          // next() returned Some(Err(InvalidBlock)): Reader::get returns the OLD block
+          // iterator's `val` (k_get above; src/reader.rs:111-122, :376-379, :195-203)
+          if (di.has_val) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
+          break;
+        }
+        if (iter_init(db, di) != R_OK) { res = MTBLX_GET_PANIC; break; }
+        restart_at(db, di, 0);                                       // seek_to_first
+        const int r = parse_next_key(db, di, t, tl);
+        if (r == R_PANIC) { res = MTBLX_GET_PANIC; break; }
+        if (!valid(db, di)) break;
+        if (di.voff + di.vlen > db.L) { res = MTBLX_GET_PANIC; break; }
+        if (cmp_key(di, tl) == 0) { res = MTBLX_GET_FOUND; ro = (uint64_t)(db.d - vbase) + di.voff; rl = di.vlen; }
+      } while (false);
+    }
+    if (q < nq) {
+      MTBLX_CHK(st + q, 4), MTBLX_CHK(voff + q, 8), MTBLX_CHK(vlen + q, 8);
+      st[q] = res;
+      voff[q] = ro;
+      vlen[q] = rl;
+    }
   }
 }
 
@@ -882,29 +1041,50 @@ extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t 
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
 
-extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
-                         uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
-                         uint64_t* val_off, uint64_t* val_len, void* stream) {
-  if (nq == 0) return MTBLX_OK;
-  if (!file || !keys || !key_end || !status || !val_off || !val_len || version > 1) return MTBLX_E_INVAL;
-  static int grid = 0;
+// k_get_lanes (one lane per query) unless MTBLX_GET_KERNEL=wave (k_get, one wave per query: A/B)
+static void get_launch(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
+                       uint64_t index_len, mtblx_rd::DecTab tab, const uint8_t* keys, const uint64_t* key_end,
+                       uint32_t nq, int32_t* status, uint64_t* val_off, uint64_t* val_len, hipStream_t s) {
+  static int grid = 0, wave = -1;
   if (!grid) {
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     grid = (ncu > 0 ? ncu : 256) * 8;
   }
-  const uint32_t need = (nq + 3u) / 4u;
-  MTBLX_LAUNCH((MTBLX_R(file, file_len), keys, MTBLX_R(key_end, 8ull * nq), MTBLX_R(status, 4ull * nq),
-                MTBLX_R(val_off, 8ull * nq), MTBLX_R(val_len, 8ull * nq)),
-               mtblx_rd::k_get,
-               dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
-                     mtblx_rd::DecTab{nullptr, nullptr, nullptr, nullptr, 0u, nullptr}, keys, key_end, nq, status,
-                     val_off, val_len);
-  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+  if (wave < 0) {
+    const char* e = getenv("MTBLX_GET_KERNEL");
+    wave = e && e[0] == 'w' ? 1 : 0;
+  }
+  const uint64_t per = wave ? 4u : 256u;   // queries per workgroup per pass
+  const uint64_t need = (nq + per - 1) / per;
+  const dim3 g((unsigned)(need < (uint64_t)grid ? need : (uint64_t)grid));
+  const uint64_t ntab = tab.dec ? tab.n : 0;
+  if (wave) {
+    MTBLX_LAUNCH((MTBLX_R(file, file_len), MTBLX_R(tab.start, 8ull * ntab), MTBLX_R(tab.doff, 8ull * ntab),
+                  MTBLX_R(tab.dlen, 8ull * ntab), MTBLX_R(tab.st, 4ull * ntab), tab.dec, keys, MTBLX_R(key_end, 8ull * nq),
+                  MTBLX_R(status, 4ull * nq), MTBLX_R(val_off, 8ull * nq), MTBLX_R(val_len, 8ull * nq)),
+                 mtblx_rd::k_get, g, dim3(256), 0, s, file, file_len, version, verify, index_off, index_len, tab, keys,
+                 key_end, nq, status, val_off, val_len);
+  } else {
+    MTBLX_LAUNCH((MTBLX_R(file, file_len), MTBLX_R(tab.start, 8ull * ntab), MTBLX_R(tab.doff, 8ull * ntab),
+                  MTBLX_R(tab.dlen, 8ull * ntab), MTBLX_R(tab.st, 4ull * ntab), tab.dec, keys, MTBLX_R(key_end, 8ull * nq),
+                  MTBLX_R(status, 4ull * nq), MTBLX_R(val_off, 8ull * nq), MTBLX_R(val_len, 8ull * nq)),
+                 mtblx_rd::k_get_lanes, g, dim3(256), 0, s, file, file_len, version, verify, index_off, index_len, tab,
+                 keys, key_end, nq, status, val_off, val_len);
+  }
 }
 
+extern "C" int mtblx_get(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
+                         uint64_t index_len, const uint8_t* keys, const uint64_t* key_end, uint32_t nq, int32_t* status,
+                         uint64_t* val_off, uint64_t* val_len, void* stream) {
+  if (nq == 0) return MTBLX_OK;
+  if (!file || !keys || !key_end || !status || !val_off || !val_len || version > 1) return MTBLX_E_INVAL;
+  get_launch(file, file_len, version, verify, index_off, index_len,
+             mtblx_rd::DecTab{nullptr, nullptr, nullptr, nullptr, 0u, nullptr}, keys, key_end, nq, status, val_off,
+             val_len, reinterpret_cast<hipStream_t>(stream));
+  return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
+}
 extern "C" int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, uint32_t version, int verify,
                                       uint64_t index_off, uint64_t index_len, const uint64_t* tab_start,
                                       const uint64_t* tab_doff, const uint64_t* tab_dlen, const int32_t* tab_st,
@@ -914,21 +1094,9 @@ extern "C" int mtblx_get_decompressed(const uint8_t* file, uint64_t file_len, ui
   if (nq == 0) return MTBLX_OK;
   if (!file || !keys || !key_end || !status || !val_off || !val_len || version > 1 || !dec) return MTBLX_E_INVAL;
   if (ntab && (!tab_start || !tab_doff || !tab_dlen || !tab_st)) return MTBLX_E_INVAL;
-  static int grid = 0;
-  if (!grid) {
-    int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = (ncu > 0 ? ncu : 256) * 8;
-  }
-  const uint32_t need = (nq + 3u) / 4u;
-  MTBLX_LAUNCH((MTBLX_R(file, file_len), MTBLX_R(tab_start, 8ull * ntab), MTBLX_R(tab_doff, 8ull * ntab),
-                MTBLX_R(tab_dlen, 8ull * ntab), MTBLX_R(tab_st, 4ull * ntab), dec, keys, MTBLX_R(key_end, 8ull * nq),
-                MTBLX_R(status, 4ull * nq), MTBLX_R(val_off, 8ull * nq), MTBLX_R(val_len, 8ull * nq)),
-               mtblx_rd::k_get, dim3(need < (uint32_t)grid ? need : (uint32_t)grid), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), file, file_len, version, verify, index_off, index_len,
-                     mtblx_rd::DecTab{tab_start, tab_doff, tab_dlen, tab_st, ntab, dec}, keys, key_end, nq, status,
-                     val_off, val_len);
+  get_launch(file, file_len, version, verify, index_off, index_len,
+             mtblx_rd::DecTab{tab_start, tab_doff, tab_dlen, tab_st, ntab, dec}, keys, key_end, nq, status, val_off,
+             val_len, reinterpret_cast<hipStream_t>(stream));
   return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
 }
 

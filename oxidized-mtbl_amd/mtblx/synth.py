@@ -39,6 +39,24 @@ def cfg2_arrays(nrec: int, seed: int = SEED_CFG2, key_tail: int = 8, val_len: in
     return keys.reshape(-1), vals.reshape(-1), klen, val_len
 
 
+def cfg2_keys(nrec: int, seed: int = SEED_CFG2, key_tail: int = 8, c0: int = 0):
+    """the keys cfg2_arrays(nrec, seed, key_tail, c0=c0) draws, as an (nrec, 8 + key_tail) array,
+    without its values (the same generator calls, in the same order, up to the key tails)"""
+    rng = np.random.default_rng(seed)
+    gaps = rng.integers(1, 1 << 20, nrec, dtype=np.uint64)
+    c = np.cumsum(gaps, dtype=np.uint64) + np.uint64(c0)
+    keys = np.empty((nrec, 8 + key_tail), np.uint8)
+    keys[:, :8] = c.astype(">u8").view(np.uint8).reshape(nrec, 8)
+    keys[:, 8:] = rng.integers(0, 256, (nrec, key_tail), dtype=np.uint8)
+    return keys
+
+
+def cfg2_file_nrec(nblocks: int, block_size: int = 4096) -> int:
+    """the records cfg2_file generates (and writes) for `nblocks` blocks"""
+    per_block = max(1, (block_size - 64) // 79)
+    return int(nblocks * per_block * 1.02) + 64
+
+
 def write_arrays(keys, vals, klen, vlen, block_size=4096, restart_interval=16):
     n = keys.size // klen
     w = Writer(block_size, restart_interval)
@@ -56,8 +74,7 @@ def cfg2_file(nblocks: int = 100_000, block_size: int = 4096, seed: int = SEED_C
     of the file are returned in the directory (the file may hold a few more).  c0: first key
     counter (shards of one key space: cfg2_shard)."""
     # ~51 records per 4 KiB block; generous estimate then trim the directory
-    per_block = max(1, (block_size - 64) // 79)
-    nrec = int(nblocks * per_block * 1.02) + 64
+    nrec = cfg2_file_nrec(nblocks, block_size)
     keys, vals, kl, vl = cfg2_arrays(nrec, seed, c0=c0)
     data, off, ln = write_arrays(keys, vals, kl, vl, block_size=block_size)
     while off.size < nblocks:  # extremely unlikely; extend

@@ -1010,6 +1010,10 @@ extern "C" int mtblx_encode_blocks_planned(const mtblx_records* rec, const uint6
   EncArgs a{{rec->keys, rec->key_end, rec->vals, rec->val_end},
             blk_rec, nblk, restart_interval, framed ? 1 : 0, out, out_cap, blk_off, blk_len, status, totals,
             nullptr, nullptr, PA, Q, SH, h[1], m, F};
+#ifdef MTBLX_ENC_STAMPS   // diagnostic build: the stamps go to the workspace's first 256 bytes (no ticket here)
+  if (hipMemsetAsync(workspace, 0, 256, s) != hipSuccess) return MTBLX_E_HIP;
+  a.ticket = reinterpret_cast<uint32_t*>(workspace);
+#endif
   MTBLX_LAUNCH((MTBLX_R(blk_rec, 8ull * (nblk + 1)), MTBLX_R(PA, 8 * m), MTBLX_R(Q, 8 * m), MTBLX_R(F, 8ull * nblk)),
                k_enc_fsize, dim3((nblk + 255) / 256), dim3(256), 0, s, a, F);
   if (hipGetLastError() != hipSuccess) return MTBLX_E_HIP;

@@ -22,10 +22,12 @@
 // can reach the block size, and a scan over 64-record chunks (skipped whole when est at the
 // chunk's end plus the chunk's largest 15 + |k| + |v| stays below it) finds the flushing record.
 // The blocks a Writer actually cuts are the chain j0 = shard start, next(j0), next(next(j0)),
-// ...: pointer doubling builds next^8 and next^512, one thread per shard walks next^512, one
-// per waypoint walks next^8 (64 hops), one per 8-block waypoint walks next (8 hops) and writes
-// the block starts.  Every step is a parallel pass over the records, so the cut of any
-// number of shards -- one Writer over all records included -- takes a fixed handful of launches.
+// ...: pointer doubling builds JL = next^8 and JH = next^(2^lvHi) (lvHi per call, so that the
+// largest shard needs at most ~128 JH hops); one thread per shard walks JH (k_plan_top), one per
+// JH waypoint walks JL (2^(lvHi-3) hops, k_plan_mid), one per 8-block waypoint walks next (8
+// hops) and writes the block starts (k_plan_emit).  Every step is a parallel pass over the
+// records, so the cut of any number of shards -- one Writer over all records included -- takes a
+// fixed handful of launches.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -1169,3 +1169,131 @@ void oracle_scan_free(oracle_scan_result* r) {
   free(r->keys); free(r->vals); free(r->key_end); free(r->val_end);
   memset(r, 0, sizeof(*r));
 }
+
+/* ==================== full-size checker: device Writer output vs this restatement ====================
+ * TEST INFRASTRUCTURE (tests/test_cfg3_oracle_gpu.py).  For every shard (an independent Writer,
+ * src/writer.rs:112-149) of a device-encoded chunk:
+ *  - the oracle Writer (oracle_writer_insert / _finish: the flush rule :125-130, BlockBuilder::add /
+ *    finish src/block_builder.rs:49-104, write_block framing :203-237) is fed the shard's records and
+ *    its data-block region is compared frame by frame with the device's framed blocks (varint64
+ *    length, crc32c, content): res[0] += equal blocks, res[1] += device blocks of the shard;
+ *  - every device block's content is decoded by the restated seek_to_first + next/get scan
+ *    (odecode_block, src/block.rs:119-238) and each yielded record compared with the input record
+ *    (key bytes, value bytes): res[2] += equal records, res[3] += records the cut assigns;
+ *  - res[4] = first block that differs (UINT64_MAX if none), res[5] = shards whose cut, block count
+ *    or framing does not line up with the oracle Writer's.
+ * key_end / val_end: u64 END offsets from record 0; blk_rec[nblk + 1], shard_rec[nshard + 1]:
+ * record cuts (int64).  Work is split over nthreads by shard. */
+typedef struct {
+  const uint8_t* keys; const uint64_t* key_end; const uint8_t* vals; const uint64_t* val_end;
+  uint64_t r, r_end, equal, seen;
+} ochk_rec;
+static int ochk_cb(void* c, const uint8_t* k, uint64_t kl, const uint8_t* v, uint64_t vl) {
+  ochk_rec* x = (ochk_rec*)c;
+  x->seen++;
+  if (x->r < x->r_end) {
+    uint64_t k0 = x->r ? x->key_end[x->r - 1] : 0, v0 = x->r ? x->val_end[x->r - 1] : 0;
+    uint64_t ekl = x->key_end[x->r] - k0, evl = x->val_end[x->r] - v0;
+    if (ekl == kl && evl == vl && (!kl || !memcmp(k, x->keys + k0, kl)) && (!vl || !memcmp(v, x->vals + v0, vl)))
+      x->equal++;
+  }
+  x->r++;
+  return 0;
+}
+typedef struct {
+  const uint8_t* file; uint64_t file_len; const uint64_t* blk_off; const uint32_t* blk_len; uint64_t nblk;
+  const int64_t* blk_rec; const uint8_t* keys; const uint64_t* key_end; const uint8_t* vals; const uint64_t* val_end;
+  const int64_t* shard_rec; uint64_t nshard; uint64_t block_size, interval;
+  volatile uint64_t next_shard;
+  pthread_mutex_t mu;
+  uint64_t res[6];
+} ochk_job;
+static uint64_t ochk_lower(const int64_t* a, uint64_t n, int64_t v) {   /* first i in [0, n] with a[i] >= v */
+  uint64_t lo = 0, hi = n + 1;
+  while (lo < hi) { uint64_t m = (lo + hi) / 2; if (a[m] >= v) hi = m; else lo = m + 1; }
+  return lo;
+}
+static void* ochk_run(void* a) {
+  ochk_job* j = (ochk_job*)a;
+  for (;;) {
+    uint64_t s = __sync_fetch_and_add(&j->next_shard, 1);
+    if (s >= j->nshard) break;
+    uint64_t res[6] = {0, 0, 0, 0, UINT64_MAX, 0};
+    int64_t r0 = j->shard_rec[s], r1 = j->shard_rec[s + 1];
+    if (r1 > j->blk_rec[j->nblk]) r1 = j->blk_rec[j->nblk];
+    if (r0 < r1) {
+      uint64_t b0 = ochk_lower(j->blk_rec, j->nblk, r0), b1 = ochk_lower(j->blk_rec, j->nblk, r1);
+      if (b0 > j->nblk || j->blk_rec[b0] != r0 || b1 > j->nblk || j->blk_rec[b1] != r1) res[5]++;
+      if (b1 > j->nblk) b1 = j->nblk;
+      /* the oracle Writer over the shard's records */
+      oracle_writer* w = oracle_writer_new(j->block_size, j->interval, 0);
+      int bad = 0;
+      for (int64_t r = r0; r < r1 && !bad; r++) {
+        uint64_t k0 = r ? j->key_end[r - 1] : 0, v0 = r ? j->val_end[r - 1] : 0;
+        bad = oracle_writer_insert(w, j->keys + k0, j->key_end[r] - k0, j->vals + v0, j->val_end[r] - v0) != 0;
+      }
+      uint8_t* of = NULL;
+      uint64_t olen = 0;
+      if (!bad) bad = oracle_writer_finish(w, &of, &olen) != 0;
+      uint64_t data_end = bad ? 0 : w->meta[M_IDX_OFF];
+      oracle_writer_free(w);
+      uint64_t pos = 0;
+      for (uint64_t b = b0; b < b1; b++) {
+        res[1]++;
+        /* the device frame: varint64(len) | crc32c | content, ending at the content's end */
+        uint8_t lb[10];
+        uint32_t ll = oracle_varint_encode64(lb, j->blk_len[b]);
+        uint64_t fl = ll + 4 + (uint64_t)j->blk_len[b];
+        int eq = 0;
+        if (!bad && j->blk_off[b] >= ll + 4 && j->blk_off[b] + j->blk_len[b] <= j->file_len && pos + fl <= data_end) {
+          const uint8_t* dv = j->file + j->blk_off[b] - ll - 4;
+          eq = memcmp(dv, of + pos, fl) == 0;
+        }
+        if (eq) res[0]++;
+        else if (res[4] == UINT64_MAX) res[4] = b;
+        pos += fl;
+        /* the restated scan over the device block's content */
+        ochk_rec x = {j->keys, j->key_end, j->vals, j->val_end, (uint64_t)j->blk_rec[b],
+                      (uint64_t)(b + 1 <= j->nblk ? j->blk_rec[b + 1] : j->blk_rec[b]), 0, 0};
+        uint64_t n = 0;
+        int st = ORC_ST_CORRUPT;
+        if (j->blk_off[b] + j->blk_len[b] <= j->file_len)
+          st = odecode_block(j->file + j->blk_off[b], j->blk_len[b], ochk_cb, &x, &n);
+        uint64_t want = x.r_end - (uint64_t)j->blk_rec[b];
+        res[3] += want;
+        if (st == ORC_ST_OK && x.seen == want) res[2] += x.equal;
+        else if (res[4] == UINT64_MAX) res[4] = b;
+      }
+      if (bad || pos != data_end) res[5]++;
+      free(of);
+    }
+    pthread_mutex_lock(&j->mu);
+    for (int i = 0; i < 4; i++) j->res[i] += res[i];
+    if (res[4] < j->res[4]) j->res[4] = res[4];
+    j->res[5] += res[5];
+    pthread_mutex_unlock(&j->mu);
+  }
+  return NULL;
+}
+int32_t oracle_check_writer_blocks(const uint8_t* file, uint64_t file_len, const uint64_t* blk_off,
+                                   const uint32_t* blk_len, uint64_t nblk, const int64_t* blk_rec,
+                                   const uint8_t* keys, const uint64_t* key_end, const uint8_t* vals,
+                                   const uint64_t* val_end, const int64_t* shard_rec, uint64_t nshard,
+                                   uint64_t block_size, uint64_t interval, int nthreads, uint64_t* res) {
+  ochk_job j;
+  memset(&j, 0, sizeof j);
+  j.file = file; j.file_len = file_len; j.blk_off = blk_off; j.blk_len = blk_len; j.nblk = nblk;
+  j.blk_rec = blk_rec; j.keys = keys; j.key_end = key_end; j.vals = vals; j.val_end = val_end;
+  j.shard_rec = shard_rec; j.nshard = nshard; j.block_size = block_size; j.interval = interval;
+  j.res[4] = UINT64_MAX;
+  pthread_mutex_init(&j.mu, NULL);
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int i = 1; i < nthreads; i++) pthread_create(&th[i], NULL, ochk_run, &j);
+  ochk_run(&j);
+  for (int i = 1; i < nthreads; i++) pthread_join(th[i], NULL);
+  free(th);
+  pthread_mutex_destroy(&j.mu);
+  memcpy(res, j.res, sizeof j.res);
+  return 0;
+}

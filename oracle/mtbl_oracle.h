@@ -145,6 +145,16 @@ int32_t oracle_iter_script(const uint8_t* data, uint64_t len, int32_t verify, in
                            oracle_scan_result* res);
 void oracle_scan_free(oracle_scan_result* res);
 
+/* Full-size parity checker (tests/test_cfg3_oracle_gpu.py): device-encoded framed blocks of
+ * independent Writers (shards) against the oracle Writer shard by shard, and every block's decode
+ * against the input records.  res[6] = {equal blocks, blocks, equal records, records, first bad
+ * block (UINT64_MAX if none), shards that do not line up}.  See mtbl_oracle.c. */
+int32_t oracle_check_writer_blocks(const uint8_t* file, uint64_t file_len, const uint64_t* blk_off,
+                                   const uint32_t* blk_len, uint64_t nblk, const int64_t* blk_rec,
+                                   const uint8_t* keys, const uint64_t* key_end, const uint8_t* vals,
+                                   const uint64_t* val_end, const int64_t* shard_rec, uint64_t nshard,
+                                   uint64_t block_size, uint64_t interval, int nthreads, uint64_t* res);
+
 /* zlib / zstd block decompression (src/compression.rs:85-92, :140-145): 0 ok, *out malloc'd */
 int32_t oracle_zlib_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len);
 int32_t oracle_zstd_decompress(const uint8_t* s, uint64_t n, uint8_t** out, uint64_t* out_len);

@@ -350,3 +350,34 @@ def iter_script(data: bytes, mode="iter", key=b"", key2=b"", ops=(), verify=True
                ops=[(int(ores[2 * i]), int(ores[2 * i + 1])) for i in range(len(code))])
     lib().oracle_scan_free(C.byref(r))
     return out
+
+
+# ---------------- full-size checker (tests/test_cfg3_oracle_gpu.py) ----------------
+def check_writer_blocks(file: np.ndarray, blk_off, blk_len, blk_rec, keys, key_end, vals, val_end, shard_rec,
+                        block_size: int, restart_interval: int, nthreads: int = 16) -> dict:
+    """oracle_check_writer_blocks: framed device blocks vs the oracle Writer per shard, and every
+    block's restated decode vs the input records.  Host numpy arrays (u8 / u64 / u32 / i64)."""
+    L = lib()
+    if not hasattr(L.oracle_check_writer_blocks, "_set"):
+        L.oracle_check_writer_blocks.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
+                                                 C.c_void_p]
+        L.oracle_check_writer_blocks.restype = C.c_int32
+        L.oracle_check_writer_blocks._set = True
+    f = np.ascontiguousarray(file, np.uint8)
+    off = np.ascontiguousarray(blk_off, np.uint64)
+    ln = np.ascontiguousarray(blk_len, np.uint32)
+    br = np.ascontiguousarray(blk_rec, np.int64)
+    sr = np.ascontiguousarray(shard_rec, np.int64)
+    kb, vb = np.ascontiguousarray(keys, np.uint8), np.ascontiguousarray(vals, np.uint8)
+    ke, ve = np.ascontiguousarray(key_end, np.uint64), np.ascontiguousarray(val_end, np.uint64)
+    nb = off.size
+    assert ln.size == nb and br.size == nb + 1 and ke.size == ve.size and ke.size >= int(br[-1])
+    res = np.zeros(6, np.uint64)
+    L.oracle_check_writer_blocks(f.ctypes.data, f.size, off.ctypes.data, ln.ctypes.data, nb, br.ctypes.data,
+                                 kb.ctypes.data, ke.ctypes.data, vb.ctypes.data, ve.ctypes.data, sr.ctypes.data,
+                                 sr.size - 1, block_size, restart_interval, nthreads, res.ctypes.data)
+    bad = int(res[4])
+    return dict(blocks_equal=int(res[0]), blocks=int(res[1]), records_equal=int(res[2]), records=int(res[3]),
+                first_bad_block=None if bad == (1 << 64) - 1 else bad, shards_misaligned=int(res[5]))

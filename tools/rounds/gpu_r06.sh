@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round 6 GPU session: MODES = tests | smoke | bench | cfg3 | cfg3oracle | bounds | ... (space separated).
+# Outputs under gpurun_out/r06/<TAG>/.  Every GPU step has its own time limit; a step that
+# times out, aborts or faults ends the call (test failures, rc 1, of a gpu_* step do not).
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r06/${TAG:-run}
+mkdir -p $O
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -3 "$O/$name.log" | cut -c1-600
+  if [ $rc -eq 1 ] && [ "${name%%_*}" = gpu ]; then echo "(test failures: going on)"; return 0; fi
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+}
+PT="python -u -m pytest -v -s --timeout 300 --timeout-method thread -p no:cacheprovider"
+for MODE in ${MODES:-tests smoke bench}; do
+case $MODE in
+tests) step gpu_tests 1000 $PT tests -m gpu --deselect tests/test_spill_gpu.py::test_spilling_build_is_exact ${PYTEST_ARGS:-} ;;
+sel) step gpu_sel 600 $PT ${SEL} ;;
+smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+bench) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+cfg3) step cfg3 900 python -u bench.py --config cfg3 --steps 3 --warmup 1 ;;
+cfg3oracle)   # every cfg3 block against the oracle, full size (1 M blocks, 10 chunks)
+  rm -f $O/cfg3_oracle.txt
+  step gpu_cfg3_oracle 1100 env MTBLX_CFG3_BLOCKS=${CFG3_BLOCKS:-1000000} MTBLX_CFG3_LOG=$O/cfg3_oracle.txt \
+    python -u -m pytest -v -s --timeout 1050 --timeout-method thread -p no:cacheprovider tests/test_cfg3_oracle_gpu.py ;;
+bounds) step gpu_bounds 1150 env MTBLX_LIB=oxidized-mtbl_amd/build/libmtblx_bounds.so MTBLX_BOUNDS_CHECK=1 $PT tests -m gpu --deselect tests/test_spill_gpu.py::test_spilling_build_is_exact ${PYTEST_ARGS:-} ;;
+*) echo "unknown mode $MODE"; exit 2 ;;
+esac
+done
+echo "=== done"

@@ -537,6 +537,8 @@ def run_cfg3(args, dist, world, rank):
                file_bytes=0, mismatches=0, chunks=0)
     done = 0
     ci = 0
+    # the block cut's scratch (caller-owned, mtblx_plan_workspace_bytes), sized once for the largest chunk
+    pws = encode.PlanWorkspace(int(min(per_chunk, total_blocks) * rec_per_blk * 1.03) + 1024, 64, 16, keep=True)
     while done < total_blocks:
         want = min(per_chunk, total_blocks - done)
         nrec = int(want * rec_per_blk * 1.03) + 1024
@@ -547,7 +549,7 @@ def run_cfg3(args, dist, world, rank):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         # the Writer's block cut, its sums kept for the encode (mtblx_encode_plan_keep)
-        blk, kept = encode.plan(recs, 65536, 16, shard_rec=cuts, keep=True)
+        blk, kept = encode.plan(recs, 65536, 16, shard_rec=cuts, keep=True, workspace=pws)
         acc["plan_ms"] += (time.perf_counter() - t0) * 1e3
         blk = blk[: want + 1].contiguous()
         nb = int(blk.numel()) - 1

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MTBLX_ABI_VERSION 2
+#define MTBLX_ABI_VERSION 3   /* 3: the block cut takes a caller-owned workspace (round 6) */
 
 /* ---- API return codes ---- */
 #define MTBLX_OK 0
@@ -359,22 +359,36 @@ typedef struct mtblx_records {
 #define MTBLX_PLAN_OUT_OF_ORDER 1u /* a key <= its predecessor: panic!("out-of-order key") (:119-123) */
 #define MTBLX_PLAN_PANIC 2u        /* restart_interval 0 and a second entry: assert (src/block_builder.rs:50) */
 #define MTBLX_PLAN_TOO_LONG 4u     /* a key or value >= 4 GiB (u32 varint lengths)                    */
+/* Scratch (device, 256-byte aligned, no fill needed) of the parallel cut for up to `nrec` records in
+ * `nshard` shards at this interval; keep != 0 for mtblx_encode_plan_keep (whose entry sizes live in
+ * the plan buffer).  A bound that holds for any record sizes, ~50 B per record.  The library keeps
+ * no scratch between calls: one workspace serves one call at a time. */
+size_t mtblx_plan_workspace_bytes(uint64_t nrec, uint32_t nshard, uint32_t restart_interval, int keep);
+/* The serial walk's scratch (one wave per shard, the round-1..4 cut): 16 B per shard. */
+size_t mtblx_plan_serial_workspace_bytes(uint32_t nshard);
+/* workspace: at least mtblx_plan_workspace_bytes(records of the shards, nshard, restart_interval, 0)
+ * runs the parallel cut (every record's next block start at once + pointer doubling); a smaller one,
+ * of at least mtblx_plan_serial_workspace_bytes(nshard), the serial walk (same cut; also taken for
+ * record ranges of 2^32 - 16 or more and under MTBLX_PLAN=serial).  NULL or misaligned: MTBLX_E_INVAL. */
 int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
                       uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
-                      uint32_t* flags_out, void* stream);
+                      uint32_t* flags_out, void* workspace, size_t ws_bytes, void* stream);
 
 /* The same block cut, keeping what the encode needs (round 5): `plan` (device, 256-byte aligned,
  * mtblx_plan_keep_bytes(number of records in the shards) bytes) receives every record's entry size
  * summed in order, the bytes a restart entry loses by not sharing summed along residue classes
- * mod restart_interval, and every record's shared-prefix length with its predecessor.
- * restart_interval must be >= 1.  Returns like mtblx_encode_plan. */
+ * mod restart_interval, and every record's shared-prefix length with its predecessor (across shard
+ * starts too).  restart_interval must be >= 1, the shards must hold fewer than 2^32 - 16 records and
+ * the workspace at least mtblx_plan_workspace_bytes(..., keep = 1): otherwise MTBLX_E_INVAL (no
+ * serial fallback: cut with mtblx_encode_plan and encode with mtblx_encode_blocks instead).
+ * Returns like mtblx_encode_plan. */
 size_t mtblx_plan_keep_bytes(uint64_t nrec);
-/* mtblx_encode_plan / _keep cache their device scratch (~50 B per record) across calls; this
- * frees it (the next call allocates again). */
+/* ABI v2 compatibility: a no-op (the cut used to cache its scratch; it keeps none now). */
 void mtblx_plan_release(void);
 int mtblx_encode_plan_keep(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
                            uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
-                           uint32_t* flags_out, void* plan, size_t plan_bytes, void* stream);
+                           uint32_t* flags_out, void* plan, size_t plan_bytes, void* workspace, size_t ws_bytes,
+                           void* stream);
 
 /* BlockBuilder::add for every record of a block, then finish (src/block_builder.rs:49-104),
  * for every block b of blk_rec at once.  framed != 0 adds write_block's framing before each

@@ -2200,7 +2200,8 @@ __device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileAr
   }
 }
 
-// The fused checksum on the matrix cores (MTBLX_FUSED_MFMA, default): the staged blocks' CRC-32C
+// The fused checksum on the matrix cores (MTBLX_FUSED_MFMA=1, the A/B variant; the default, 0, is
+// the VALU slicing path below, which measured faster -- DESIGN §0.4 item 6): the staged blocks' CRC-32C
 // by the method of k_crc32c_mfma (crc_mfma.h) read straight from the tile's LDS stage.  Work unit
 // = (block j, super-window sw: 8 steps of 1 KiB counted from the block's 16-byte aligned end in
 // the stage); copy wave cw takes units cw, cw + NC, ... of the tile after its copy.  Per step a
@@ -2208,7 +2209,7 @@ __device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileAr
 // and folds the init into bytes 0..3 (head_chunk), masks the pad after the block end
 // (tail_chunk), then 8 fp4 + 2 f16 MFMAs (mfma_step); per unit the column parities, the column
 // and super-window shifts and the pad removal x^(-8t) (nibble tables), XORed into the block's
-// accumulator.  Round 4's VALU window loop (slicing-by-4, MTBLX_FUSED_MFMA=0) stays for A/B.
+// accumulator.  Round 4's VALU window loop (slicing-by-4, MTBLX_FUSED_MFMA=0) is the product.
 #ifndef MTBLX_FUSED_MFMA
 #define MTBLX_FUSED_MFMA 0
 #endif

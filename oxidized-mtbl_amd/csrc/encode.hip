@@ -714,7 +714,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   if (iv == 0 && n > 1) st = MTBLX_ST_CORRUPT;            // assert!(counter <= interval) (:50)
   if (entries > 0xFFFFFFFFull) st = MTBLX_ST_UNSUPPORTED;  // u64 restart arrays: blocks >= 4 GiB
   const uint64_t L = entries + 4 * nrest + 4;
-  const uint64_t F = a.framed ? vlen64(L) + 4 + L : L;
+  // a planned block outside the plan was counted 0 by k_enc_fsize: F = 0 keeps totals[0] the scan's total
+  const uint64_t F = !pl_ok ? 0 : (a.framed ? vlen64(L) + 4 + L : L);
   if (!PL && tid == 0) {   // publish this block's framed size as early as possible
     __hip_atomic_store(a.lbw + b, (b == 0 ? kIncl : kAgg) | F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -799,7 +800,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     if (w != 0 || PL) crc_mfma_part(S, (uint32_t)L);
   }
   if constexpr (PL) {   // the file offset: the scan of the framed sizes
-    if (tid == 0) S.sh_u64[0] = pl_ok ? a.fincl[b] - F : 0;
+    if (tid == 0) S.sh_u64[0] = a.fincl[b] - F;
   } else if (w == 0) {
     bool to = false;
     const uint64_t excl = b == 0 ? 0 : lookback(a, b, lane, to);
@@ -905,15 +906,17 @@ extern "C" size_t mtblx_encode_workspace_bytes(uint32_t nblk) {
 }
 
 // the round-1..4 block cut: one wave per shard walking the Writer's chain (plan.hip dispatches here
-// for MTBLX_PLAN=serial and record ranges of 2^32 or more)
+// for MTBLX_PLAN=serial, record ranges of 2^32 or more, and workspaces too small for the parallel
+// cut).  Scratch from the caller's workspace: [nshard] counts | [nshard] firsts | flags.
 extern "C" int mtblx_encode_plan_serial(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
                                         uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
-                                 uint64_t* nblk_out, uint32_t* flags_out, void* stream) {
+                                        uint64_t* nblk_out, uint32_t* flags_out, void* workspace, size_t ws_bytes,
+                                        void* stream) {
   if (!rec || !shard_rec || !nblk_out || nshard == 0) return MTBLX_E_INVAL;
+  if (!workspace || ws_bytes < 16ull * nshard + 16 || (reinterpret_cast<uintptr_t>(workspace) & 7u)) return MTBLX_E_INVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (block_size < 1024) block_size = 1024;   // WriterBuilder::block_size clamp (src/writer.rs:43-46)
-  uint64_t* d = nullptr;   // [nshard] counts | [nshard] firsts | flags
-  if (hipMalloc(reinterpret_cast<void**>(&d), 16ull * nshard + 16) != hipSuccess) return MTBLX_E_HIP;
+  uint64_t* d = static_cast<uint64_t*>(workspace);
   uint32_t* dflags = reinterpret_cast<uint32_t*>(d + 2 * nshard);
   int rc = MTBLX_OK;
   std::vector<uint64_t> cnt(nshard), first(nshard);
@@ -949,7 +952,6 @@ extern "C" int mtblx_encode_plan_serial(const mtblx_records* rec, const uint64_t
     rc = MTBLX_E_INVAL;   // blk_cap too small: *nblk_out says how many are needed
   }
   if (hipStreamSynchronize(s) != hipSuccess) rc = MTBLX_E_HIP;
-  (void)hipFree(d);
   if (rc == MTBLX_OK && (fl & (MTBLX_PLAN_OUT_OF_ORDER | MTBLX_PLAN_PANIC | MTBLX_PLAN_TOO_LONG))) rc = MTBLX_E_FORMAT;
   return rc;
 }

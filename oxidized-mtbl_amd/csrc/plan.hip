@@ -34,7 +34,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <mutex>
 #include <vector>
 
 #include "bounds.h"
@@ -42,7 +41,8 @@
 
 extern "C" int mtblx_encode_plan_serial(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
                                         uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec,
-                                        uint64_t blk_cap, uint64_t* nblk_out, uint32_t* flags_out, void* stream);
+                                        uint64_t blk_cap, uint64_t* nblk_out, uint32_t* flags_out, void* workspace,
+                                        size_t ws_bytes, void* stream);
 
 namespace mtblx_plan {
 
@@ -111,7 +111,11 @@ __global__ void __launch_bounds__(kT) k_plan_rec(RecArgs a) {
       if (kl > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) fl |= MTBLX_PLAN_TOO_LONG;
       const uint32_t s = shard_of(a.sb, a.nsh, j);
       uint64_t sh = 0;
-      if (j != a.sb[s]) {   // not a Writer's first record: shared prefix + order (src/writer.rs:119-123)
+      // the shared prefix with the predecessor (also across a shard start: a block of another cut
+      // that spans it shares there, mtblx_encode_blocks_planned; the Writer's own cut starts a
+      // block at every shard start, where the restart entry pays D back); the order check only
+      // inside a Writer (src/writer.rs:119-123)
+      if (i > 0) {
         const uint64_t p0 = i > 1 ? a.R.key_end[i - 2] : 0, pl = k0 - p0;
         const uint8_t* x = a.R.keys + p0;
         const uint8_t* y = a.R.keys + k0;
@@ -134,7 +138,7 @@ __global__ void __launch_bounds__(kT) k_plan_rec(RecArgs a) {
           while (c < mm && (MTBLX_CHK(x + c, 1), MTBLX_CHK(y + c, 1), x[c] == y[c])) ++c;
           cmp = c < mm ? (x[c] < y[c] ? -1 : 1) : (pl < kl ? -1 : (pl > kl ? 1 : 0));
         }
-        if (cmp >= 0) fl |= MTBLX_PLAN_OUT_OF_ORDER;
+        if (cmp >= 0 && j != a.sb[s]) fl |= MTBLX_PLAN_OUT_OF_ORDER;
         sh = c;
       }
       const uint64_t A = entry_bytes(sh, kl, vl), Z = entry_bytes(0, kl, vl);
@@ -407,7 +411,8 @@ struct WalkArgs {
   uint32_t* n12;           // [nsh]
   uint32_t* W12;           // [slots]
   uint32_t* n6;            // [slots]
-  uint32_t* W6;            // [slots * 64]
+  const uint64_t* base6;   // [nsh + 1] W6 bases: shard s holds ceil(r_s / 8) next^8 waypoints at most
+  uint32_t* W6;            // [base6[nsh]]
   const uint32_t* J0;
   const uint32_t* J6;
   const uint32_t* J12;
@@ -441,7 +446,10 @@ __global__ void __launch_bounds__(kT) k_plan_top(WalkArgs a) {
   a.n12[s] = c;
 }
 
-// one thread per next^512 waypoint slot: its (up to) 64 next^8 waypoints
+// one thread per next^(2^lvHi) waypoint slot: its (up to) `mid` next^8 waypoints.  Waypoint q of
+// shard s writes W6[base6[s] + q * mid + c]: every slot before the shard's last one is full (a JH
+// hop is `mid` JL hops), so index q * mid + c counts JL waypoints from the shard start, i.e. block
+// starts / 8 < ceil(r_s / 8) -- the shard's W6 range is sized by its own records (not by `top`)
 __global__ void __launch_bounds__(kT) k_plan_mid(WalkArgs a) {
   const uint64_t u = (uint64_t)blockIdx.x * kT + threadIdx.x;
   if (u >= a.slots) return;
@@ -453,10 +461,11 @@ __global__ void __launch_bounds__(kT) k_plan_mid(WalkArgs a) {
   uint32_t c = 0;
   if (u - a.base12[s] < a.n12[s]) {
     const uint64_t e = a.sb[s + 1];
+    const uint64_t w0 = a.base6[s] + (u - a.base12[s]) * a.mid, w1 = a.base6[s + 1];
     uint64_t cur = a.W12[u];
-    for (c = 0; c < a.mid;) {
-      MTBLX_CHK(a.W6 + u * a.mid + c, 4), MTBLX_CHK(a.J6 + cur, 4);
-      a.W6[u * a.mid + c] = (uint32_t)cur;
+    for (c = 0; c < a.mid && w0 + c < w1;) {
+      MTBLX_CHK(a.W6 + w0 + c, 4), MTBLX_CHK(a.J6 + cur, 4);
+      a.W6[w0 + c] = (uint32_t)cur;
       ++c;
       const uint64_t nx = a.J6[cur];
       if (nx >= e) break;
@@ -476,7 +485,7 @@ __global__ void __launch_bounds__(kT) k_plan_count(WalkArgs a) {
     const uint64_t u = a.base12[s] + a.n12[s] - 1;
     const uint32_t c6 = a.n6[u];
     const uint64_t e = a.sb[s + 1];
-    uint64_t cur = a.W6[u * a.mid + c6 - 1], c = 0;
+    uint64_t cur = a.W6[a.base6[s] + (uint64_t)(a.n12[s] - 1) * a.mid + c6 - 1], c = 0;
     while (true) {
       ++c;
       const uint64_t nx = a.J0[cur];
@@ -488,19 +497,21 @@ __global__ void __launch_bounds__(kT) k_plan_count(WalkArgs a) {
   a.nb[s] = n;
 }
 
-// one thread per next^8 waypoint slot: its (up to) 8 blocks -> blk_rec; the restart-interval-0
+// one thread per next^8 waypoint slot of W6: its (up to) 8 blocks -> blk_rec; the restart-interval-0
 // panic of any block holding two records
 __global__ void __launch_bounds__(kT) k_plan_emit(WalkArgs a) {
   const uint64_t v = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (v >= a.slots * a.mid) return;
-  const uint64_t u = v / a.mid, w = v % a.mid;
-  uint32_t s = 0, hi = a.nsh;
+  if (v >= a.base6[a.nsh]) return;
+  uint32_t s = 0, hi = a.nsh;   // the shard whose W6 range holds v: last s with base6[s] <= v
   while (hi - s > 1) {
     const uint32_t mid = (s + hi) >> 1;
-    if (a.base12[mid] <= u) s = mid; else hi = mid;
+    if (a.base6[mid] <= v) s = mid; else hi = mid;
   }
-  const uint64_t q = u - a.base12[s];
-  if (q >= a.n12[s] || w >= a.n6[u]) return;
+  const uint64_t q = (v - a.base6[s]) / a.mid, w = (v - a.base6[s]) % a.mid;
+  if (q >= a.n12[s]) return;
+  const uint64_t u = a.base12[s] + q;
+  MTBLX_CHK(a.n6 + u, 4);
+  if (w >= a.n6[u]) return;
   const uint64_t e = a.sb[s + 1];
   uint64_t cur = a.W6[v];
   uint64_t out = a.bb ? a.bb[s] + q * a.top + w * kLow : 0;
@@ -633,22 +644,6 @@ int sscan(uint64_t* X, uint64_t m, uint64_t w, uint64_t* S, hipStream_t s) {
 
 using namespace mtblx_plan;
 
-static std::mutex g_ws_mu;   // the planner's cached scratch
-static uint8_t* g_ws = nullptr;
-static size_t g_ws_bytes = 0;
-static int g_ws_dev = -1;
-
-extern "C" void mtblx_plan_release(void) {
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  if (g_ws) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(g_ws);
-  }
-  g_ws = nullptr;
-  g_ws_bytes = 0;
-  g_ws_dev = -1;
-}
-
 // the kept plan (mtblx_encode_plan_keep): header, then PA [m] u64, Q [m] u64, SH [m] u32
 struct KeepHdr {
   uint64_t magic, lo, m, iv;
@@ -656,10 +651,63 @@ struct KeepHdr {
 constexpr uint64_t kKeepMagic = 0x4e414c5058544d31ull;   // "1MTXPLAN"
 inline size_t keep_bytes(uint64_t n) { return 256 + 16 * (n + 1) + 4 * (n + 1) + 256; }
 
+// The parallel cut's scratch, carved from the caller's workspace (the library keeps none of its
+// own).  Sized by bounds that hold whatever the record sizes: the next^(2^lvHi) waypoint slots,
+// sum over shards of ceil(r_s / top) <= m / 16 + nshard (top >= 16), and the next^8 waypoints,
+// sum of ceil(r_s / 8) <= m / 8 + nshard -- so the size depends on (records, shards, interval) only.
+struct PlanLayout {
+  size_t oA, oD, oG, oGM, oS, oSB, oB12, oB6, oNB, oBB, oMX, oFL, oE, oJ0, oT1, oT2, oJ6, oJ12, oN12, oW12, oN6, oW6,
+      oPAN, bytes;
+};
+static PlanLayout plan_layout(uint64_t m, uint32_t nshard, uint32_t iv, bool keep) {
+  PlanLayout L{};
+  const uint64_t m1 = std::max<uint64_t>(m, 1), nchunk = std::max<uint64_t>((m + 63) / 64, 1);
+  const uint64_t scan_words = std::max<uint64_t>(std::max(sscan_words(m, 1), iv ? sscan_words(m, iv) : 0), 1);
+  const uint64_t slots = m / 16 + nshard + 1, w6 = m / 8 + nshard + 1;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+  // 8-byte arrays first (A and D live in the kept plan in keep mode)
+  L.oA = keep ? 0 : take(8 * m1);
+  L.oD = keep ? 0 : take(8 * m1);
+  L.oG = take(8 * m1);
+  L.oGM = take(8 * nchunk);
+  L.oS = take(8 * scan_words);
+  L.oSB = take(8ull * (nshard + 1));
+  L.oB12 = take(8ull * (nshard + 1));
+  L.oB6 = take(8ull * (nshard + 1));
+  L.oNB = take(8ull * nshard);
+  L.oBB = take(8ull * nshard);
+  L.oMX = take(8);
+  L.oFL = take(4);
+  L.oE = take(4 * ((m1 + 32) / 32 + 1));
+  L.oJ0 = take(4 * m1);
+  L.oT1 = take(4 * m1);
+  L.oT2 = take(4 * m1);
+  L.oJ6 = take(4 * m1);
+  L.oJ12 = take(4 * m1);
+  L.oN12 = take(4ull * nshard);
+  L.oW12 = take(4 * slots);
+  L.oN6 = take(4 * slots);
+  L.oW6 = take(4 * w6);
+  L.oPAN = take(iv == 0 ? m1 : 1);
+  L.bytes = off;
+  return L;
+}
+inline size_t serial_ws_bytes(uint32_t nshard) { return 16ull * nshard + 256; }
+
+extern "C" size_t mtblx_plan_workspace_bytes(uint64_t nrec, uint32_t nshard, uint32_t restart_interval, int keep) {
+  return plan_layout(nrec, nshard ? nshard : 1u, restart_interval, keep != 0).bytes;
+}
+extern "C" size_t mtblx_plan_serial_workspace_bytes(uint32_t nshard) { return serial_ws_bytes(nshard ? nshard : 1u); }
+// ABI v2 compatibility: the cut used to cache its scratch in the library; it holds none now
+extern "C" void mtblx_plan_release(void) {}
+
 static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard, uint64_t block_size,
                      uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap, uint64_t* nblk_out,
-                     uint32_t* flags_out, void* keep, size_t keep_cap, void* stream) {
+                     uint32_t* flags_out, void* keep, size_t keep_cap, void* workspace, size_t ws_bytes,
+                     void* stream) {
   if (!rec || !shard_rec || !nblk_out || nshard == 0) return MTBLX_E_INVAL;
+  if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 255u)) return MTBLX_E_INVAL;
   static const int serial = [] {
     const char* e = getenv("MTBLX_PLAN");
     return e && !strcmp(e, "serial") ? 1 : 0;
@@ -684,16 +732,24 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
     if (sh[i + 1] < sh[i]) return MTBLX_E_INVAL;
   if (hi > rec->n) return MTBLX_E_INVAL;
   const uint64_t m = hi - lo;
-  if (keep && (keep_cap < keep_bytes(m) || (reinterpret_cast<uintptr_t>(keep) & 255u) || restart_interval == 0))
+  // keep mode: the kept sums are the encode's, and the 32-bit next / waypoint arrays and FastDiv
+  // need m < 2^32 - 16 -- no serial fallback here (the caller cuts without keep instead)
+  if (keep && (keep_cap < keep_bytes(m) || (reinterpret_cast<uintptr_t>(keep) & 255u) || restart_interval == 0 ||
+               m >= 0xFFFFFFF0ull))
     return MTBLX_E_INVAL;
-  if (!keep && (serial || m >= 0xFFFFFFF0ull))
-    return mtblx_encode_plan_serial(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out,
-                                    flags_out, stream);
-  if (block_size < 1024) block_size = 1024;   // WriterBuilder::block_size clamp (src/writer.rs:43-46)
   const uint32_t iv = restart_interval;
-  // slot bases of the next^512 waypoints: a shard of r records has at most ceil(r / 512)
-  std::vector<uint64_t> sb(nshard + 1), base12(nshard + 1);
-  base12[0] = 0;
+  const PlanLayout Ly = plan_layout(m, nshard, iv, keep != nullptr);
+  if (keep && ws_bytes < Ly.bytes) return MTBLX_E_INVAL;
+  // a workspace too small for the parallel cut (or MTBLX_PLAN=serial, or >= 2^32 - 16 records):
+  // the serial walk, whose scratch is 16 B per shard (mtblx_plan_serial_workspace_bytes)
+  if (!keep && (serial || m >= 0xFFFFFFF0ull || ws_bytes < Ly.bytes))
+    return mtblx_encode_plan_serial(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out,
+                                    flags_out, workspace, ws_bytes, stream);
+  if (block_size < 1024) block_size = 1024;   // WriterBuilder::block_size clamp (src/writer.rs:43-46)
+  // slot bases of the next^(2^lvHi) waypoints (a shard of r records has at most ceil(r / top)) and
+  // of the next^8 waypoints (at most ceil(r / 8))
+  std::vector<uint64_t> sb(nshard + 1), base12(nshard + 1), base6(nshard + 1);
+  base12[0] = base6[0] = 0;
   uint64_t maxr = 0;
   for (uint32_t i = 0; i <= nshard; ++i) sb[i] = sh[i] - lo;
   for (uint32_t i = 0; i < nshard; ++i) maxr = std::max<uint64_t>(maxr, sb[i + 1] - sb[i]);
@@ -706,51 +762,22 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
     while (lvHi < 20 && blocks / (double)(1u << lvHi) > 128.0) ++lvHi;
   }
   const uint32_t top = 1u << lvHi, mid = top / kLow;
-  for (uint32_t i = 0; i < nshard; ++i) base12[i + 1] = base12[i] + (sb[i + 1] - sb[i] + top - 1) / top;
-  const uint64_t slots = base12[nshard];
+  for (uint32_t i = 0; i < nshard; ++i) {
+    base12[i + 1] = base12[i] + (sb[i + 1] - sb[i] + top - 1) / top;
+    base6[i + 1] = base6[i] + (sb[i + 1] - sb[i] + kLow - 1) / kLow;
+  }
+  const uint64_t slots = base12[nshard], w6 = base6[nshard];
   const uint64_t nchunk = (m + 63) / 64;
-  const uint64_t scan_words = std::max<uint64_t>(std::max(sscan_words(m, 1), iv ? sscan_words(m, iv) : 0), 1);
-  // one scratch allocation, 8-byte arrays first
   const uint64_t m1 = std::max<uint64_t>(m, 1);
-  size_t off = 0;
-  auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-  const size_t oA = take(8 * m1), oD = take(8 * m1), oG = take(8 * m1), oGM = take(8 * std::max<uint64_t>(nchunk, 1)),
-               oS = take(8 * scan_words), oSB = take(8 * (nshard + 1)), oB12 = take(8 * (nshard + 1)),
-               oNB = take(8 * nshard), oBB = take(8 * nshard), oMX = take(8), oFL = take(4), oE = take(4 * ((m1 + 32) / 32 + 1)),
-               oJ0 = take(4 * m1), oT1 = take(4 * m1), oT2 = take(4 * m1), oJ6 = take(4 * m1), oJ12 = take(4 * m1),
-               oN12 = take(4 * nshard), oW12 = take(4 * std::max<uint64_t>(slots, 1)), oN6 = take(4 * std::max<uint64_t>(slots, 1)),
-               oW6 = take(4 * std::max<uint64_t>(slots, 1) * mid), oPAN = take(iv == 0 ? m1 : 1);
-  // the scratch is cached across calls (grow-only; mtblx_plan_release frees it): a 66 M-record
-  // cut needs ~3 GB, and mapping that afresh each call cost more than the cut's kernels
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (g_ws && (g_ws_bytes < off || g_ws_dev != dev)) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(g_ws);
-    g_ws = nullptr;
-    g_ws_bytes = 0;
-  }
-  if (!g_ws && hipMalloc(reinterpret_cast<void**>(&g_ws), off) == hipSuccess) {
-    g_ws_bytes = off;
-    g_ws_dev = dev;
-  }
-  uint8_t* ws = g_ws;
-  if (!ws) {
-    (void)hipGetLastError();
-    if (keep) return MTBLX_E_HIP;
-    // ~50 B of scratch per record did not fit: the serial walk needs none
-    return mtblx_encode_plan_serial(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out,
-                                    flags_out, stream);
-  }
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
   auto p64 = [&](size_t o) { return reinterpret_cast<uint64_t*>(ws + o); };
   auto p32 = [&](size_t o) { return reinterpret_cast<uint32_t*>(ws + o); };
-  uint64_t *A = keep ? reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(keep) + 256) : p64(oA),
-           *D = keep ? A + (m + 1) : p64(oD), *G = p64(oG), *GM = p64(oGM), *S = p64(oS), *dsb = p64(oSB), *db12 = p64(oB12),
-           *dnb = p64(oNB), *dbb = p64(oBB), *mx = p64(oMX);
-  uint32_t *fl = p32(oFL), *bnd = p32(oE), *J0 = p32(oJ0), *T1 = p32(oT1), *T2 = p32(oT2), *J6 = p32(oJ6),
-           *J12 = p32(oJ12), *n12 = p32(oN12), *W12 = p32(oW12), *n6 = p32(oN6), *W6 = p32(oW6);
-  uint8_t* pan = iv == 0 ? ws + oPAN : nullptr;
+  uint64_t *A = keep ? reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(keep) + 256) : p64(Ly.oA),
+           *D = keep ? A + (m + 1) : p64(Ly.oD), *G = p64(Ly.oG), *GM = p64(Ly.oGM), *S = p64(Ly.oS), *dsb = p64(Ly.oSB), *db12 = p64(Ly.oB12),
+           *dnb = p64(Ly.oNB), *dbb = p64(Ly.oBB), *mx = p64(Ly.oMX), *db6 = p64(Ly.oB6);
+  uint32_t *fl = p32(Ly.oFL), *bnd = p32(Ly.oE), *J0 = p32(Ly.oJ0), *T1 = p32(Ly.oT1), *T2 = p32(Ly.oT2), *J6 = p32(Ly.oJ6),
+           *J12 = p32(Ly.oJ12), *n12 = p32(Ly.oN12), *W12 = p32(Ly.oW12), *n6 = p32(Ly.oN6), *W6 = p32(Ly.oW6);
+  uint8_t* pan = iv == 0 ? ws + Ly.oPAN : nullptr;
   int rc = MTBLX_OK;
   uint32_t flags = 0;
   uint64_t total = 0;
@@ -759,7 +786,8 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
   do {
     if (!ok(hipMemcpyAsync(dsb, sb.data(), 8ull * (nshard + 1), hipMemcpyHostToDevice, s))) break;
     if (!ok(hipMemcpyAsync(db12, base12.data(), 8ull * (nshard + 1), hipMemcpyHostToDevice, s))) break;
-    if (!ok(hipMemsetAsync(ws + oFL, 0, 4, s))) break;   // flags
+    if (!ok(hipMemcpyAsync(db6, base6.data(), 8ull * (nshard + 1), hipMemcpyHostToDevice, s))) break;
+    if (!ok(hipMemsetAsync(ws + Ly.oFL, 0, 4, s))) break;   // flags
     if (m) {
       uint32_t* SH = keep ? reinterpret_cast<uint32_t*>(D + (m + 1)) : nullptr;
       RecArgs ra{{rec->keys, rec->key_end, rec->vals, rec->val_end}, lo, m, dsb, nshard, A, D, G, GM, fl, SH};
@@ -791,17 +819,17 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
       }
       if (!ok(hipGetLastError())) break;
     }
-    WalkArgs wa{dsb, nshard, db12, n12, W12, n6, W6, J0, J6, J12, dnb, nullptr, nullptr, lo, pan, fl, slots, mid, top};
+    WalkArgs wa{dsb, nshard, db12, n12, W12, n6, db6, W6, J0, J6, J12, dnb, nullptr, nullptr, lo, pan, fl, slots, mid, top};
     MTBLX_LAUNCH((MTBLX_R(dsb, 8 * (nshard + 1)), MTBLX_R(db12, 8 * (nshard + 1)), MTBLX_R(n12, 4 * nshard),
                   MTBLX_R(W12, 4 * std::max<uint64_t>(slots, 1)), MTBLX_R(J12, 4 * m1)),
                  k_plan_top, dim3(grid_of(nshard)), dim3(kT), 0, s, wa);
     if (slots) {
       MTBLX_LAUNCH((MTBLX_R(dsb, 8 * (nshard + 1)), MTBLX_R(db12, 8 * (nshard + 1)), MTBLX_R(n12, 4 * nshard),
-                    MTBLX_R(W12, 4 * slots), MTBLX_R(n6, 4 * slots), MTBLX_R(W6, 4 * slots * mid), MTBLX_R(J6, 4 * m1)),
+                    MTBLX_R(W12, 4 * slots), MTBLX_R(n6, 4 * slots), MTBLX_R(db6, 8 * (nshard + 1)), MTBLX_R(W6, 4 * w6), MTBLX_R(J6, 4 * m1)),
                    k_plan_mid, dim3(grid_of(slots)), dim3(kT), 0, s, wa);
     }
     MTBLX_LAUNCH((MTBLX_R(dsb, 8 * (nshard + 1)), MTBLX_R(db12, 8 * (nshard + 1)), MTBLX_R(n12, 4 * nshard),
-                  MTBLX_R(n6, 4 * std::max<uint64_t>(slots, 1)), MTBLX_R(W6, 4 * std::max<uint64_t>(slots, 1) * mid),
+                  MTBLX_R(n6, 4 * std::max<uint64_t>(slots, 1)), MTBLX_R(db6, 8 * (nshard + 1)), MTBLX_R(W6, 4 * std::max<uint64_t>(w6, 1)),
                   MTBLX_R(J0, 4 * m1), MTBLX_R(dnb, 8 * nshard)),
                  k_plan_count, dim3(grid_of(nshard)), dim3(kT), 0, s, wa);
     if (!ok(hipGetLastError())) break;
@@ -818,9 +846,9 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
     wa.blk_rec = write ? blk_rec : nullptr;
     if (slots) {
       MTBLX_LAUNCH((MTBLX_R(db12, 8 * (nshard + 1)), MTBLX_R(dsb, 8 * (nshard + 1)), MTBLX_R(n12, 4 * nshard),
-                    MTBLX_R(n6, 4 * slots), MTBLX_R(W6, 4 * slots * mid), MTBLX_R(J0, 4 * m1), MTBLX_R(dbb, 8 * nshard),
+                    MTBLX_R(n6, 4 * slots), MTBLX_R(db6, 8 * (nshard + 1)), MTBLX_R(W6, 4 * w6), MTBLX_R(J0, 4 * m1), MTBLX_R(dbb, 8 * nshard),
                     MTBLX_R(blk_rec, 8 * (write ? total : 0)), pan ? MTBLX_R(pan, m1) : MTBLX_R(nullptr, 0), MTBLX_R(fl, 4)),
-                   k_plan_emit, dim3(grid_of(slots * mid)), dim3(kT), 0, s, wa);
+                   k_plan_emit, dim3(grid_of(w6)), dim3(kT), 0, s, wa);
     }
     if (!ok(hipGetLastError())) break;
     // blk_rec[total] = the end of the last shard
@@ -841,9 +869,10 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
 
 extern "C" int mtblx_encode_plan(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
                                  uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
-                                 uint64_t* nblk_out, uint32_t* flags_out, void* stream) {
+                                 uint64_t* nblk_out, uint32_t* flags_out, void* workspace, size_t ws_bytes,
+                                 void* stream) {
   return plan_impl(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out, flags_out, nullptr,
-                   0, stream);
+                   0, workspace, ws_bytes, stream);
 }
 
 extern "C" size_t mtblx_plan_keep_bytes(uint64_t nrec) { return keep_bytes(nrec); }
@@ -851,8 +880,8 @@ extern "C" size_t mtblx_plan_keep_bytes(uint64_t nrec) { return keep_bytes(nrec)
 extern "C" int mtblx_encode_plan_keep(const mtblx_records* rec, const uint64_t* shard_rec, uint32_t nshard,
                                       uint64_t block_size, uint32_t restart_interval, uint64_t* blk_rec, uint64_t blk_cap,
                                       uint64_t* nblk_out, uint32_t* flags_out, void* plan, size_t plan_bytes,
-                                      void* stream) {
+                                      void* workspace, size_t ws_bytes, void* stream) {
   if (!plan) return MTBLX_E_INVAL;
   return plan_impl(rec, shard_rec, nshard, block_size, restart_interval, blk_rec, blk_cap, nblk_out, flags_out, plan,
-                   plan_bytes, stream);
+                   plan_bytes, workspace, ws_bytes, stream);
 }

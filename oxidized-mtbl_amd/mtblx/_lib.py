@@ -36,7 +36,8 @@ EXPORTS = [
     "mtblx_snappy_compress", "mtblx_snappy_decompress_blocks", "mtblx_pipe_new", "mtblx_pipe_free",
     "mtblx_pipe_decode", "mtblx_pipe_set", "mtblx_host_alloc", "mtblx_host_free", "mtblx_host_register", "mtblx_host_unregister",
     "mtblx_encode_plan", "mtblx_encode_workspace_bytes", "mtblx_encode_blocks", "mtblx_plan_keep_bytes",
-    "mtblx_encode_plan_keep", "mtblx_encode_blocks_planned", "mtblx_plan_release",
+    "mtblx_encode_plan_keep", "mtblx_encode_blocks_planned", "mtblx_plan_release", "mtblx_plan_workspace_bytes",
+    "mtblx_plan_serial_workspace_bytes",
     "mtblx_snappy_workspace_bytes", "mtblx_snappy_dir", "mtblx_snappy_decompress_dev", "mtblx_stream_copy", "mtblx_encode_index",
     "mtblx_codec_available", "mtblx_decompress", "mtblx_compress", "mtblx_decompress_blocks", "mtblx_writer_set_level",
     "mtblx_index_seek_batch", "mtblx_block_seek_batch", "mtblx_block_seek_batch_kbuf", "mtblx_block_seek_batch_ex", "mtblx_copy_ranges", "mtblx_entry_offsets",
@@ -168,7 +169,7 @@ def lib() -> C.CDLL:
         L.mtblx_pipe_set.argtypes = [C.c_void_p, C.c_int, C.c_int64]
         L.mtblx_pipe_set.restype = C.c_int
         L.mtblx_encode_plan.argtypes = [C.POINTER(Records), C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
-                                        C.c_void_p, C.c_uint64, u64p, u32p, C.c_void_p]
+                                        C.c_void_p, C.c_uint64, u64p, u32p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.mtblx_encode_plan.restype = C.c_int
         L.mtblx_encode_workspace_bytes.argtypes = [C.c_uint32]
         L.mtblx_encode_workspace_bytes.restype = C.c_size_t
@@ -178,7 +179,12 @@ def lib() -> C.CDLL:
         L.mtblx_encode_blocks.restype = C.c_int
         L.mtblx_plan_keep_bytes.argtypes = [C.c_uint64]
         L.mtblx_plan_keep_bytes.restype = C.c_size_t
-        L.mtblx_encode_plan_keep.argtypes = L.mtblx_encode_plan.argtypes[:-1] + [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.mtblx_encode_plan_keep.argtypes = L.mtblx_encode_plan.argtypes[:-3] + [C.c_void_p, C.c_size_t, C.c_void_p,
+                                                                                 C.c_size_t, C.c_void_p]
+        L.mtblx_plan_workspace_bytes.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int]
+        L.mtblx_plan_workspace_bytes.restype = C.c_size_t
+        L.mtblx_plan_serial_workspace_bytes.argtypes = [C.c_uint32]
+        L.mtblx_plan_serial_workspace_bytes.restype = C.c_size_t
         L.mtblx_encode_plan_keep.restype = C.c_int
         L.mtblx_encode_blocks_planned.argtypes = L.mtblx_encode_blocks.argtypes[:-1] + [C.c_void_p, C.c_void_p]
         L.mtblx_encode_blocks_planned.restype = C.c_int

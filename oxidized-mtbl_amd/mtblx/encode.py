@@ -52,16 +52,45 @@ class DeviceRecords:
         return DeviceRecords(t(ks), torch.from_numpy(ke).to(device), t(vs), torch.from_numpy(ve).to(device))
 
 
+class PlanWorkspace:
+    """Caller-owned scratch of the block cut (mtblx_plan_workspace_bytes): sized for up to `nrec`
+    records in `nshard` shards, reusable across calls (one call at a time).  The library keeps no
+    scratch of its own (include/mtblx.h)."""
+
+    def __init__(self, nrec: int, nshard: int = 1, restart_interval: int = 16, keep: bool = False, device="cuda",
+                 serial: bool = False):
+        L = _lib.lib()
+        if serial:   # the serial walk's 16 B per shard (same cut, one wave per shard)
+            self.nbytes = int(L.mtblx_plan_serial_workspace_bytes(max(int(nshard), 1)))
+        else:
+            self.nbytes = int(L.mtblx_plan_workspace_bytes(max(int(nrec), 0), max(int(nshard), 1),
+                                                           int(restart_interval), 1 if keep else 0))
+        self.buf = torch.empty(self.nbytes + 256, dtype=torch.uint8, device=device)
+        self.ptr = (self.buf.data_ptr() + 255) & ~255   # 256-byte aligned
+
+
+KEEP_MAX_RECORDS = (1 << 32) - 16   # mtblx_encode_plan_keep: 32-bit next / waypoint arrays
+
+
 def plan(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16, shard_rec=None,
-         stream=None, keep: bool = False):
+         stream=None, keep: bool = False, workspace: "PlanWorkspace | None" = None):
     """-> blk_rec (device int64 [nblk + 1]): block b = records [blk_rec[b], blk_rec[b+1]).
     shard_rec: record boundaries of independent Writers (default: one Writer over all).
-    keep=True (restart_interval >= 1): -> (blk_rec, Plan), the cut's sums kept for encode_into."""
+    keep=True (restart_interval >= 1): -> (blk_rec, Plan), the cut's sums kept for encode_into.
+    workspace: a PlanWorkspace to reuse (default: one allocated for this call; without keep, a
+    workspace that does not fit falls back to the serial walk's 16 B per shard)."""
     L = codec._require_device()
     dev = recs.key_end.device
     if shard_rec is None:
         shard_rec = torch.tensor([0, recs.n], dtype=torch.int64, device=dev)
     nsh = int(shard_rec.numel()) - 1
+    if workspace is None:
+        try:
+            workspace = PlanWorkspace(recs.n, nsh, restart_interval, keep, device=dev)
+        except torch.OutOfMemoryError:
+            if keep:
+                raise
+            workspace = PlanWorkspace(recs.n, nsh, restart_interval, device=dev, serial=True)
     rc_ = recs.cstruct()
     nb = C.c_uint64(0)
     fl = C.c_uint32(0)
@@ -71,13 +100,14 @@ def plan(recs: DeviceRecords, block_size: int = 8192, restart_interval: int = 16
     blk = torch.empty(cap, dtype=torch.int64, device=dev)
     args = [C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, int(block_size), int(restart_interval),
             C.c_void_p(blk.data_ptr()), cap, C.byref(nb), C.byref(fl)]
+    ws = [C.c_void_p(workspace.ptr), workspace.nbytes]
     kept = None
     if keep:
         kb = int(L.mtblx_plan_keep_bytes(recs.n))
-        kept = Plan(torch.empty(kb, dtype=torch.uint8, device=dev), int(restart_interval))
-        rc = L.mtblx_encode_plan_keep(*args, C.c_void_p(kept.buf.data_ptr()), kb, st)
+        kept = Plan(torch.empty(kb + 256, dtype=torch.uint8, device=dev), int(restart_interval))
+        rc = L.mtblx_encode_plan_keep(*args, C.c_void_p(kept.ptr), kb, *ws, st)
     else:
-        rc = L.mtblx_encode_plan(*args, st)
+        rc = L.mtblx_encode_plan(*args, *ws, st)
     if rc == _lib.MTBLX_E_FORMAT:
         raise WriterPanic(int(fl.value))
     if rc != 0:
@@ -92,6 +122,11 @@ class Plan:
     the look-back (mtblx_encode_blocks_planned)"""
     buf: torch.Tensor
     restart_interval: int
+
+    @property
+    def ptr(self) -> int:
+        """the plan's 256-byte aligned start inside buf"""
+        return (self.buf.data_ptr() + 255) & ~255
 
 
 @dataclass
@@ -143,7 +178,7 @@ def encode_into(recs: DeviceRecords, blk_rec: torch.Tensor, bufs: EncodeBuffers,
             C.c_void_p(bufs.blk_len.data_ptr()), C.c_void_p(bufs.status.data_ptr()), C.c_void_p(bufs.totals.data_ptr()),
             C.c_void_p(bufs.ws.data_ptr()), bufs.ws_bytes]
     if plan is not None:
-        rc = L.mtblx_encode_blocks_planned(*args, C.c_void_p(plan.buf.data_ptr()), C.c_void_p(codec._stream_handle(stream)))
+        rc = L.mtblx_encode_blocks_planned(*args, C.c_void_p(plan.ptr), C.c_void_p(codec._stream_handle(stream)))
     else:
         rc = L.mtblx_encode_blocks(*args, C.c_void_p(codec._stream_handle(stream)))
     if rc != 0:
@@ -165,9 +200,12 @@ def write_file(recs: DeviceRecords, block_size: int = 8192, restart_interval: in
     L = codec._require_device()
     dev = recs.key_end.device
     kept = None
-    if restart_interval >= 1:   # the cut's sums drive the encode (no size pass, no look-back)
-        blk, kept = plan(recs, block_size, restart_interval, stream=stream, keep=True)
-    else:
+    if 1 <= restart_interval and recs.n < KEEP_MAX_RECORDS:
+        try:   # the cut's sums drive the encode (no size pass, no look-back)
+            blk, kept = plan(recs, block_size, restart_interval, stream=stream, keep=True)
+        except torch.OutOfMemoryError:   # keep mode's plan + scratch (~70 B per record) did not fit
+            kept = None
+    if kept is None:   # the cut alone (serial walk if even its scratch does not fit) + the self-contained encode
         blk = plan(recs, block_size, restart_interval, stream=stream)
     nblk = int(blk.numel()) - 1
     kbytes = int(recs.key_end[-1].item()) if recs.n else 0

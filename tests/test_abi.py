@@ -36,7 +36,7 @@ def test_library_exports_all_declared(mtblx_lib):
 
 
 def test_abi_version(mtblx_lib):
-    assert mtblx_lib.mtblx_abi_version() == 2
+    assert mtblx_lib.mtblx_abi_version() == 3
 
 
 def test_workspace_size_monotone(mtblx_lib):

@@ -133,9 +133,71 @@ def _plan_serial(recs, shard_rec, bs, iv, cap):
     blk = torch.empty(cap, dtype=torch.int64, device="cuda")
     nb, fl = C.c_uint64(0), C.c_uint32(0)
     rc_ = recs.cstruct()
-    rc = f(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), int(shard_rec.numel()) - 1, bs, iv, C.c_void_p(blk.data_ptr()),
-           cap, C.byref(nb), C.byref(fl), C.c_void_p(codec._stream_handle(None)))
+    nsh = int(shard_rec.numel()) - 1
+    ws = torch.empty(int(L.mtblx_plan_serial_workspace_bytes(nsh)), dtype=torch.uint8, device="cuda")
+    rc = f(C.byref(rc_), C.c_void_p(shard_rec.data_ptr()), nsh, bs, iv, C.c_void_p(blk.data_ptr()),
+           cap, C.byref(nb), C.byref(fl), C.c_void_p(ws.data_ptr()), ws.numel(), C.c_void_p(codec._stream_handle(None)))
     return rc, int(fl.value), blk[: int(nb.value) + 1].cpu().numpy()
+
+
+def test_plan_caller_workspace_and_concurrent_cuts():
+    """The block cut keeps no state of its own (include/mtblx.h: re-entrant, caller-owned
+    workspace): two host threads on two streams cut two different cfg3 record
+    sets at once, each with its own PlanWorkspace, and both equal the serial walk; a workspace too
+    small for the parallel cut takes the serial walk (same cut); NULL, misaligned or (keep mode)
+    too small are MTBLX_E_INVAL."""
+    enc = _enc()
+    import ctypes as C
+    import threading
+    import torch
+    from mtblx import _lib, codec, synth
+    L = _lib.lib()
+    sets = [synth.cfg3_records_device(300_000, seed=41 + i)[0] for i in range(2)]
+    cuts = [torch.tensor(c, dtype=torch.int64, device="cuda") for c in ([0, 100_000, 300_000], [0, 300_000])]
+    exp = [_plan_serial(r, c, 65536, 16, 300_002) for r, c in zip(sets, cuts)]
+    assert all(e[0] == 0 for e in exp)
+    streams = [torch.cuda.Stream() for _ in sets]
+    wss = [enc.PlanWorkspace(r.n, int(c.numel()) - 1, 16, keep) for r, c, keep in zip(sets, cuts, (True, False))]
+    got, errs = [None, None], []
+    torch.cuda.synchronize()
+
+    def run(i):
+        try:
+            for _ in range(4):
+                with torch.cuda.stream(streams[i]):
+                    r = enc.plan(sets[i], 65536, 16, shard_rec=cuts[i], stream=streams[i], keep=(i == 0),
+                                 workspace=wss[i])
+                b = r[0] if i == 0 else r
+                streams[i].synchronize()
+                got[i] = b.cpu().numpy()
+                assert np.array_equal(got[i], exp[i][2]), i
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    # a workspace too small for the parallel cut: the serial walk, same cut
+    small = enc.PlanWorkspace(sets[1].n, 1, 16, serial=True)
+    assert np.array_equal(enc.plan(sets[1], 65536, 16, shard_rec=cuts[1], workspace=small).cpu().numpy(), exp[1][2])
+    # keep mode has no serial fallback: a small workspace is MTBLX_E_INVAL
+    with pytest.raises(RuntimeError, match="-1"):
+        enc.plan(sets[1], 65536, 16, shard_rec=cuts[1], keep=True, workspace=small)
+    # NULL and misaligned workspaces
+    rc_ = sets[1].cstruct()
+    blk = torch.empty(300_002, dtype=torch.int64, device="cuda")
+    nb, fl = C.c_uint64(0), C.c_uint32(0)
+    for ptr in (0, wss[1].ptr + 8):
+        assert L.mtblx_encode_plan(C.byref(rc_), C.c_void_p(cuts[1].data_ptr()), 1, 65536, 16, C.c_void_p(blk.data_ptr()),
+                                   300_002, C.byref(nb), C.byref(fl), C.c_void_p(ptr), wss[1].nbytes,
+                                   C.c_void_p(codec._stream_handle(None))) == _lib.MTBLX_E_INVAL
+    # the bound does not depend on the records: many tiny shards and one large one stay small
+    b1 = int(L.mtblx_plan_workspace_bytes(1_000_000, 1, 16, 0))
+    b2 = int(L.mtblx_plan_workspace_bytes(1_000_000, 50_000, 16, 0))
+    assert b2 - b1 < 50_000 * 64
 
 
 def test_parallel_plan_equals_writer_chain():
@@ -208,6 +270,14 @@ def test_planned_encode_equals_encode():
     sr = torch.tensor([0, 70_000, 200_000], dtype=torch.int64, device="cuda")
     blk, kept = enc.plan(recs, 65536, 16, shard_rec=sr, keep=True)
     same(enc.encode_blocks(recs, blk, 16), enc.encode_blocks(recs, blk, 16, plan=kept), blk.numel() - 1)
+    # blocks of another cut that span the plan's shard start (record 70 000) share a
+    # prefix there like mtblx_encode_blocks does (interval 16 and 7: the shard start in and out of
+    # a restart phase)
+    for iv in (16, 7):
+        blk, kept = enc.plan(recs, 65536, iv, shard_rec=sr, keep=True)
+        span = torch.tensor([0, 69_990, 70_013, 70_500, 200_000], dtype=torch.int64, device="cuda")
+        same(enc.encode_blocks(recs, span, iv), enc.encode_blocks(recs, span, iv, plan=kept), span.numel() - 1)
+    blk, kept = enc.plan(recs, 65536, 16, shard_rec=sr, keep=True)
     # a plan over the second shard only: blocks outside it are refused (UNSUPPORTED), the rest exact
     sr2 = torch.tensor([70_000, 200_000], dtype=torch.int64, device="cuda")
     blk2, kept2 = enc.plan(recs, 65536, 16, shard_rec=sr2, keep=True)
@@ -215,6 +285,13 @@ def test_planned_encode_equals_encode():
     e = enc.encode_blocks(recs, mix, 16, plan=kept2)
     st = e.status.cpu().numpy()
     assert (st[:3] == 4).all() and (st[3:] == 0).all()
+    # a LAST block outside the plan adds no bytes: totals[0] == the in-plan blocks' total
+    sr3 = torch.tensor([0, 70_000], dtype=torch.int64, device="cuda")
+    blk3, kept3 = enc.plan(recs, 65536, 16, shard_rec=sr3, keep=True)
+    tail = torch.cat([blk3, torch.tensor([70_010], dtype=torch.int64, device="cuda")])
+    e3 = enc.encode_blocks(recs, tail, 16, plan=kept3)
+    ref = enc.encode_blocks(recs, blk3, 16, plan=kept3)
+    assert int(e3.status[-1].item()) == 4 and int(e3.totals[0].item()) == int(ref.totals[0].item())
 
 def test_cfg3_roundtrip_sample(oracle):
     """cfg3 scheme on the device: plan -> encode -> decode == the generated records; a sample of

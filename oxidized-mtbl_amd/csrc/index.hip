@@ -17,6 +17,7 @@
 // placed right after the data blocks, and the footer follows.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mtblx.h"
@@ -159,7 +160,9 @@ namespace {
 struct DevMem {   // temporaries of this (synchronous, once-per-file) call
   void* p = nullptr;
   ~DevMem() { if (p) (void)hipFree(p); }
-  bool alloc(size_t n) { return hipMalloc(&p, n ? n : 1) == hipSuccess; }
+  bool alloc(size_t n) {   // MTBLX_DEBUG_POISON (test knob): fresh memory filled with 0xFF
+    return hipMalloc(&p, n ? n : 1) == hipSuccess && (!getenv("MTBLX_DEBUG_POISON") || hipMemset(p, 0xFF, n ? n : 1) == hipSuccess);
+  }
   template <class T> T* as(size_t byte_off = 0) const { return reinterpret_cast<T*>(static_cast<uint8_t*>(p) + byte_off); }
 };
 }  // namespace

@@ -1185,6 +1185,12 @@ extern "C" int mtblx_entry_offsets(const uint8_t* block, uint64_t len, uint64_t*
   // Reader; r05: no stream-ordered pool allocations next to the caller's caching allocator)
   uint64_t* scratch = nullptr;
   if (hipMalloc(reinterpret_cast<void**>(&scratch), nr * sizeof(uint64_t)) != hipSuccess) return MTBLX_E_HIP;
+  // test knob (MTBLX_DEBUG_POISON, tests/conftest.py): fresh scratch filled with 0xFF, so a read
+  // before a write is deterministic and far out of range
+  if (getenv("MTBLX_DEBUG_POISON") && hipMemsetAsync(scratch, 0xFF, nr * sizeof(uint64_t), s) != hipSuccess) {
+    (void)hipFree(scratch);
+    return MTBLX_E_HIP;
+  }
   MTBLX_LAUNCH((MTBLX_R(block, len), MTBLX_R(offs, 8 * cap), MTBLX_R(count, 8), MTBLX_R(scratch, 8 * nr),
                 MTBLX_R(regular, 4)), mtblx_rd::k_entry_offsets, dim3(1), dim3(1024), 0, s, block, len, offs, cap, count, scratch,
                      regular);

@@ -152,12 +152,37 @@ class HostDecoded:
         return out
 
 
+class WorkspaceBusy(RuntimeError):
+    """A decode workspace was handed to a launch on one stream while a launch on another stream
+    still used it (include/mtblx.h: one workspace serves one call at a time).  Its launch-parity
+    protocol (decode.hip ws_begin: the parity comes from the epoch the previous launch left, and
+    the other parity's slots are cleared for the next launch) holds only in stream order, which
+    the kernels cannot check; two launches in flight on one workspace would read each other's
+    look-back words.  Nothing was launched (the C ABI's MTBLX_E_INVAL class of error)."""
+
+
 class Workspace:
     def __init__(self, nblk: int, device="cuda"):
         L = _lib.lib()
         self.nbytes = int(L.mtblx_decode_workspace_bytes(nblk))
         # zero-filled once: the kernels keep it consistent from call to call (include/mtblx.h)
         self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self._last = None   # (stream handle, event recorded after the last launch on this workspace)
+
+    def _claim(self, stream) -> int:
+        """-> the stream handle for a launch on this workspace; raises WorkspaceBusy if the last
+        launch ran on another stream and has not completed (on the same stream, stream order
+        already serialises them)"""
+        h = _stream_handle(stream)
+        if self._last is not None and self._last[0] != h and not self._last[1].query():
+            raise WorkspaceBusy(f"decode workspace in use by a launch on stream 0x{self._last[0]:x} (not complete); "
+                                f"one workspace serves one call at a time -- synchronise, or give each stream its own")
+        return h
+
+    def _launched(self, stream, h: int) -> None:
+        ev = self._last[1] if self._last is not None else torch.cuda.Event()
+        ev.record(stream if stream is not None else torch.cuda.current_stream())
+        self._last = (h, ev)
 
 
 def _stream_handle(stream) -> int:
@@ -168,8 +193,10 @@ def _stream_handle(stream) -> int:
 def count_blocks(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=None) -> None:
     L = _require_device()
     b, o = batch.cstruct(), out.cstruct()
+    h = ws._claim(stream)
     rc = L.mtblx_count_blocks(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
-                              C.c_void_p(_stream_handle(stream)))
+                              C.c_void_p(h))
+    ws._launched(stream, h)
     if rc != 0:
         raise RuntimeError(f"mtblx_count_blocks failed: {rc}")
 
@@ -180,8 +207,10 @@ def decode_into(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream=No
     synchronize first): the library orders nothing across streams."""
     L = _require_device()
     b, o = batch.cstruct(), out.cstruct()
+    h = ws._claim(stream)
     rc = L.mtblx_decode_blocks(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
-                               C.c_void_p(_stream_handle(stream)))
+                               C.c_void_p(h))
+    ws._launched(stream, h)
     if rc != 0:
         raise RuntimeError(f"mtblx_decode_blocks failed: {rc}")
 
@@ -197,9 +226,11 @@ def decode_verify_into(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, cr
     L = _require_device()
     b, o = batch.cstruct(), out.cstruct()
     flags = (1 if framed else 0) | (VERIFY_FUSED if fused else 0)
+    h = ws._claim(stream)
     rc = L.mtblx_decode_blocks_verify(C.byref(b), C.byref(o), C.c_void_p(_u(crc)), C.c_void_p(_u(bad)),
                                       flags, C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
-                                      C.c_void_p(_stream_handle(stream)))
+                                      C.c_void_p(h))
+    ws._launched(stream, h)
     if rc != 0:
         raise RuntimeError(f"mtblx_decode_blocks_verify failed: {rc}")
 
@@ -224,8 +255,10 @@ def decode_counted(batch: DeviceBatch, out: DecodedBlocks, ws: Workspace, stream
     """Decode using the counts a previous count_blocks(batch, out, ws) left behind."""
     L = _require_device()
     b, o = batch.cstruct(), out.cstruct()
+    h = ws._claim(stream)
     rc = L.mtblx_decode_counted(C.byref(b), C.byref(o), C.c_void_p(ws.buf.data_ptr()), ws.nbytes,
-                                C.c_void_p(_stream_handle(stream)))
+                                C.c_void_p(h))
+    ws._launched(stream, h)
     if rc != 0:
         raise RuntimeError(f"mtblx_decode_counted failed: {rc}")
 

@@ -11,6 +11,16 @@ for p in (os.path.join(ROOT, "oxidized-mtbl_amd"), os.path.join(ROOT, "oracle"),
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (runs on the MI355X box)")
+    if os.environ.get("MTBLX_POISON"):
+        # every uninitialised allocation -- torch.empty here, the library's own
+        # scratch through MTBLX_DEBUG_POISON -- is filled with all-ones (0xFF bytes, INT_MAX words)
+        # instead of whatever a previous test left, so a kernel whose addressing depends on memory
+        # it reads before writing faults or differs deterministically rather than now and then
+        os.environ["MTBLX_DEBUG_POISON"] = "1"
+        import torch
+        import torch.utils.deterministic
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.utils.deterministic.fill_uninitialized_memory = True
 
 
 @pytest.fixture(scope="session")

@@ -212,3 +212,39 @@ def test_timeout_before_tile0_survives(oracle, monkeypatch):
     assert out.totals_host() == tot
     h, r = out.to_host(), ref.to_host()
     assert np.array_equal(h.keys, r.keys) and np.array_equal(h.key_end, r.key_end)
+
+
+@pytest.mark.gpu
+def test_workspace_one_launch_at_a_time(monkeypatch):
+    """the workspace's launch-parity protocol (decode.hip ws_begin: parity from
+    the epoch the previous launch left; the other parity's slots cleared for the next launch) holds
+    only in stream order.  The surface enforces it: a launch on stream B while stream A's launch on
+    the same workspace is still running is refused (WorkspaceBusy, nothing launched), not run into
+    the other launch's look-back words.  Stream A's launch is held ~300 ms by the debug knob that
+    starts workgroup 0 late (the look-back waits on it; no timeout at the default bound)."""
+    codec = _codec()
+    import torch
+    from mtblx import synth
+    data, off, ln = synth.cfg2_file(600)
+    batch = codec.DeviceBatch.from_host(data, off, ln)
+    ref = codec.decode_blocks(batch)
+    torch.cuda.synchronize()
+    ws = codec.Workspace(batch.nblk)
+    out_a, out_b = codec.decode_blocks(batch), codec.decode_blocks(batch)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    monkeypatch.setenv("MTBLX_DEBUG_DELAY0_MS", "300")
+    codec.decode_into(batch, out_a, ws, sa)
+    monkeypatch.delenv("MTBLX_DEBUG_DELAY0_MS")
+    with pytest.raises(codec.WorkspaceBusy):
+        codec.decode_into(batch, out_b, ws, sb)
+    with pytest.raises(codec.WorkspaceBusy):
+        codec.count_blocks(batch, out_b, ws, sb)
+    codec.decode_into(batch, out_a, ws, sa)       # the same stream: ordered after it, allowed
+    sa.synchronize()
+    codec.decode_into(batch, out_b, ws, sb)       # A is done: B may take the workspace
+    torch.cuda.synchronize()
+    for o in (out_a, out_b):
+        assert o.totals_host() == ref.totals_host()
+        h, r = o.to_host(), ref.to_host()
+        assert np.array_equal(h.keys, r.keys) and np.array_equal(h.vals, r.vals) and np.array_equal(h.key_end, r.key_end)

@@ -29,6 +29,7 @@ cfg3oracle)   # every cfg3 block against the oracle, full size (1 M blocks, 10 c
   rm -f $O/cfg3_oracle.txt
   step gpu_cfg3_oracle 1100 env MTBLX_CFG3_BLOCKS=${CFG3_BLOCKS:-1000000} MTBLX_CFG3_LOG=$O/cfg3_oracle.txt \
     python -u -m pytest -v -s --timeout 1050 --timeout-method thread -p no:cacheprovider tests/test_cfg3_oracle_gpu.py ;;
+poison) step gpu_poison 1100 env MTBLX_POISON=1 $PT tests -m gpu --deselect tests/test_spill_gpu.py::test_spilling_build_is_exact ${PYTEST_ARGS:-} ;;
 bounds) step gpu_bounds 1150 env MTBLX_LIB=oxidized-mtbl_amd/build/libmtblx_bounds.so MTBLX_BOUNDS_CHECK=1 $PT tests -m gpu --deselect tests/test_spill_gpu.py::test_spilling_build_is_exact ${PYTEST_ARGS:-} ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac

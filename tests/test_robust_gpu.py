@@ -248,3 +248,15 @@ def test_workspace_one_launch_at_a_time(monkeypatch):
         assert o.totals_host() == ref.totals_host()
         h, r = o.to_host(), ref.to_host()
         assert np.array_equal(h.keys, r.keys) and np.array_equal(h.vals, r.vals) and np.array_equal(h.key_end, r.key_end)
+
+
+@pytest.mark.gpu
+def test_poison_fill_is_active():
+    """MTBLX_POISON=1 runs (tests/conftest.py): fresh device allocations really are all-ones"""
+    if not os.environ.get("MTBLX_POISON"):
+        pytest.skip("poison mode off")
+    _codec()
+    import torch
+    assert bool((torch.empty(4096, dtype=torch.uint8, device="cuda") == 255).all().item())
+    assert bool((torch.empty(64, dtype=torch.int64, device="cuda") == (1 << 63) - 1).all().item())
+    assert os.environ.get("MTBLX_DEBUG_POISON") == "1"

@@ -232,6 +232,9 @@ static __constant__ X8Tab kX8 = X8Tab();
 #ifndef MTBLX_ENC_LAZY_T   // slicing-by-4 tables built only by blocks that use them
 #define MTBLX_ENC_LAZY_T 1
 #endif
+#ifndef MTBLX_ENC_TW   // planned mode: stores before the block CRC, stage-2 operand per wave (see k_encode)
+#define MTBLX_ENC_TW 1
+#endif
 #ifndef MTBLX_ENC_CRC_UNROLL
 #define MTBLX_ENC_CRC_UNROLL 4
 #endif
@@ -464,8 +467,12 @@ __device__ __forceinline__ void crc_mfma_part(EncLds& S, uint32_t L) {
           v4a x = {0u, 0u, 0u, 0u};
           if (pos >= 0) x = *reinterpret_cast<const v4a*>(S.ob + pos);
           if (pos == 0) x.x ^= 0xFFFFFFFFu;   // the init, folded into bytes 0..3
+#if defined(MTBLX_ENC_ABL) && MTBLX_ENC_ABL == 4   // timing ablation only: no stage-2 operand loads
+          const v4i a2lo = A[tt & 3][0], a2hi = A[tt & 3][1];
+#else
           const v4i a2lo = reinterpret_cast<const v4i*>(&kEncMfma.a2[tt][0][0][0])[lane];
           const v4i a2hi = reinterpret_cast<const v4i*>(&kEncMfma.a2[tt][1][0][0])[lane];
+#endif
           mfma_step(A, v4u{x.x, x.y, x.z, x.w}, a2lo, a2hi, c2a, c2b);
         }
       }
@@ -655,6 +662,19 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     b = S.sh_u32[0];
   }
   if (b >= a.nblk) return;
+#if MTBLX_ENC_TW
+  // planned mode: the file offset and the Horner table of the block CRC (below) loaded now, so
+  // their latency overlaps the assembly
+  uint64_t tw_fin = 0;
+  uint32_t tw_swk = 0;
+  if constexpr (PL) {
+    if (tid == 0) {
+      MTBLX_CHK(a.fincl + b, 8);
+      tw_fin = a.fincl[b];
+    }
+    if (tid < 128) tw_swk = (&kEncMfma.swk[0][0])[tid];
+  }
+#endif
   const uint64_t r0 = a.blk_rec[b], n = a.blk_rec[b + 1] - r0;
   const uint32_t iv = a.interval;
   ESTAMP(2);   // tables + ticket
@@ -792,9 +812,122 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   if (in_lds) assemble(S.ob, std::true_type{});
   ESTAMP(4);   // assembly in LDS
 
+#if MTBLX_ENC_TW && !defined(MTBLX_ENC_ABL)
+  // Planned mode with the block CRC on the matrix cores (cfg3's path).  The file offset is known
+  // (the scan of the framed sizes), so the block streams out right after the assembly and the
+  // CRC runs beside its stores; only the 4-byte checksum of the frame waits for it.  The CRC's
+  // operands are loaded -- and waited for -- BEFORE the stores: a vector-memory wait counts loads
+  // and stores in issue order (round 5 issued the stores first and lost 5 % to exactly that).
+  // Wave w takes step position t = w of every super-window (steps s = 8 S + w counted from the
+  // padded end), so it needs one stage-2 operand (a2[w]) instead of one per step; the integer
+  // parity is linear, so each step's stage-2 parities are Horner-combined over S with
+  // x^(8·8192) (a 512-byte nibble table in LDS) and the waves' partial column words XOR-combined.
+  if constexpr (PL) {
+    static_assert(kWaves == mtblx_crc::kMSup, "one wave per step position of a super-window");
+    if (MTBLX_ENC_CRC_MFMA && a.framed && in_lds && L >= 256 && st == MTBLX_ST_OK) {   // uniform
+      using namespace mtblx_crc;
+      const int g = lane >> 4, nn = lane & 15;
+      v4i A[kMKs][2];
+#pragma unroll
+      for (int k = 0; k < kMKs; ++k) {
+        A[k][0] = reinterpret_cast<const v4i*>(&kEncMfma.a[k][0][0][0])[lane];
+        A[k][1] = reinterpret_cast<const v4i*>(&kEncMfma.a[k][1][0][0])[lane];
+      }
+      const v4i a2lo = reinterpret_cast<const v4i*>(&kEncMfma.a2[w][0][0][0])[lane];
+      const v4i a2hi = reinterpret_cast<const v4i*>(&kEncMfma.a2[w][1][0][0])[lane];
+      uint32_t(*hk)[16] = reinterpret_cast<uint32_t(*)[16]>(&S.T[0][0]);   // x^(8·8192): swk
+      if (tid < 128) (&hk[0][0])[tid] = tw_swk;
+      if (tid == 0) S.sh_u64[0] = tw_fin - F;
+      __syncthreads();   // the block (and its zero pad), the table, the offset
+#pragma unroll
+      for (int k = 0; k < kMKs; ++k) asm volatile("" ::"v"(A[k][0]), "v"(A[k][1]));
+      asm volatile("" ::"v"(a2lo), "v"(a2hi));   // the operands' wait is here, before the stores
+      const uint64_t pre = S.sh_u64[0];
+      const uint64_t coff = pre + vlen64(L) + 4;
+      const bool fits = pre + F <= a.out_cap;
+      if (fits) {   // stream the block out: aligned 16 B LDS reads, unaligned 16 B stores
+        uint8_t* dst = a.out + coff;
+        const uint64_t nch = L / 16;
+        for (uint64_t c = tid; c < nch; c += kThreads) {
+          const v4a x = *reinterpret_cast<const v4a*>(S.ob + 16 * c);
+#if MTBLX_ENC_NT_STORES
+          __builtin_nontemporal_store(v4u{x.x, x.y, x.z, x.w}, reinterpret_cast<v4u*>(dst + 16 * c));
+#else
+          *reinterpret_cast<v4u*>(dst + 16 * c) = v4u{x.x, x.y, x.z, x.w};
+#endif
+        }
+        for (uint64_t o = 16 * nch + tid; o < L; o += kThreads) dst[o] = S.ob[o];
+      }
+      // this wave's steps, from the block start (Horner over the super-windows)
+      uint32_t acc = 0;
+      const uint32_t t = (16u - (uint32_t)(L & 15u)) & 15u, Lp = (uint32_t)L + t;
+      const uint32_t steps = (Lp + kMStep - 1) / kMStep, nsup = (steps + kMSup - 1) / kMSup;
+      const int32_t kx16 = 16 * (60 - 4 * nn + g);   // the lane's chunk of a step
+      if (fits) {
+        for (int sw = (int)nsup - 1; sw >= 0; --sw) {
+          const uint32_t sp = (uint32_t)sw * kMSup + (uint32_t)w;
+          uint32_t dv = 0;
+          if (sp < steps) {   // wave-uniform
+            const int32_t pos = (int32_t)Lp - (int32_t)(kMStep * (sp + 1)) + kx16;   // a multiple of 16
+            v4a x = {0u, 0u, 0u, 0u};
+            if (pos >= 0) x = *reinterpret_cast<const v4a*>(S.ob + pos);
+            if (pos == 0) x.x ^= 0xFFFFFFFFu;   // the init, folded into bytes 0..3
+            v4f c2a = {0.f, 0.f, 0.f, 0.f}, c2b = c2a;
+            mfma_step(A, v4u{x.x, x.y, x.z, x.w}, a2lo, a2hi, c2a, c2b);
+            dv = (par_nib(c2a) << (4 * g)) | (par_nib(c2b) << (16 + 4 * g));
+          }
+          acc = mul_nib(acc, hk) ^ dv;
+        }
+      }
+      uint32_t* part = reinterpret_cast<uint32_t*>(S.shc);   // planned mode never reads shc
+      part[w * kWave + lane] = acc;
+      __syncthreads();
+      ESTAMP(6);   // stores issued + CRC
+      if (w == 0 && fits) {   // column shift x^(8·64·n), XOR over the columns, pad removal x^(-8t)
+        uint32_t pw = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) pw ^= part[k * kWave + lane];
+        uint32_t c = row_xor(mul_nib(pw, kEncMfma.col[nn]));
+        uint32_t C = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 16) ^
+                     (uint32_t)__builtin_amdgcn_readlane((int)c, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
+        if (t) {
+          const uint32_t j = (uint32_t)lane & 15u;
+          const uint32_t v = j < 8u ? kEncMfma.inv[t][j][(C >> (4 * j)) & 15u] : 0u;
+          C = (uint32_t)__builtin_amdgcn_readlane((int)row_xor(v), 0);
+        }
+        if (tid == 0) {   // varint64(L) | crc32c (write_block, src/writer.rs:203-237)
+          uint32_t hl;
+          const uint64_t hw = vpack(L, hl);
+#pragma unroll
+          for (uint32_t k = 0; k < 5; ++k)
+            if (k < hl) a.out[pre + k] = (uint8_t)(hw >> (8 * k));
+          put32(a.out + pre + hl, C ^ 0xFFFFFFFFu);
+        }
+      }
+      ESTAMP(7);
+#ifdef MTBLX_ENC_STAMPS
+      if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket) + 15, 1ull);
+#endif
+      if (tid == 0) {
+        const int32_t st2 = fits ? MTBLX_ST_OK : MTBLX_ST_OVERFLOW;
+        a.blk_off[b] = fits ? coff : 0;
+        a.blk_len[b] = fits ? (uint32_t)L : 0u;
+        a.status[b] = st2;
+        if (!fits) atomicOr(reinterpret_cast<unsigned long long*>(a.totals + 1), 1ull);
+        if (b == a.nblk - 1) a.totals[0] = pre + F;
+      }
+      return;
+    }
+  }
+#endif
+
   // ---- look-back: this block's offset in the output (wave 0), beside the block CRC (all waves,
   // wave 0 after its look-back) ----
+#if defined(MTBLX_ENC_ABL) && MTBLX_ENC_ABL == 3   // timing ablation only (wrong checksums): no block CRC
+  const bool crc_mfma = false;
+#else
   const bool crc_mfma = MTBLX_ENC_CRC_MFMA && a.framed && in_lds && L >= 4;
+#endif
   if (crc_mfma) {
     __syncthreads();   // the assembled block (entries, restarts, count, pad) before its CRC
     if (w != 0 || PL) crc_mfma_part(S, (uint32_t)L);
@@ -826,13 +959,18 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       src = dst;
     }
     if (a.framed) {
-#if MTBLX_ENC_LAZY_T
+#if MTBLX_ENC_LAZY_T && !(defined(MTBLX_ENC_ABL) && MTBLX_ENC_ABL == 3)
       if (!crc_mfma) {   // uniform over the workgroup
         build_tables();
         __syncthreads();
       }
 #endif
+#if defined(MTBLX_ENC_ABL) && MTBLX_ENC_ABL == 3
+      const uint32_t crc = 0u;
+      (void)src;
+#else
       const uint32_t crc = crc_mfma ? crc_mfma_final(S, (uint32_t)L) : wg_crc32c(S, src, L);
+#endif
       ESTAMP(6);   // CRC-32C
       if (tid == 0) {
         uint32_t hl;   // varint64(L) | crc32c (write_block, src/writer.rs:203-237)

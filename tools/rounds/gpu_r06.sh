@@ -31,6 +31,13 @@ cfg3oracle)   # every cfg3 block against the oracle, full size (1 M blocks, 10 c
     python -u -m pytest -v -s --timeout 1050 --timeout-method thread -p no:cacheprovider tests/test_cfg3_oracle_gpu.py ;;
 poison) step gpu_poison 1100 env MTBLX_POISON=1 $PT tests -m gpu --deselect tests/test_spill_gpu.py::test_spilling_build_is_exact ${PYTEST_ARGS:-} ;;
 bounds) step gpu_bounds 1150 env MTBLX_LIB=oxidized-mtbl_amd/build/libmtblx_bounds.so MTBLX_BOUNDS_CHECK=1 $PT tests -m gpu --deselect tests/test_spill_gpu.py::test_spilling_build_is_exact ${PYTEST_ARGS:-} ;;
+encab)   # k_encode A/B on one cfg3 chunk: product vs build/libmtblx_<v>.so for v in $ENCV, twice
+  B="python bench.py --config cfg3 --cfg3-blocks 100000 --steps 1 --warmup 0 --no-cpu-baseline"
+  for r in 1 2; do
+    step encab_prod$r 300 $B
+    for v in ${ENCV:-}; do step encab_${v}_$r 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
+  done
+  grep -H -o '"encode_GiB_per_s": [0-9.]*' $O/encab_*.log || true ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

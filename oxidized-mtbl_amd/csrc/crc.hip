@@ -197,6 +197,9 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in
 #ifndef MTBLX_CRC_RING
 #define MTBLX_CRC_RING 8
 #endif
+#ifndef MTBLX_CRC_PAIR   // two steps per loop iteration (in-wave ILP, A/B: measured slower); 0 = one
+#define MTBLX_CRC_PAIR 0
+#endif
 #ifndef MTBLX_CRC_DMA_AUX
 #define MTBLX_CRC_DMA_AUX 2   // non-temporal: the block bytes are read once
 #endif
@@ -228,6 +231,18 @@ __device__ __forceinline__ void wait_ring(uint32_t k) {
     default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
   }
 }
+__device__ __forceinline__ void wait_vm(uint32_t k) {   // vmcnt(k), k <= 7
+  switch (k) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+  }
+}
 __device__ __forceinline__ void wait_steady() {
   static_assert(kRing >= 2 && kRing <= 8, "wait_ring covers up to 7 steps ahead");
   switch (kRing - 1) {
@@ -256,6 +271,22 @@ __device__ __forceinline__ v4u ring_read(uint32_t ax, uint32_t aa, v4i& lo, v4i&
       : "v"(ax), "v"(aa)
       : "memory");
   return x;
+}
+
+// two landed slots (steps s and s - 1 of one super-window) and their stage-2 operands, one wait
+__device__ __forceinline__ void ring_read2(uint32_t ax, uint32_t ay, uint32_t aa, uint32_t ab, v4u& x, v4u& y,
+                                           v4i& lo, v4i& hi, v4i& lo2, v4i& hi2) {
+  asm volatile(
+      "ds_read_b128 %2, %8\n\t"
+      "ds_read_b128 %3, %8 offset:1024\n\t"
+      "ds_read_b128 %4, %9\n\t"
+      "ds_read_b128 %5, %9 offset:1024\n\t"
+      "ds_read_b128 %0, %6\n\t"
+      "ds_read_b128 %1, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(x), "=&v"(y), "=&v"(lo), "=&v"(hi), "=&v"(lo2), "=&v"(hi2)
+      : "v"(ax), "v"(ay), "v"(aa), "v"(ab)
+      : "memory");
 }
 
 // serial CRC-32C of a short block (< 4 bytes), one lane
@@ -424,33 +455,58 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
       uint32_t acc = 0, lo = 0, hi = 0;
       bool first_sw = true;
       for (;;) {
+        // two steps of one super-window per iteration when the block has them (MTBLX_CRC_PAIR):
+        // their stage-1 chains are independent, so the wave keeps two in flight -- the per-wave
+        // step is latency-bound (LDS read -> bit planes -> 8 dependent-pair MFMAs -> f16 stage 2)
+        const bool pair = MTBLX_CRC_PAIR && s >= 1u && (s & (uint32_t)(kMSup - 1)) != 0u;
         if (ilive) {   // steady state: kRing - 1 steps stay in flight behind this one
           issue();
-          wait_steady();
-        } else {
-          wait_ring(pend - 1);
-          --pend;
+          ++pend;
         }
+        wait_vm(pend - (pair ? 2u : 1u));
         const uint32_t t = s & (uint32_t)(kMSup - 1);
-        v4i a2lo, a2hi;
-        v4u x = ring_read(ring_lane + coff, a2_lane + t * 2048u, a2lo, a2hi);
-        coff = (coff + (uint32_t)kMStep) & kRingMask;
+        v4i a2lo, a2hi, b2lo, b2hi;
+        v4u x, y;
+        if (pair) {
+          ring_read2(ring_lane + coff, ring_lane + ((coff + (uint32_t)kMStep) & kRingMask), a2_lane + t * 2048u,
+                     a2_lane + (t - 1u) * 2048u, x, y, a2lo, a2hi, b2lo, b2hi);
+          coff = (coff + 2u * (uint32_t)kMStep) & kRingMask;
+          pend -= 2;
+          if (ilive) {   // into the slot just read
+            issue();
+            ++pend;
+          }
+        } else {
+          x = ring_read(ring_lane + coff, a2_lane + t * 2048u, a2lo, a2hi);
+          coff = (coff + (uint32_t)kMStep) & kRingMask;
+          pend -= 1;
+        }
         if (sbc < 4) {   // the block's first bytes (sbc > -1024)
           x = head_chunk(x, sbc + 16 * (int)kx);
           sbc += kMStep;
         }
-        if (s == 0) {   // the pad after the block's end: lane (g 3, n 0) holds chunk 63
+        if (pair && sbc < 4) {
+          y = head_chunk(y, sbc + 16 * (int)kx);
+          sbc += kMStep;
+        }
+        const uint32_t sl = pair ? s - 1u : s;   // the iteration's last step
+        if (sl == 0) {   // the pad after the block's end: lane (g 3, n 0) holds chunk 63
           asm volatile("");   // a branch, not a select in every step
-          if (Cb.t != 0 && lane == 48) x = tail_chunk(x, Cb.t);
+          if (Cb.t != 0 && lane == 48) {
+            if (pair) y = tail_chunk(y, Cb.t);
+            else x = tail_chunk(x, Cb.t);
+          }
         }
 #if MTBLX_CRC_ABL == 1
         acc ^= x.x ^ x.y ^ x.z ^ x.w;
         lo = acc & 15u;
         (void)a2lo;
         (void)a2hi;
+        (void)y;
 #else
         mfma_step(A, x, a2lo, a2hi, c2a, c2b);
-        if (t == 0) {
+        if (pair) mfma_step(A, y, b2lo, b2hi, c2a, c2b);
+        if ((sl & (uint32_t)(kMSup - 1)) == 0u) {
           // super-window done: the parities of the column's raw CRC bits 4g + i (lo) and
           // 16 + 4g + i (hi); with more than one super-window, Horner-combined as a full word with
           // the super-windows before it (nearer the block start)
@@ -466,8 +522,8 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
           }
         }
 #endif
-        if (s == 0) break;
-        --s;
+        if (sl == 0) break;
+        s = sl - 1u;
       }
       // block done: column shift, XOR over all 64 lanes, pad removal.  With one super-window the
       // lane holds only its own 8 bits of the column -- nibbles g and 4 + g -- so the column

@@ -435,6 +435,11 @@ __device__ __forceinline__ uint64_t* lb_slot(const TileArgs& a, uint64_t t) { re
 __device__ __forceinline__ uint64_t* lbx_slot(const TileArgs& a, uint64_t t) { return a.lbw + kTileWords * t + 2; }
 __device__ __forceinline__ uint64_t* lbx2_slot(const TileArgs& a, uint64_t t) { return a.lbw + kTileWords * t + 3; }
 
+// n records / bytes at `base` fit a buffer of `cap`, without wrap-around: a prefix built from a
+// stale or corrupt look-back word (a side word is a full u64) must not pass by overflowing the
+// sum and then address below the buffer (base + n wrapping to a small number)
+__device__ __forceinline__ bool fits_at(uint64_t base, uint64_t n, uint64_t cap) { return base <= cap && n <= cap - base; }
+
 // kernel prologue: pick the parity, clear the other parity's slots of every tile a previous
 // launch of that parity used (the next launch uses them)
 __device__ __forceinline__ void ws_begin(TileArgs& a) {
@@ -1065,7 +1070,8 @@ __global__ void __launch_bounds__(kThreads, C::MINW) k_decode_tiles(TileArgs a) 
       a.key_base[b] = kb;
       a.val_base[b] = vb;
       int32_t st = S.bst[j];
-      if (a.write && (rb + S.bcnt[j] > a.rec_cap || kb + S.bkb[j] > a.keys_cap || vb + S.bvb[j] > a.vals_cap)) {
+      if (a.write && !(fits_at(rb, S.bcnt[j], a.rec_cap) && fits_at(kb, S.bkb[j], a.keys_cap) &&
+                       fits_at(vb, S.bvb[j], a.vals_cap))) {
         st = MTBLX_ST_OVERFLOW;
         S.bwr[j] = 0;
         ws_flag(a, 1ull);
@@ -1809,7 +1815,8 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
   }
   // the copy waves need only tpre, and bwr where a block overflows the caller's buffers: when
   // the whole tile fits, release them before the per-block outputs are written
-  const bool fits = !a.write || (tinc[0] <= a.rec_cap && tinc[1] <= a.keys_cap && tinc[2] <= a.vals_cap);
+  const bool fits = !a.write || (fits_at(pr, B.ttot[0], a.rec_cap) && fits_at(pk, B.ttot[1], a.keys_cap) &&
+                                 fits_at(pv, B.ttot[2], a.vals_cap));
   if (fits) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(ready, rv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1827,7 +1834,8 @@ __device__ __forceinline__ void pipe_lookback(PipeBuf<P>& B, const TileArgs& a, 
     a.key_base[b] = kb;
     a.val_base[b] = vb;
     int32_t st = B.bst[j];
-    if (a.write && (rb + B.bcnt[j] > a.rec_cap || kb + B.bkb[j] > a.keys_cap || vb + B.bvb[j] > a.vals_cap)) {
+    if (a.write && !(fits_at(rb, B.bcnt[j], a.rec_cap) && fits_at(kb, B.bkb[j], a.keys_cap) &&
+                     fits_at(vb, B.bvb[j], a.vals_cap))) {
       st = MTBLX_ST_OVERFLOW;
       B.bwr[j] = 0;
       ws_flag(a, 1ull);

@@ -38,6 +38,19 @@ encab)   # k_encode A/B on one cfg3 chunk: product vs build/libmtblx_<v>.so for 
     for v in ${ENCV:-}; do step encab_${v}_$r 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
   done
   grep -H -o '"encode_GiB_per_s": [0-9.]*' $O/encab_*.log || true ;;
+crcab)   # CRC kernel variants: parity of each (test_crc_mfma_gpu) then scripts/crc_ab.py over all of them
+  ARGS=""
+  for v in ${CRCV:-}; do
+    step gpu_crc_$v 300 env MTBLX_LIB=oxidized-mtbl_amd/build/libmtblx_$v.so $PT tests/test_crc_mfma_gpu.py
+    ARGS="$ARGS mfma@oxidized-mtbl_amd/build/libmtblx_$v.so"
+  done
+  step crcab 600 python -u scripts/crc_ab.py $ARGS ;;
+snapprof)   # k_snappy_lanes on the compressible 100 000-block stream: kernel stats + SQ counters (separate passes)
+  A="scripts/snappy_probe.py --blocks 25000 --tile 4 --compressible --reps 3"
+  P="rocprofv3 --output-format csv"
+  step snap_stats 240 $P --kernel-trace --stats -d $O/snap_stats -o run -- python3 $A
+  step snap_p1 120 $P --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-include-regex k_snappy -d $O/snap_p1 -o run -- python3 $A
+  step snap_p2 120 $P --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES --kernel-include-regex k_snappy -d $O/snap_p2 -o run -- python3 $A ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

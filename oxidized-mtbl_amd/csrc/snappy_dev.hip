@@ -1431,6 +1431,340 @@ __global__ void __launch_bounds__(kWave) k_snappy_exec(const uint8_t* src, const
 }
 }  // namespace two
 
+// ---- Compressible blocks (round 6): one WAVE per block, the element chain found in parallel ----
+//
+// k_snappy_lanes pays the whole tag chain of a block serially on one lane (~300 vector and ~250
+// scalar instructions per 16-byte chunk, 65 % of wave time waiting, SQ counters in
+// profiles/r06/snappy).  Its copies do not need that order: on the bench's compressible stream a
+// block's 316 elements (199 copies) form a dependency DAG only ~25 levels deep (a copy depends on
+// the elements that wrote its source bytes).  Here a wave takes one block, everything in LDS:
+//  1. parse: J(p) = p + size of the element whose tag is at stream position p, for EVERY p; the
+//     element starts are the positions reachable from the preamble end, marked by pointer doubling
+//     (mark J_k(p) for marked p, J_(k+1) = J_k o J_k; ceil(log2(n + 2)) rounds) -- position n ends
+//     the chain, n + 1 is an overshoot (a header or literal past the end: corrupt);
+//  2. the starts compacted in stream order, every element decoded at once, output offsets by a
+//     wave prefix sum; the checks of the serial decoder per element (header bytes present,
+//     literal inside the stream, copy offset in 1 .. bytes before it, output not past the stated
+//     length) and the total, so CORRUPT exactly where the serial decode is;
+//  3. literals written at once; then copies in ROUNDS: a copy runs once every byte it reads is
+//     written (a bitmap of written output bytes), ~25 rounds instead of 199 steps;
+//  4. the output to HBM with 16-byte stores.
+// Blocks whose stream or output exceed the LDS buffers, or with more than 512 elements, are left
+// to k_snappy_deferred (status kDefer).
+namespace wavep {
+constexpr int IN = 2304;                        // stored bytes (compressible: W > 2n, W <= OUT)
+constexpr int OUT = 4608;                       // output bytes
+constexpr int K = 8;                            // elements per lane
+constexpr int MAXE = K * kWave;                 // 512
+constexpr int NP = IN + 2;                      // chain positions: stream, n (end), n + 1 (overshoot)
+constexpr int PPL = (NP + kWave - 1) / kWave;   // positions per lane (contiguous)
+#ifndef MTBLX_WAVEP_WG_PER_CU
+#define MTBLX_WAVEP_WG_PER_CU 12
+#endif
+
+struct alignas(16) Lds {
+  uint8_t in[IN + 32];          // the stored stream; slack: 8-byte header reads past its end
+  uint8_t out[OUT + 64];        // the output; during the parse J_k as u16 per position
+  uint16_t jb[NP + 2];          // element starts after the parse (epos)
+  uint32_t mark[NP / 32 + 2];   // reachable chain positions
+  uint32_t rdy[OUT / 32 + 4];   // output bytes written
+  uint32_t psel[16][4][3];      // period selectors of short overlapping copies (as k_snappy_lanes)
+};
+
+typedef uint32_t v4w __attribute__((ext_vector_type(4)));
+typedef uint32_t v4g __attribute__((ext_vector_type(4), aligned(1)));   // unaligned global loads
+
+// 16 bytes of LDS at any byte address a (5 aligned dwords joined)
+__device__ __forceinline__ v4w lds16(const uint8_t* base, uint32_t a) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (a & ~3u));
+  const uint32_t r = a & 3u;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  return v4w{__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+             __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
+}
+__device__ __forceinline__ uint32_t wsel(const v4w& v, uint32_t i) {   // dword i (0..4, 4 = 0)
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : i == 3 ? v.w : 0u;
+}
+// bytes [0, cnt) of v (cnt <= 16) to LDS address a, exactly: bytes up to the first dword boundary,
+// whole dwords, trailing bytes (no read-modify-write: neighbouring bytes may belong to other lanes)
+__device__ __forceinline__ void lds_put(uint8_t* base, uint32_t a, const v4w& v, uint32_t cnt) {
+  const uint32_t h = (4u - (a & 3u)) & 3u;   // head bytes
+  const uint32_t hb = h < cnt ? h : cnt;
+  for (uint32_t i = 0; i < hb; ++i) base[a + i] = (uint8_t)(wsel(v, i >> 2) >> (8 * (i & 3u)));
+  // dword k of the rest starts at byte hb + 4k of v
+  const uint32_t nw = (cnt - hb) >> 2, sh = hb & 3u, q = hb >> 2;
+  uint32_t* wd = reinterpret_cast<uint32_t*>(base + a + hb);
+  for (uint32_t k = 0; k < nw; ++k)
+    wd[k] = __builtin_amdgcn_alignbyte(wsel(v, q + k + 1), wsel(v, q + k), sh);
+  for (uint32_t i = hb + 4 * nw; i < cnt; ++i) base[a + i] = (uint8_t)(wsel(v, i >> 2) >> (8 * (i & 3u)));
+}
+// output bytes [a, b) written: bits in rdy
+__device__ __forceinline__ void set_rdy(uint32_t* rdy, uint32_t a, uint32_t b) {
+  for (uint32_t w = a >> 5; a < b && w <= (b - 1) >> 5; ++w) {
+    const uint32_t lo = w == (a >> 5) ? (a & 31u) : 0u, hi = w == ((b - 1) >> 5) ? ((b - 1) & 31u) : 31u;
+    const uint32_t m = (hi == 31u ? 0xFFFFFFFFu : ((1u << (hi + 1u)) - 1u)) & ~((1u << lo) - 1u);
+    atomicOr(rdy + w, m);
+  }
+}
+__device__ __forceinline__ bool all_rdy(const uint32_t* rdy, uint32_t a, uint32_t b) {   // [a, b), b - a <= 64
+  bool ok = true;
+  for (uint32_t w = a >> 5; a < b && w <= (b - 1) >> 5; ++w) {
+    const uint32_t lo = w == (a >> 5) ? (a & 31u) : 0u, hi = w == ((b - 1) >> 5) ? ((b - 1) & 31u) : 31u;
+    const uint32_t m = (hi == 31u ? 0xFFFFFFFFu : ((1u << (hi + 1u)) - 1u)) & ~((1u << lo) - 1u);
+    ok = ok && (rdy[w] & m) == m;
+  }
+  return ok;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int lane, uint32_t& total) {
+  uint32_t v = x;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)v, d, kWave);
+    if (lane >= d) v += y;
+  }
+  total = (uint32_t)__shfl((int)v, kWave - 1, kWave);
+  return v - x;
+}
+
+constexpr uint32_t kRounds = 10;   // pointer-doubling rounds: chains of up to 2^10 elements (more: kDefer)
+// J(p): the position after the element whose tag is at p (n + 1: past the stream's end)
+__device__ __forceinline__ uint32_t jnext(const uint8_t* in, uint32_t p, uint32_t pos0, uint32_t n) {
+  if (p < pos0 || p >= n) return p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + (p & ~3u));
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], p & 3u), hi = __builtin_amdgcn_alignbyte(w[2], w[1], p & 3u);
+  const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2;
+  const uint32_t raw = __builtin_amdgcn_alignbyte(hi, lo, 1u);
+  uint64_t sz;
+  if (kind == 0u) {
+    const uint32_t nb = t2 >= 60u ? t2 - 59u : 0u;
+    const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * nb)) - 1u);
+    sz = t2 >= 60u ? 2ull + nb + (uint64_t)ext : 2ull + t2;
+  } else {
+    sz = kind == 1u ? 2u : kind == 2u ? 3u : 5u;
+  }
+  return (uint64_t)p + sz > (uint64_t)n ? n + 1u : p + (uint32_t)sz;
+}
+
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) k_snappy_waves(const uint8_t* src, const uint64_t* src_off,
+                                                        const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
+                                                        const uint64_t* dst_off, const uint32_t* dst_len,
+                                                        int32_t* status, uint32_t* dec_len, int only_marked) {
+  __shared__ Lds S;
+  const int lane = threadIdx.x;
+  {   // period selectors: offset o < 16, output dword i, byte j = source byte (4 i + j) mod o
+    const uint32_t o = (uint32_t)lane >> 2, i = (uint32_t)lane & 3u;
+    uint32_t lo = 0, hi = 0, mk = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t m = o ? (4u * i + j) % o : 0u;
+      if (m < 8u) lo |= m << (8 * j);
+      else {
+        hi |= (m - 8u) << (8 * j);
+        mk |= 0xFFu << (8 * j);
+      }
+    }
+    S.psel[o][i][0] = lo;
+    S.psel[o][i][1] = hi;
+    S.psel[o][i][2] = mk;
+  }
+  uint16_t* J = reinterpret_cast<uint16_t*>(S.out);
+  uint64_t wdbg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    MTBLX_CHK(status + b, 4);
+    if (only_marked && status[b] != quad::kLanes) continue;   // uniform
+    const uint8_t* s = src + src_off[b];
+    const uint32_t n = src_len[b];
+    uint8_t* dg = dst + dst_off[b];
+    const uint32_t cap = dst_len[b];
+    if (n) MTBLX_CHK(s, n);
+    if (cap) MTBLX_CHK(dg, cap);
+    // ---- preamble (the quad kernel's checks) ----
+    uint64_t want = 0;
+    uint32_t pos0 = 0;
+    bool term = false;
+    for (uint32_t i = 0; i < 5 && i < n; ++i) {
+      const uint32_t byte = s[i];
+      want |= (uint64_t)(byte & 0x7fu) << (7 * i);
+      if (!(byte & 0x80u)) {
+        term = true;
+        pos0 = i + 1;
+        break;
+      }
+    }
+    int32_t st = MTBLX_SNAPPY_OK;
+    if (!term || want > 0xFFFFFFFFull || want > kMaxExpand * (uint64_t)n) st = MTBLX_SNAPPY_CORRUPT;
+    else if (want > cap) st = MTBLX_SNAPPY_TOO_SMALL;
+    else if (n > (uint32_t)IN || want > (uint64_t)OUT) st = quad::kDefer;
+    const uint32_t W = (uint32_t)want;
+    uint64_t tw = SNAP_T();   // diagnostic stamps (snapstamps build): per-phase cycles, summed per wave
+    auto stamp = [&](int k) { const uint64_t t = SNAP_T(); wdbg[k] += t - tw; tw = t; };
+    wdbg[5] += 1;
+    if (st == MTBLX_SNAPPY_OK) {
+      // ---- the stream into LDS (16-byte chunks; zeros past n) ----
+      for (uint32_t c = (uint32_t)lane; 16u * c < n + 16u; c += kWave) {
+        const uint32_t p = 16u * c;
+        v4w v = {0u, 0u, 0u, 0u};
+        if (p + 16u <= n) {
+          MTBLX_CHK(s + p, 16);
+          v = *reinterpret_cast<const v4g*>(s + p);
+        } else if (p < n) {
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
+          for (uint32_t t = 0; p + t < n; ++t) w[t >> 2] |= (uint32_t)s[p + t] << (8 * (t & 3u));
+          v = v4w{w[0], w[1], w[2], w[3]};
+        }
+        *reinterpret_cast<v4w*>(S.in + p) = v;
+      }
+      stamp(0);
+      // ---- 1. the chain: J(p) for every position (lane + 64 i), reachability by doubling ----
+      const uint32_t np = n + 2u;
+      uint16_t* A = J;        // J_k
+      uint16_t* B = S.jb;     // J_(k+1)
+      for (uint32_t p = (uint32_t)lane; p < np; p += kWave) A[p] = (uint16_t)jnext(S.in, p, pos0, n);
+      for (uint32_t w = (uint32_t)lane; w < np / 32u + 2u; w += kWave) S.mark[w] = 0u;
+      if (lane == 0) atomicOr(&S.mark[pos0 >> 5], 1u << (pos0 & 31u));
+      for (uint32_t r = 0; r < kRounds; ++r) {
+#pragma unroll 4
+        for (uint32_t p = (uint32_t)lane; p < np; p += kWave) {
+          const uint32_t j = A[p];
+          if ((S.mark[p >> 5] >> (p & 31u)) & 1u) atomicOr(&S.mark[j >> 5], 1u << (j & 31u));
+          B[p] = A[j];
+        }
+        uint16_t* t = A;
+        A = B;
+        B = t;
+      }
+      const bool ends = (S.mark[n >> 5] >> (n & 31u)) & 1u, over = (S.mark[(n + 1u) >> 5] >> ((n + 1u) & 31u)) & 1u;
+      if (over) st = MTBLX_SNAPPY_CORRUPT;
+      else if (!ends) st = quad::kDefer;   // a chain of more than 2^kRounds elements
+      stamp(1);
+      // ---- 2. element records in stream order (row i = positions 64 i .. 64 i + 63) ----
+      uint32_t* erec = reinterpret_cast<uint32_t*>(S.jb);   // [e] = d | L << 16, [MAXE + e] = x | lit << 31
+      uint32_t m = 0, dsum = 0;
+      bool bad = false;
+      for (uint32_t row = 0; st == MTBLX_SNAPPY_OK && 64u * row < n; ++row) {
+        const uint32_t p = 64u * row + (uint32_t)lane;
+        const bool isel = p >= pos0 && p < n && ((S.mark[p >> 5] >> (p & 31u)) & 1u);
+        uint32_t L = 0, x = 0;
+        bool lit = false, eb = false;
+        if (isel) {
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(S.in + (p & ~3u));
+          const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], p & 3u), hi = __builtin_amdgcn_alignbyte(w[2], w[1], p & 3u);
+          const uint32_t tag = lo & 0xffu, kind = tag & 3u, t2 = tag >> 2, avail = n - p - 1u;
+          const uint32_t raw = __builtin_amdgcn_alignbyte(hi, lo, 1u);
+          lit = kind == 0u;
+          if (lit) {
+            const bool lg = t2 >= 60u;
+            const uint32_t nb = lg ? t2 - 59u : 0u;
+            const uint32_t ext = raw & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * nb)) - 1u);
+            const uint32_t sp = p + 1u + nb;
+            L = lg ? ext + 1u : t2 + 1u;
+            eb = (lg && (avail < nb || ext == 0xFFFFFFFFu)) || sp > n || n - sp < L;
+            x = sp;
+          } else {
+            const uint32_t need = kind == 1u ? 1u : kind == 2u ? 2u : 4u;
+            L = kind == 1u ? 4u + (t2 & 7u) : t2 + 1u;
+            x = kind == 1u ? ((tag >> 5) << 8) | ((lo >> 8) & 0xffu) : kind == 2u ? raw & 0xffffu : raw;
+            eb = avail < need || x == 0u;
+          }
+        }
+        const uint64_t mk = __ballot(isel);
+        const uint32_t e = m + (uint32_t)__builtin_popcountll(mk & ((1ull << lane) - 1ull));
+        const uint32_t Lc = L > 0xFFFFu ? 0xFFFFu : L;   // a bad element's length: only the sum must not wrap
+        uint32_t tot = 0;
+        const uint32_t d = dsum + wave_excl_scan(isel ? Lc : 0u, lane, tot);
+        if (isel) {
+          eb = eb || (!lit && x > d) || d > W || W - d < L;
+          bad = bad || eb;
+          if (e < (uint32_t)MAXE) {
+            erec[e] = d | (Lc << 16);
+            erec[MAXE + e] = (x & 0xFFFFu) | (lit ? 0x80000000u : 0u);
+          }
+        }
+        m += (uint32_t)__builtin_popcountll(mk);
+        dsum += tot;
+      }
+      if (st == MTBLX_SNAPPY_OK) {
+        if (__ballot(bad) != 0ull || dsum != W) st = MTBLX_SNAPPY_CORRUPT;
+        else if (m > (uint32_t)MAXE) st = quad::kDefer;
+      }
+      if (st == MTBLX_SNAPPY_OK) {
+        stamp(2);
+        // ---- 3. literals, then copies in rounds (element e on lane e mod 64) ----
+        for (uint32_t w = (uint32_t)lane; w < W / 32u + 2u; w += kWave) S.rdy[w] = 0u;
+        uint32_t pend = 0;   // bit k: element lane + 64 k is a copy not yet written
+        for (uint32_t k = 0, e = (uint32_t)lane; e < m; ++k, e += kWave) {
+          const uint32_t r0 = erec[e], r1 = erec[MAXE + e];
+          const uint32_t d = r0 & 0xFFFFu, L = r0 >> 16;
+          if (r1 & 0x80000000u) {
+            const uint32_t sp = r1 & 0xFFFFu;
+            for (uint32_t c = 0; c < L; c += 16u) lds_put(S.out, d + c, lds16(S.in, sp + c), L - c < 16u ? L - c : 16u);
+            set_rdy(S.rdy, d, d + L);
+          } else {
+            pend |= 1u << k;
+          }
+        }
+        stamp(3);
+        for (uint32_t guard = 0; __ballot(pend != 0u) != 0ull && guard <= (uint32_t)MAXE; ++guard) {
+          wdbg[6] += 1;
+          uint32_t go = 0;
+          for (uint32_t q = pend; q; q &= q - 1u) {
+            const uint32_t k = (uint32_t)__builtin_ctz(q), e = (uint32_t)lane + (uint32_t)kWave * k;
+            const uint32_t r0 = erec[e], off = erec[MAXE + e] & 0xFFFFu;
+            const uint32_t d = r0 & 0xFFFFu, L = r0 >> 16;
+            if (all_rdy(S.rdy, d - off, d - off + (L < off ? L : off))) go |= 1u << k;
+          }
+          for (uint32_t q = go; q; q &= q - 1u) {
+            const uint32_t k = (uint32_t)__builtin_ctz(q), e = (uint32_t)lane + (uint32_t)kWave * k;
+            const uint32_t r0 = erec[e], off = erec[MAXE + e] & 0xFFFFu;
+            const uint32_t d = r0 & 0xFFFFu, L = r0 >> 16;
+            if (off < 16u && off < L) {   // the period: chunk 0 by byte permutes, later chunks at off2
+              const v4w qv = lds16(S.out, d - off);
+              uint32_t pw[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const uint32_t pl = __builtin_amdgcn_perm(qv.y, qv.x, S.psel[off][i][0]);
+                const uint32_t ph = __builtin_amdgcn_perm(qv.w, qv.z, S.psel[off][i][1]);
+                const uint32_t mk = S.psel[off][i][2];
+                pw[i] = (pl & ~mk) | (ph & mk);
+              }
+              lds_put(S.out, d, v4w{pw[0], pw[1], pw[2], pw[3]}, L < 16u ? L : 16u);
+              const uint32_t off2 = off * ((16u + off - 1u) / off);
+              for (uint32_t c = 16u; c < L; c += 16u) lds_put(S.out, d + c, lds16(S.out, d + c - off2), L - c < 16u ? L - c : 16u);
+            } else {
+              for (uint32_t c = 0; c < L; c += 16u) lds_put(S.out, d + c, lds16(S.out, d - off + c), L - c < 16u ? L - c : 16u);
+            }
+            set_rdy(S.rdy, d, d + L);
+          }
+          pend &= ~go;
+        }
+        if (__ballot(pend != 0u) != 0ull) st = MTBLX_SNAPPY_CORRUPT;   // unreachable: a round without progress
+        stamp(4);
+      }
+    }
+    // ---- 4. output, statuses ----
+    if (st == MTBLX_SNAPPY_OK) {
+      const uint32_t n16 = W / 16u;
+      if (((uintptr_t)dg & 15u) == 0) {
+        for (uint32_t c = (uint32_t)lane; c < n16; c += kWave) {
+          MTBLX_CHK(dg + 16u * c, 16);
+          *reinterpret_cast<v4w*>(dg + 16u * c) = *reinterpret_cast<const v4w*>(S.out + 16u * c);
+        }
+        for (uint32_t j = 16u * n16 + (uint32_t)lane; j < W; j += kWave) dg[j] = S.out[j];
+      } else {
+        for (uint32_t j = (uint32_t)lane; j < W; j += kWave) dg[j] = S.out[j];
+      }
+    }
+    if (lane == 0) {
+      status[b] = st;
+      if (dec_len && st != quad::kDefer) dec_len[b] = st == MTBLX_SNAPPY_OK ? W : 0u;
+    }
+    stamp(7);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) SNAP_ADD(k, wdbg[k]);
+  (void)wdbg;
+}
+}  // namespace wavep
+
 
 // ---- directory: preamble lengths, 16-byte aligned exclusive prefix ----
 constexpr int kDirThreads = 256, kDirPer = 8, kDirSpan = kDirThreads * kDirPer;
@@ -1577,7 +1911,8 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
   // >= kLanesMinBlocks, blocks expanding > 2x go to k_snappy_lanes, the rest to the quad /
   // one-wave kernels), "lanes" (every block), "quads"
   const char* e = getenv("MTBLX_SNAPPY_KERNEL");
-  const int mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : (e && !strcmp(e, "two")) ? 3 : 0;
+  const int mode = (e && !strcmp(e, "lanes")) ? 2 : (e && !strcmp(e, "quads")) ? 1 : (e && !strcmp(e, "two")) ? 3
+                   : (e && !strcmp(e, "waves")) ? 4 : 0;
   // the compressible blocks k_snappy_quads marks: two passes (parse, execute) or one lane each
 #ifndef MTBLX_SNAPPY_TWO_DEFAULT
 #define MTBLX_SNAPPY_TWO_DEFAULT 0
@@ -1591,7 +1926,7 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
     // k_snappy_lanes costs about one block's serial decode however many blocks run (all are in
     // flight), the quads ~0.19 ms per round of 8 192 blocks: the lanes win from ~50 000 blocks
     // (25 000 compressible blocks: quads 0.66 ms, lanes ~1.0 ms; 100 000: 2.33 vs 1.24 ms)
-    const uint32_t lanes_x = ((mode == 0 && nblk >= kLanesMinBlocks) || mode == 3) ? 2u : 0u;
+    const uint32_t lanes_x = ((mode == 0 && nblk >= kLanesMinBlocks) || mode == 3 || mode == 4) ? 2u : 0u;
     MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), quad::k_snappy_quads, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                        dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, dst_len, max_dst_len, status,
                        dec_len, lanes_x);
@@ -1601,6 +1936,9 @@ extern "C" int mtblx_snappy_decompress_dev(const uint8_t* src, const uint64_t* s
                          status, dec_len);
       MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), two::k_snappy_exec, dim3(grid_for(quad::WG_PER_CU, (nblk + quad::NG - 1) / quad::NG)),
                          dim3(kWave), 0, s, src, src_off, src_len, nblk, dst, dst_off, status, dec_len);
+    } else if (lanes_x && mode == 4) {   // the wave-per-block kernel (round 6); its oversize blocks -> deferred
+      MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), wavep::k_snappy_waves, dim3(grid_for(MTBLX_WAVEP_WG_PER_CU, nblk)), dim3(kWave), 0, s,
+                         src, src_off, src_len, nblk, dst, dst_off, dst_len, status, dec_len, 1);
     } else if (lanes_x) {
       MTBLX_LAUNCH((src, MTBLX_R(src_off, 8ull * nblk), MTBLX_R(src_len, 4ull * nblk), dst, MTBLX_R(dst_off, 8ull * nblk), MTBLX_R(dst_len, 4ull * nblk), MTBLX_R(status, 4ull * nblk), MTBLX_R(dec_len, 4ull * nblk)), lanes::k_snappy_lanes, glanes, tlanes, 0, s, src, src_off, src_len, nblk, dst, dst_off,
                          dst_len, status, dec_len, 1);

@@ -83,6 +83,12 @@ def main():
             print("lanes: wave iterations %d; share of iterations where any lane took: %s" % (
                 it, ", ".join("%s %.3f" % (names[k], dbg[k] / it) for k in range(1, 8))), flush=True)
             return
+        if os.environ.get("MTBLX_SNAPPY_KERNEL") == "waves":   # k_snappy_waves' per-phase stamps
+            nb = max(int(dbg[5]), 1)
+            print("waves per block: stage %.0f  chain %.0f  records %.0f  literals %.0f  copy rounds %.0f (%.1f rounds)"
+                  "  output %.0f cycles" % (dbg[0] / nb, dbg[1] / nb, dbg[2] / nb, dbg[3] / nb, dbg[4] / nb,
+                                            dbg[6] / nb, dbg[7] / nb), flush=True)
+            return
         nb = max(int(dbg[5]), 1)
         print("per block: cycles %.0f  in flush %.0f  store %.0f  elements %.1f  flushes %.1f  restages %.2f  steps %.1f"
               % (dbg[0] / nb, dbg[1] / nb, dbg[2] / nb, dbg[3] / nb, dbg[4] / nb, dbg[6] / nb, dbg[7] / nb), flush=True)

@@ -18,13 +18,13 @@ from test_snappy import _inputs, _libsnappy
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["auto", "lanes", "two"], autouse=True)
+@pytest.fixture(params=["auto", "lanes", "two", "waves"], autouse=True)
 def snappy_kernel(request, monkeypatch):
     """every test under the default routing, with every block on k_snappy_lanes (one lane per
     block, output streamed to HBM) -- auto sends blocks there only in large batches -- and with
     the blocks expanding > 2x on the two-pass kernels (k_snappy_parse + k_snappy_exec) whatever
     the batch size"""
-    if request.param in ("lanes", "two"):
+    if request.param in ("lanes", "two", "waves"):
         monkeypatch.setenv("MTBLX_SNAPPY_KERNEL", request.param)
     else:
         monkeypatch.delenv("MTBLX_SNAPPY_KERNEL", raising=False)

@@ -46,11 +46,22 @@ crcab)   # CRC kernel variants: parity of each (test_crc_mfma_gpu) then scripts/
   done
   step crcab 600 python -u scripts/crc_ab.py $ARGS ;;
 snapprof)   # k_snappy_lanes on the compressible 100 000-block stream: kernel stats + SQ counters (separate passes)
-  A="scripts/snappy_probe.py --blocks 25000 --tile 4 --compressible --reps 3"
+  A="scripts/snappy_probe.py --blocks 100000 --tile 4 --compressible --reps 3"; export MTBLX_SNAPPY_KERNEL=lanes
   P="rocprofv3 --output-format csv"
   step snap_stats 240 $P --kernel-trace --stats -d $O/snap_stats -o run -- python3 $A
   step snap_p1 120 $P --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-include-regex k_snappy -d $O/snap_p1 -o run -- python3 $A
   step snap_p2 120 $P --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES --kernel-include-regex k_snappy -d $O/snap_p2 -o run -- python3 $A ;;
+snapstat)   # kernel stats of one snappy routing on the compressible stream
+  step snapstat 240 env MTBLX_SNAPPY_KERNEL=${SNAPK:-waves} rocprofv3 --kernel-trace --stats --output-format csv -d $O/snapstat -o run -- python3 scripts/snappy_probe.py --blocks 100000 --tile 4 --compressible --reps 3 ;;
+snapst)   # k_snappy_waves per-phase stamps (snapstamps diagnostic build)
+  step snapst 200 env MTBLX_LIB=oxidized-mtbl_amd/mtblx/libmtblx_snapstamps.so MTBLX_SNAPPY_KERNEL=waves python3 scripts/snappy_probe.py --blocks 100000 --tile 4 --compressible --reps 3 ;;
+snapab)   # device snappy kernels on the compressible 100 000-block stream, alternating, HIP events
+  for r in 1 2; do
+    for k in ${SNAPK:-lanes waves}; do
+      step snapab_${k}_$r 200 env MTBLX_SNAPPY_KERNEL=$k python3 scripts/snappy_probe.py --blocks 100000 --tile 4 --compressible --reps 10
+    done
+  done
+  grep -H "decompress" $O/snapab_*.log || true ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

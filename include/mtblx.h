@@ -19,7 +19,10 @@
  *    look-back words of both launch parities), so a call needs no fill: ZERO-FILL IT ONCE
  *    after allocating it, then reuse it for any sequence of batches of at most the
  *    nblk it was sized for.  One workspace serves one call at a time (per stream).
- *  - calls are asynchronous on `stream` and re-entrant (no global mutable state).
+ *  - calls are asynchronous on `stream` and re-entrant: the library keeps no mutable state
+ *    between calls -- every scratch buffer is the caller's (the block cut's too, since ABI v3);
+ *    the one process-wide datum is a per-device cache of what the hardware is (compute-unit
+ *    counts, kernel occupancy: csrc/devinfo.h), filled on first use with relaxed atomics.
  *  - return value: MTBLX_OK or a negative MTBLX_E_* (argument / HIP launch errors).
  *    Per-block outcomes are reported in `status[]` (MTBLX_ST_*), never by aborting.
  */

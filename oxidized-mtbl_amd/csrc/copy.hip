@@ -8,6 +8,7 @@
 
 #include "mtblx.h"
 #include "bounds.h"
+#include "devinfo.h"
 
 namespace {
 
@@ -106,13 +107,7 @@ extern "C" int mtblx_copy_ranges(const uint8_t* src, const uint64_t* src_off, ui
                                  void* stream) {
   if (n == 0 || nchunks == 0) return MTBLX_OK;
   if (!src || !src_off || !dst || !dst_off || !len || !chunk_base) return MTBLX_E_INVAL;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  const int ncu = mtblx_dev::cu_count();
   const uint64_t want = (nchunks + 4 * 256 - 1) / (4 * 256);
   const dim3 g((unsigned)(want < (uint64_t)ncu * 8u ? want : (uint64_t)ncu * 8u));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -125,13 +120,7 @@ extern "C" int mtblx_copy_ranges(const uint8_t* src, const uint64_t* src_off, ui
 extern "C" int mtblx_stream_copy(void* dst, const void* src, uint64_t bytes, int variant, void* stream) {
   if (!dst || !src || (bytes & 15u) || ((uintptr_t)dst & 15u) || ((uintptr_t)src & 15u)) return MTBLX_E_INVAL;
   if (bytes == 0) return MTBLX_OK;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  const int ncu = mtblx_dev::cu_count();
   const uint64_t n16 = bytes / 16u;
   const dim3 g((unsigned)ncu * 8u);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

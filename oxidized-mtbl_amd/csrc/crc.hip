@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include "bounds.h"
+#include "devinfo.h"
 #include "crc_dev.h"
 #include "crc_mfma.h"
 #include "crc_mfma_dev.h"
@@ -579,13 +580,7 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
   // 0.102 vs 0.120 ms on cfg2 (profiles/r04/crc_mfma)
   const char* kv = getenv("MTBLX_CRC_KERNEL");
   if (!kv || kv[0] != 'l') {
-    static int mgrid = 0;   // persistent: one 16-wave workgroup (160 KiB LDS) per CU
-    if (!mgrid) {
-      int dev = 0, ncu = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      mgrid = ncu > 0 ? ncu : 256;
-    }
+    const int mgrid = mtblx_dev::cu_count();   // persistent: one 16-wave workgroup (160 KiB LDS) per CU
     const uint32_t need = (in->nblk + mtblx_crc::kMWaves - 1u) / mtblx_crc::kMWaves;
     const dim3 g(need < (uint32_t)mgrid ? need : (uint32_t)mgrid), t(mtblx_crc::kMThreads);
     MTBLX_LAUNCH((MTBLX_R(in->data, in->data_len), MTBLX_R(in->blk_off, 8ull * in->nblk),
@@ -595,18 +590,12 @@ extern "C" int mtblx_crc32c_blocks(const mtblx_block_batch* in, uint32_t* crc, u
                        in->data_len, in->blk_off, in->blk_len, in->nblk, crc, bad, framed);
     return hipGetLastError() == hipSuccess ? MTBLX_OK : MTBLX_E_HIP;
   }
-  static int grid = 0;
-  if (!grid) {
-    int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
 // 98 VGPRs: one 1024-thread workgroup is resident per CU, so a grid of one workgroup per CU runs
 // in a single round; 2 per CU measured 0.1256-0.1261 ms against 0.1232 (profiles/r03/final2)
 #ifndef MTBLX_CRC_WG_PER_CU
 #define MTBLX_CRC_WG_PER_CU 1
 #endif
-    grid = (ncu > 0 ? ncu : 256) * MTBLX_CRC_WG_PER_CU;
-  }
+  const int grid = mtblx_dev::cu_count() * MTBLX_CRC_WG_PER_CU;
   const uint32_t wpg = mtblx_crc::kCrcThreads / mtblx_crc::kWave;   // waves (blocks in flight) per workgroup
   const uint32_t need = (in->nblk + wpg - 1u) / wpg;
   const dim3 g(need < (uint32_t)grid ? need : (uint32_t)grid), t(mtblx_crc::kCrcThreads);

@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "bounds.h"
+#include "devinfo.h"
 #include "crc_dev.h"
 #include "crc_mfma.h"
 #include "crc_mfma_dev.h"
@@ -2761,33 +2762,29 @@ Plan make_plan(uint32_t nblk, uint32_t max_len) {
 // workgroups needs.  MTBLX_PIPE_CUS caps it (diagnostic: several processes sharing one GPU, e.g.
 // bench.py --share-gpu, each keep their launches co-resident on their share of the CUs).
 int pipe_grid(uint32_t ntiles) {
-  static int cached = 0;
-  if (!cached) {
-    int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  static mtblx_dev::Cache cache;
+  const int g = cache.get([] {
+    int ncu = mtblx_dev::cu_count();
     const char* cap = getenv("MTBLX_PIPE_CUS");
     if (cap && atoi(cap) > 0) ncu = std::min(ncu, atoi(cap));
-    cached = std::max(1, std::min(ncu, kMaxLookbackLoads * kWave + 1));
-  }
-  return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
+    return std::max(1, std::min(ncu, kMaxLookbackLoads * kWave + 1));
+  });
+  return (int)std::min<uint32_t>(ntiles, (uint32_t)g);
 }
 
 template <class C>
 int resident_grid(uint32_t ntiles) {
-  static int cached = 0;
-  if (!cached) {
-    int dev = 0, ncu = 0, occ = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  static mtblx_dev::Cache cache;
+  const int g = cache.get([] {
+    int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_decode_tiles<C>, kThreads, 0) != hipSuccess || occ < 1)
       occ = 1;
     int lds_lim = (int)((160u * 1024u) / sizeof(TileLds<C>));
     if (lds_lim < 1) lds_lim = 1;
-    cached = std::max(1, ncu * std::min(occ, lds_lim));
-    cached = std::min(cached, kMaxLookbackLoads * kThreads + 1);  // look-back window = G - 1
-  }
-  return (int)std::min<uint32_t>(ntiles, (uint32_t)cached);
+    const int c = std::max(1, mtblx_dev::cu_count() * std::min(occ, lds_lim));
+    return std::min(c, kMaxLookbackLoads * kThreads + 1);  // look-back window = G - 1
+  });
+  return (int)std::min<uint32_t>(ntiles, (uint32_t)g);
 }
 }  // namespace
 

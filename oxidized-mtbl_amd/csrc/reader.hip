@@ -15,6 +15,7 @@
 #include <stdlib.h>
 
 #include "bounds.h"
+#include "devinfo.h"
 #include "crc_dev.h"
 #include "mtblx.h"
 
@@ -1045,17 +1046,9 @@ extern "C" int mtblx_block_dir(const uint8_t* file, uint64_t file_len, uint32_t 
 static void get_launch(const uint8_t* file, uint64_t file_len, uint32_t version, int verify, uint64_t index_off,
                        uint64_t index_len, mtblx_rd::DecTab tab, const uint8_t* keys, const uint64_t* key_end,
                        uint32_t nq, int32_t* status, uint64_t* val_off, uint64_t* val_len, hipStream_t s) {
-  static int grid = 0, wave = -1;
-  if (!grid) {
-    int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = (ncu > 0 ? ncu : 256) * 8;
-  }
-  if (wave < 0) {
-    const char* e = getenv("MTBLX_GET_KERNEL");
-    wave = e && e[0] == 'w' ? 1 : 0;
-  }
+  const int grid = mtblx_dev::cu_count() * 8;
+  const char* ge = getenv("MTBLX_GET_KERNEL");   // A/B knob, read per call
+  const int wave = ge && ge[0] == 'w' ? 1 : 0;
   const uint64_t per = wave ? 4u : 256u;   // queries per workgroup per pass
   const uint64_t need = (nq + per - 1) / per;
   const dim3 g((unsigned)(need < (uint64_t)grid ? need : (uint64_t)grid));

@@ -40,6 +40,7 @@
 #include <utility>
 
 #include "bounds.h"
+#include "devinfo.h"
 #include "mtblx.h"
 
 // timing ablations (wrong output by construction): diagnostic targets only (-DMTBLX_DIAG)
@@ -1862,14 +1863,7 @@ __global__ void __launch_bounds__(kDirThreads) k_snap_off(const uint32_t* dst_le
 }
 
 int grid_for(int per_cu, uint32_t units) {
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
-  const uint32_t g = (uint32_t)(ncu * per_cu);
+  const uint32_t g = (uint32_t)(mtblx_dev::cu_count() * per_cu);
   return (int)(units < g ? (units ? units : 1u) : g);
 }
 

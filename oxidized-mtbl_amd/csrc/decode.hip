@@ -2404,6 +2404,12 @@ constexpr bool kLargeSerial = false;
 #ifndef MTBLX_LARGE_LATE
 #define MTBLX_LARGE_LATE 1
 #endif
+#ifndef MTBLX_PHASE_DELAY     // A/B: PipeLarge workgroups of one half start this many cycles late
+#define MTBLX_PHASE_DELAY 0
+#endif
+#ifndef MTBLX_PHASE_SEL       // ... the half: 0 = odd workgroups, 1 = (g >> 3) odd (half of each XCD)
+#define MTBLX_PHASE_SEL 0
+#endif
 #ifndef MTBLX_LATE_LOADCOPY   // late walk: the loaders copy rows of tile it after their DMA
 #define MTBLX_LATE_LOADCOPY 0
 #endif
@@ -2483,6 +2489,17 @@ __global__ void __launch_bounds__(kPipeThreads, 1) k_decode_pipe(TileArgs a) {
   }
   __syncthreads();
   TL(1);
+#if MTBLX_PHASE_DELAY > 0
+  // A/B (diagnostic builds): start half of the workgroups MTBLX_PHASE_DELAY shader cycles late so
+  // that the two halves' DMA + store phases (HBM-bound) do not coincide
+  if constexpr (P::NBUF == 2) {
+    const bool late_half = MTBLX_PHASE_SEL == 0 ? (g & 1u) != 0u : ((g >> 3) & 1u) != 0u;
+    if (late_half) {
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)MTBLX_PHASE_DELAY) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+#endif
   if (wv == 0) __builtin_amdgcn_s_setprio(2);  // the walk is a serial latency chain
   uint64_t ntl = 0;
   uint32_t wmode = 0;   // wave 0: which interval walk goes first (pipe_walk)

@@ -62,6 +62,17 @@ snapab)   # device snappy kernels on the compressible 100 000-block stream, alte
     done
   done
   grep -H "decompress" $O/snapab_*.log || true ;;
+decab)   # PipeLarge A/B on one cfg3 chunk (decode GiB/s = value): product vs build/libmtblx_<v>.so for v in $DECV, twice
+  B="python bench.py --config cfg3 --cfg3-blocks 100000 --steps 3 --warmup 1 --no-cpu-baseline --no-get"
+  for r in 1 2; do
+    step decab_prod$r 300 $B
+    for v in ${DECV:-}; do step decab_${v}_$r 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
+  done
+  grep -H -o '"value": [0-9.]*' $O/decab_*.log || true ;;
+decst)   # PipeLarge per-phase stamps: the product stamps build vs build/libmtblx_<v>.so for v in $STV
+  B="python bench.py --config cfg3 --cfg3-blocks 100000 --no-cpu-baseline --no-get --stamps"
+  step decst_prod 300 $B --lib oxidized-mtbl_amd/mtblx/libmtblx_stamps.so
+  for v in ${STV:-}; do step decst_$v 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

@@ -2223,8 +2223,11 @@ __device__ __forceinline__ void pipe_crc_final(const PipeBuf<P>& B, const TileAr
 #define MTBLX_FUSED_MFMA 0
 #endif
 constexpr int kDecSup = (65664 + mtblx_crc::kMStep * mtblx_crc::kMSup - 1) / (mtblx_crc::kMStep * mtblx_crc::kMSup) + 1;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunneeded-internal-declaration"   // read only by the A/B path
 static __constant__ mtblx_crc::MfmaTabs kDecMfma = mtblx_crc::MfmaTabs();
 static __constant__ mtblx_crc::SwTabs<kDecSup> kDecSw = mtblx_crc::SwTabs<kDecSup>();
+#pragma clang diagnostic pop
 
 template <class P>
 __device__ __forceinline__ void pipe_crc_mfma(const PipeBuf<P>& B, PipeLds<P>& S, uint32_t cw, int lane, uint32_t par) {

@@ -632,6 +632,17 @@ __device__ __forceinline__ uint64_t lookback(const EncArgs& a, uint32_t b, int l
 #define ESTAMP(k) do { } while (0)
 #endif
 
+#ifndef MTBLX_ENC_RAWB   // TW path: LDS-only barriers (1) or __syncthreads (0: also waits for the block's stores)
+#define MTBLX_ENC_RAWB 0
+#endif
+__device__ __forceinline__ void tw_barrier() {
+#if MTBLX_ENC_RAWB
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
 template <bool PL>   // PL: planned mode (sizes and offsets from the block cut's sums; no look-back)
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MTBLX_ENC_WPE))) k_encode(EncArgs a) {   // 2 per CU
   __shared__ EncLds S;
@@ -838,7 +849,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       uint32_t(*hk)[16] = reinterpret_cast<uint32_t(*)[16]>(&S.T[0][0]);   // x^(8·8192): swk
       if (tid < 128) (&hk[0][0])[tid] = tw_swk;
       if (tid == 0) S.sh_u64[0] = tw_fin - F;
-      __syncthreads();   // the block (and its zero pad), the table, the offset
+      tw_barrier();   // the block (and its zero pad), the table, the offset
 #pragma unroll
       for (int k = 0; k < kMKs; ++k) asm volatile("" ::"v"(A[k][0]), "v"(A[k][1]));
       asm volatile("" ::"v"(a2lo), "v"(a2hi));   // the operands' wait is here, before the stores
@@ -881,7 +892,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
       }
       uint32_t* part = reinterpret_cast<uint32_t*>(S.shc);   // planned mode never reads shc
       part[w * kWave + lane] = acc;
-      __syncthreads();
+      tw_barrier();   // the parts (LDS); the block's stores stay in flight
       ESTAMP(6);   // stores issued + CRC
       if (w == 0 && fits) {   // column shift x^(8·64·n), XOR over the columns, pad removal x^(-8t)
         uint32_t pw = 0;

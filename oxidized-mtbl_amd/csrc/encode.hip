@@ -302,12 +302,6 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
   return before + inc - x;
 }
 
-// copy n bytes from global src to dst (LDS or global, generic pointer).  Four 16-byte loads
-// are in flight before their stores (the loads are the latency: a serial load -> store chain
-// per 16 bytes was most of the encode time); stores are unaligned 16-byte stores (gfx950 runs
-// in unaligned access mode).  A tail of 1..15 bytes is read as the 16-byte window ending at n
-// when the record is at least 16 bytes long (never before `base`, the blob's start), else
-// byte by byte.
 #ifndef MTBLX_ENC_CARRY   // the next entry's offsets carried from this one (A/B: 0 = reload both ends)
 #define MTBLX_ENC_CARRY 1
 #endif
@@ -318,6 +312,53 @@ __device__ __forceinline__ uint64_t wg_excl_scan(EncLds& S, uint64_t x, uint64_t
 #define MTBLX_ENC_NT_STORES 1
 #endif
 
+// the last t (1..15) bytes of the 16-byte window w, stored at d
+__device__ __forceinline__ void store_tail(uint8_t* d, const v4u& w, uint32_t t) {
+#if MTBLX_ENC_TAILV
+  // the window shifted right by r = 16 - t bytes (funnel shifts), then stored as pieces of 8,
+  // 4, 2 and 1 bytes (the bits of t) instead of t byte stores: a wave paid for its longest tail
+  const uint32_t r = 16u - t, dq = r >> 2, bs = r & 3u;
+  const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  uint32_t o[4];
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t lo = dq + i < 4 ? (dq + i == 0 ? ws[0] : dq + i == 1 ? ws[1] : dq + i == 2 ? ws[2] : ws[3]) : 0u;
+    const uint32_t hi = dq + i + 1 < 4 ? (dq + i + 1 == 1 ? ws[1] : dq + i + 1 == 2 ? ws[2] : ws[3]) : 0u;
+    o[i] = __builtin_amdgcn_alignbyte(hi, lo, bs);
+  }
+  typedef uint64_t __attribute__((aligned(1))) u64t;
+  typedef uint32_t __attribute__((aligned(1))) u32t;
+  typedef uint16_t __attribute__((aligned(1))) u16t;
+  uint32_t off = 0;
+  if (t & 8u) {
+    *reinterpret_cast<u64t*>(d) = (uint64_t)o[0] | ((uint64_t)o[1] << 32);
+    off = 8;
+  }
+  if (t & 4u) {
+    *reinterpret_cast<u32t*>(d + off) = off ? o[2] : o[0];
+    off += 4;
+  }
+  const auto word = [&](uint32_t q) { return q == 0 ? o[0] : q == 1 ? o[1] : q == 2 ? o[2] : o[3]; };
+  if (t & 2u) {
+    *reinterpret_cast<u16t*>(d + off) = (uint16_t)(word(off >> 2) >> (8 * (off & 3u)));
+    off += 2;
+  }
+  if (t & 1u) d[off] = (uint8_t)(word(off >> 2) >> (8 * (off & 3u)));
+#else
+  for (uint32_t k = 0; k < t; ++k) {
+    const uint32_t q = 16 - t + k;
+    const uint32_t v = q < 4 ? w.x : q < 8 ? w.y : q < 12 ? w.z : w.w;
+    d[k] = (uint8_t)(v >> (8 * (q & 3)));
+  }
+#endif
+}
+
+// copy n bytes from global src to dst (LDS or global, generic pointer).  Four 16-byte loads
+// are in flight before their stores (the loads are the latency: a serial load -> store chain
+// per 16 bytes was most of the encode time); stores are unaligned 16-byte stores (gfx950 runs
+// in unaligned access mode).  A tail of 1..15 bytes is read as the 16-byte window ending at n
+// when the record is at least 16 bytes long (never before `base`, the blob's start), else
+// byte by byte.
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n, const uint8_t* base) {
   // chunks of 16 bytes: [0, nfull); tail bytes [16 nfull, n)
   const uint64_t nfull = n / 16;
@@ -334,48 +375,51 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   if (t == 0) return;
   const uint64_t to = 16 * nfull;
   if (src + n >= base + 16) {   // the 16-byte window ending at n holds the tail in its last t bytes
-    const v4u w = *reinterpret_cast<const v4u*>(src + n - 16);
-#if MTBLX_ENC_TAILV
-    // the window shifted right by r = 16 - t bytes (funnel shifts), then stored as pieces of 8,
-    // 4, 2 and 1 bytes (the bits of t) instead of t byte stores: a wave paid for its longest tail
-    const uint32_t r = 16u - t, dq = r >> 2, bs = r & 3u;
-    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-    uint32_t o[4];
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-      const uint32_t lo = dq + i < 4 ? (dq + i == 0 ? ws[0] : dq + i == 1 ? ws[1] : dq + i == 2 ? ws[2] : ws[3]) : 0u;
-      const uint32_t hi = dq + i + 1 < 4 ? (dq + i + 1 == 1 ? ws[1] : dq + i + 1 == 2 ? ws[2] : ws[3]) : 0u;
-      o[i] = __builtin_amdgcn_alignbyte(hi, lo, bs);
-    }
-    typedef uint64_t __attribute__((aligned(1))) u64t;
-    typedef uint32_t __attribute__((aligned(1))) u32t;
-    typedef uint16_t __attribute__((aligned(1))) u16t;
-    uint8_t* d = dst + to;
-    uint32_t off = 0;
-    if (t & 8u) {
-      *reinterpret_cast<u64t*>(d) = (uint64_t)o[0] | ((uint64_t)o[1] << 32);
-      off = 8;
-    }
-    if (t & 4u) {
-      *reinterpret_cast<u32t*>(d + off) = off ? o[2] : o[0];
-      off += 4;
-    }
-    const auto word = [&](uint32_t q) { return q == 0 ? o[0] : q == 1 ? o[1] : q == 2 ? o[2] : o[3]; };
-    if (t & 2u) {
-      *reinterpret_cast<u16t*>(d + off) = (uint16_t)(word(off >> 2) >> (8 * (off & 3u)));
-      off += 2;
-    }
-    if (t & 1u) d[off] = (uint8_t)(word(off >> 2) >> (8 * (off & 3u)));
-    return;
-#endif
-    for (uint32_t k = 0; k < t; ++k) {
-      const uint32_t q = 16 - t + k;
-      const uint32_t d = q < 4 ? w.x : q < 8 ? w.y : q < 12 ? w.z : w.w;
-      dst[to + k] = (uint8_t)(d >> (8 * (q & 3)));
-    }
+    store_tail(dst + to, *reinterpret_cast<const v4u*>(src + n - 16), t);
   } else {
     for (uint64_t k = to; k < n; ++k) dst[k] = src[k];
   }
+}
+
+// an entry's key suffix (kn bytes at ks) and value (vn bytes at vs), back to back at dst: when
+// both are at most 64 bytes (cfg3's common case) every load of both -- whole chunks and the two
+// tail windows -- is issued before the first store, one memory round trip instead of the 2-4 of
+// two copy_bytes calls (each waits for its chunks, then for its tail window)
+#ifndef MTBLX_ENC_EARLY   // planned mode: first entry's fields loaded beside phase A's sums
+#define MTBLX_ENC_EARLY 0
+#endif
+#ifndef MTBLX_ENC_KV
+#define MTBLX_ENC_KV 0
+#endif
+__device__ __forceinline__ void copy_kv(uint8_t* dst, const uint8_t* ks, uint64_t kn, const uint8_t* kbase,
+                                        const uint8_t* vs, uint64_t vn, const uint8_t* vbase) {
+  if (!MTBLX_ENC_KV || kn > 64 || vn > 64) {
+    copy_bytes(dst, ks, kn, kbase);
+    copy_bytes(dst + kn, vs, vn, vbase);
+    return;
+  }
+  const uint32_t nk = (uint32_t)kn / 16u, tk = (uint32_t)kn % 16u, nv = (uint32_t)vn / 16u, tv = (uint32_t)vn % 16u;
+  const bool wk = tk && ks + kn >= kbase + 16, wv = tv && vs + vn >= vbase + 16;
+  v4u K[4], V[4], KT = {0u, 0u, 0u, 0u}, VT = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u)
+    if (u < nk) K[u] = *reinterpret_cast<const v4u*>(ks + 16 * u);
+  if (wk) KT = *reinterpret_cast<const v4u*>(ks + kn - 16);
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u)
+    if (u < nv) V[u] = *reinterpret_cast<const v4u*>(vs + 16 * u);
+  if (wv) VT = *reinterpret_cast<const v4u*>(vs + vn - 16);
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u)
+    if (u < nk) *reinterpret_cast<v4u*>(dst + 16 * u) = K[u];
+  if (wk) store_tail(dst + 16 * nk, KT, tk);
+  else for (uint32_t k = 16 * nk; k < (uint32_t)kn; ++k) dst[k] = ks[k];
+  uint8_t* dv = dst + kn;
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u)
+    if (u < nv) *reinterpret_cast<v4u*>(dv + 16 * u) = V[u];
+  if (wv) store_tail(dv + 16 * nv, VT, tv);
+  else for (uint32_t k = 16 * nv; k < (uint32_t)vn; ++k) dv[k] = vs[k];
 }
 
 __device__ __forceinline__ void put32(uint8_t* p, uint32_t v) {
@@ -589,8 +633,7 @@ __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent
   put_varint(dst + l0, ks, l1);
   put_varint(dst + l0 + l1, vl, l2);
   const uint32_t n = l0 + l1 + l2;
-  copy_bytes(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys);
-  copy_bytes(dst + n + (e.kl - e.sh), R.vals + e.v0, e.vl, R.vals);
+  copy_kv(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys, R.vals + e.v0, e.vl, R.vals);
 }
 __device__ __forceinline__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
   uint64_t excl = 0;
@@ -705,6 +748,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
   // the restart phase of entry i0 (i0 mod interval), then advanced per entry
   const uint32_t ph0 = iv ? (uint32_t)(i0 % iv) : 0u;
   uint32_t ph = ph0;
+  // planned mode: the first entry's fields are loaded now, beside the sums' loads (phase A), not
+  // after them
+  Ent en0{};
+  (void)en0;
+  if constexpr (PL && MTBLX_ENC_EARLY) {
+    if (pl_ok && i0 < i1) en0 = entry_of(a.R, r0, i0, iv ? (i0 > 0 && ph0 != 0) : (i0 > 0), nullptr, a.SH + j0);
+  }
   Ent pe{};   // the previous entry (MTBLX_ENC_CARRY)
   (void)pe;
   for (uint64_t i = i0; i < i1 && !PL; ++i) {
@@ -765,7 +815,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(M
     uint32_t rp = ph0;
     uint64_t ri = iv ? (i0 + iv - 1) / iv : 0;
     const auto share_at = [&](uint64_t i, uint32_t p) { return iv ? (i > 0 && p != 0) : (i > 0); };
-    if (i0 < i1) en = entry_of(a.R, r0, i0, share_at(i0, rp), S.shc, SHb);
+    if (i0 < i1) en = (PL && MTBLX_ENC_EARLY) ? en0 : entry_of(a.R, r0, i0, share_at(i0, rp), S.shc, SHb);
     for (uint64_t i = i0; i < i1; ++i) {
       const Ent e = en;
       const uint32_t rp1 = iv ? (rp + 1 == iv ? 0u : rp + 1) : 0u;

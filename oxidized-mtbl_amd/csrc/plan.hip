@@ -768,6 +768,7 @@ static int plan_impl(const mtblx_records* rec, const uint64_t* shard_rec, uint32
   }
   const uint64_t slots = base12[nshard], w6 = base6[nshard];
   const uint64_t nchunk = (m + 63) / 64;
+  [[maybe_unused]] const uint64_t m1 = std::max<uint64_t>(m, 1);   // the bounds build's range sizes
   uint8_t* ws = static_cast<uint8_t*>(workspace);
   auto p64 = [&](size_t o) { return reinterpret_cast<uint64_t*>(ws + o); };
   auto p32 = [&](size_t o) { return reinterpret_cast<uint32_t*>(ws + o); };

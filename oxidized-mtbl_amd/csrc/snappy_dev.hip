@@ -137,6 +137,7 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
                                            int lane, int32_t* st_out, uint32_t* dec_len) {
   const uint64_t t_blk = SNAP_T();
   uint64_t t_fl = 0, n_el = 0, n_fl = 0, n_rs = 0, n_st = 0;
+  (void)t_blk; (void)t_fl; (void)n_el; (void)n_fl; (void)n_rs; (void)n_st;   // debug counters only
   // ---- LDS window over the stored bytes ----
   int32_t wstart = pf.wstart;   // block position of window byte 0 (16-byte aligned in memory; may be < 0)
   uint32_t whi = pf.whi;        // window holds block positions [max(wstart, 0), whi)
@@ -364,7 +365,7 @@ __device__ __forceinline__ void snap_block(WaveLds<C>& S, Window<C>& pf, const u
     if (d != W) st = MTBLX_SNAPPY_CORRUPT;
   }
   // ---- LDS output -> HBM ----
-  const uint64_t t_out = SNAP_T();
+  [[maybe_unused]] const uint64_t t_out = SNAP_T();
   if (st == MTBLX_SNAPPY_OK && !glob) {
     lds_fence();
     if (((uintptr_t)dg & 15u) == 0) {
@@ -1458,7 +1459,7 @@ constexpr int OUT = 4608;                       // output bytes
 constexpr int K = 8;                            // elements per lane
 constexpr int MAXE = K * kWave;                 // 512
 constexpr int NP = IN + 2;                      // chain positions: stream, n (end), n + 1 (overshoot)
-constexpr int PPL = (NP + kWave - 1) / kWave;   // positions per lane (contiguous)
+[[maybe_unused]] constexpr int PPL = (NP + kWave - 1) / kWave;   // positions per lane (contiguous)
 #ifndef MTBLX_WAVEP_WG_PER_CU
 #define MTBLX_WAVEP_WG_PER_CU 12
 #endif
@@ -1546,7 +1547,7 @@ __device__ __forceinline__ uint32_t jnext(const uint8_t* in, uint32_t p, uint32_
   return (uint64_t)p + sz > (uint64_t)n ? n + 1u : p + (uint32_t)sz;
 }
 
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) k_snappy_waves(const uint8_t* src, const uint64_t* src_off,
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) k_snappy_waves(const uint8_t* src, const uint64_t* src_off,
                                                         const uint32_t* src_len, uint32_t nblk, uint8_t* dst,
                                                         const uint64_t* dst_off, const uint32_t* dst_len,
                                                         int32_t* status, uint32_t* dec_len, int only_marked) {

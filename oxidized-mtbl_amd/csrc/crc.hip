@@ -201,6 +201,9 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in
 #ifndef MTBLX_CRC_PAIR   // two steps per loop iteration (in-wave ILP, A/B: measured slower); 0 = one
 #define MTBLX_CRC_PAIR 0
 #endif
+#ifndef MTBLX_CRC_STEADY   // steady-state steps wait with the constant vmcnt(kRing - 1) (0: the variable wait)
+#define MTBLX_CRC_STEADY 1
+#endif
 #ifndef MTBLX_CRC_DMA_AUX
 #define MTBLX_CRC_DMA_AUX 2   // non-temporal: the block bytes are read once
 #endif
@@ -460,11 +463,15 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
         // their stage-1 chains are independent, so the wave keeps two in flight -- the per-wave
         // step is latency-bound (LDS read -> bit planes -> 8 dependent-pair MFMAs -> f16 stage 2)
         const bool pair = MTBLX_CRC_PAIR && s >= 1u && (s & (uint32_t)(kMSup - 1)) != 0u;
+        bool steady = false;
         if (ilive) {   // steady state: kRing - 1 steps stay in flight behind this one
           issue();
           ++pend;
+          steady = MTBLX_CRC_STEADY && !pair;   // pend == kRing here: the wait is a constant
         }
-        wait_vm(pend - (pair ? 2u : 1u));
+        // (the variable wait is a switch: ~25 scalar instructions and 8 branches per step)
+        if (steady) wait_steady();
+        else wait_vm(pend - (pair ? 2u : 1u));
         const uint32_t t = s & (uint32_t)(kMSup - 1);
         v4i a2lo, a2hi, b2lo, b2hi;
         v4u x, y;

@@ -204,6 +204,9 @@ static_assert(MfmaTabs().max_row < 1024, "stage-1 sums stay below 2^10: exact in
 #ifndef MTBLX_CRC_STEADY   // steady-state steps wait with the constant vmcnt(kRing - 1) (0: the variable wait)
 #define MTBLX_CRC_STEADY 1
 #endif
+#ifndef MTBLX_CRC_HEAD2   // head steps: branch-free masks (head_chunk_fast); 0 = head_chunk
+#define MTBLX_CRC_HEAD2 1
+#endif
 #ifndef MTBLX_CRC_DMA_AUX
 #define MTBLX_CRC_DMA_AUX 2   // non-temporal: the block bytes are read once
 #endif
@@ -490,7 +493,7 @@ __global__ void __launch_bounds__(kMThreads, 1) k_crc32c_mfma(const uint8_t* __r
           pend -= 1;
         }
         if (sbc < 4) {   // the block's first bytes (sbc > -1024)
-          x = head_chunk(x, sbc + 16 * (int)kx);
+          x = MTBLX_CRC_HEAD2 ? head_chunk_fast(x, sbc + 16 * (int)kx) : head_chunk(x, sbc + 16 * (int)kx);
           sbc += kMStep;
         }
         if (pair && sbc < 4) {

@@ -97,6 +97,24 @@ __device__ __forceinline__ v4u head_chunk(v4u x, int a) {
   if (a >= 4) return x;
   return v4u{head_dword(x.x, a), head_dword(x.y, a + 4), head_dword(x.z, a + 8), head_dword(x.w, a + 12)};
 }
+// head_chunk without branches (k_crc32c_mfma's head steps): dword d of the chunk starts at block
+// position pos = a + 4 d; with S = 32 + 8 pos, the kept bytes (positions >= 0) are the low word of
+// 0xFFFFFFFF'00000000 >> clamp(S, 0, 32) and the init bytes (positions 0..3) the low word of the same
+// value >> clamp(S, 0, 64) mod 64 -- two 64-bit shifts and a bitop per dword, no divergent exec
+__device__ __forceinline__ v4u head_chunk_fast(v4u x, int a) {
+  constexpr uint64_t V = 0xFFFFFFFF00000000ull;
+  const int S0 = 32 + 8 * a;
+  uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int S = S0 + 32 * d;
+    const int c = S < 0 ? 0 : S;
+    const uint32_t keep = (uint32_t)(V >> (c < 32 ? c : 32));
+    const uint32_t fold = (uint32_t)(V >> ((c < 64 ? c : 64) & 63));
+    w[d] = (w[d] & keep) ^ fold;
+  }
+  return v4u{w[0], w[1], w[2], w[3]};
+}
 // the pad after the block's end: t < 16 zero bytes in the last chunk of the block's last step
 __device__ __forceinline__ v4u tail_chunk(v4u y, uint32_t t) {
   const uint32_t k = 16u - t;   // bytes kept

@@ -381,6 +381,55 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   }
 }
 
+// n bytes from src to dst as 16-byte chunks at offsets min(16 c, n - 16): the last, partial chunk
+// is the 16-byte window ending at n, rewriting bytes of the chunk before it with the same values,
+// so a field of n >= 16 bytes takes ceil(n / 16) whole loads and stores, issued four at a time --
+// one round trip for up to 64 bytes, no tail pieces.  A field of 1..15 bytes is the window ending
+// at n shifted down; with `fwd` (this thread rewrites the bytes after the field later: the key
+// suffix before its value) it goes out as one 16-byte store, else as 8/4/2/1-byte pieces.
+#ifndef MTBLX_ENC_OVER
+#define MTBLX_ENC_OVER 0
+#endif
+__device__ __forceinline__ void copy_over(uint8_t* dst, const uint8_t* src, uint32_t n, const uint8_t* base, bool fwd) {
+  if (n >= 16u) {
+    const uint32_t m = (n + 15u) >> 4;
+    for (uint32_t c = 0; c < m; c += 4) {
+      v4u w[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t o = 16u * (c + u) < n - 16u ? 16u * (c + u) : n - 16u;
+        if (c + u < m) w[u] = *reinterpret_cast<const v4u*>(src + o);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t o = 16u * (c + u) < n - 16u ? 16u * (c + u) : n - 16u;
+        if (c + u < m) *reinterpret_cast<v4u*>(dst + o) = w[u];
+      }
+    }
+    return;
+  }
+  if (n == 0u) return;
+  if (src + n >= base + 16) {
+    const v4u w = *reinterpret_cast<const v4u*>(src + n - 16);
+    if (fwd) {   // bytes n..15 of the store are rewritten by this thread afterwards
+      const uint32_t r = 16u - n, dq = r >> 2, bs = r & 3u;
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+      uint32_t o[4];
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t lo = dq + i < 4 ? (dq + i == 0 ? ws[0] : dq + i == 1 ? ws[1] : dq + i == 2 ? ws[2] : ws[3]) : 0u;
+        const uint32_t hi = dq + i + 1 < 4 ? (dq + i + 1 == 1 ? ws[1] : dq + i + 1 == 2 ? ws[2] : ws[3]) : 0u;
+        o[i] = __builtin_amdgcn_alignbyte(hi, lo, bs);
+      }
+      *reinterpret_cast<v4u*>(dst) = v4u{o[0], o[1], o[2], o[3]};
+    } else {
+      store_tail(dst, w, n);
+    }
+  } else {
+    for (uint32_t k = 0; k < n; ++k) dst[k] = src[k];
+  }
+}
+
 // an entry's key suffix (kn bytes at ks) and value (vn bytes at vs), back to back at dst: when
 // both are at most 64 bytes (cfg3's common case) every load of both -- whole chunks and the two
 // tail windows -- is issued before the first store, one memory round trip instead of the 2-4 of
@@ -626,14 +675,35 @@ __device__ __forceinline__ void put_varint(uint8_t* p, uint32_t v, uint32_t len)
   for (uint32_t k = 0; k < 5; ++k)
     if (k < len) p[k] = (uint8_t)(((v >> (7 * k)) & 0x7fu) | (k + 1 < len ? 0x80u : 0u));
 }
+// varint32(v) (len = vlen32(v) bytes) as a little-endian word, branch-free: the 7-bit groups
+// spread to bytes, the continuation bit on all but the last
+__device__ __forceinline__ uint64_t vbytes32(uint32_t v, uint32_t len) {
+  const uint64_t g = (uint64_t)(v & 0x7fu) | ((uint64_t)(v & 0x3f80u) << 1) | ((uint64_t)(v & 0x1fc000u) << 2) |
+                     ((uint64_t)(v & 0xfe00000u) << 3) | ((uint64_t)(v >> 28) << 32);
+  return g | (0x0000008080808080ull & ((1ull << (8 * (len - 1u))) - 1ull));
+}
+#ifndef MTBLX_ENC_HDR   // the three header varints as one 8-byte store when they fit (1) or byte by byte (0)
+#define MTBLX_ENC_HDR 1
+#endif
 __device__ __forceinline__ void put_entry(uint8_t* dst, const Recs& R, const Ent& e) {
   const uint32_t sh = (uint32_t)e.sh, ks = (uint32_t)(e.kl - e.sh), vl = (uint32_t)e.vl;   // < 4 GiB (k_plan)
   const uint32_t l0 = vlen32(sh), l1 = vlen32(ks), l2 = vlen32(vl);
-  put_varint(dst, sh, l0);
-  put_varint(dst + l0, ks, l1);
-  put_varint(dst + l0 + l1, vl, l2);
   const uint32_t n = l0 + l1 + l2;
+  if (MTBLX_ENC_HDR && n <= 8u && (uint64_t)n + ks + vl >= 8u) {
+    // one unaligned 8-byte store: its bytes n..7 are the key suffix / value's, rewritten below by
+    // this thread (in program order) -- no conditional byte stores
+    *reinterpret_cast<u64u*>(dst) = vbytes32(sh, l0) | (vbytes32(ks, l1) << (8 * l0)) | (vbytes32(vl, l2) << (8 * (l0 + l1)));
+  } else {
+    put_varint(dst, sh, l0);
+    put_varint(dst + l0, ks, l1);
+    put_varint(dst + l0 + l1, vl, l2);
+  }
+#if MTBLX_ENC_OVER
+  copy_over(dst + n, R.keys + e.k0 + e.sh, ks, R.keys, (uint64_t)ks + vl >= 16u);
+  copy_over(dst + n + ks, R.vals + e.v0, vl, R.vals, false);
+#else
   copy_kv(dst + n, R.keys + e.k0 + e.sh, e.kl - e.sh, R.keys, R.vals + e.v0, e.vl, R.vals);
+#endif
 }
 __device__ __forceinline__ uint64_t lookback(const EncArgs& a, uint32_t b, int lane, bool& timeout) {
   uint64_t excl = 0;

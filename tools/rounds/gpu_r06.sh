@@ -73,6 +73,12 @@ decst)   # PipeLarge per-phase stamps: the product stamps build vs build/libmtbl
   B="python bench.py --config cfg3 --cfg3-blocks 100000 --no-cpu-baseline --no-get --stamps"
   step decst_prod 300 $B --lib oxidized-mtbl_amd/mtblx/libmtblx_stamps.so
   for v in ${STV:-}; do step decst_$v 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done ;;
+encpmc)   # k_encode LDS / wait counters (one PMC pass each): product vs build/libmtblx_<v>.so for v in $ENCV
+  A="bench.py --config cfg3 --cfg3-blocks 100000 --steps 1 --warmup 0 --no-cpu-baseline --no-get"
+  for v in prod ${ENCV:-}; do
+    L=""; [ "$v" = prod ] || L="--lib oxidized-mtbl_amd/build/libmtblx_$v.so"
+    step encpmc_$v 200 rocprofv3 --output-format csv --kernel-include-regex k_encode --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS -d $O/encpmc_$v -o run -- python3 $A $L
+  done ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

@@ -279,6 +279,9 @@ __device__ __forceinline__ uint64_t est(const NextArgs& a, uint64_t j, uint64_t 
   return buf + nr * (buf > 0xFFFFFFFFull ? 8u : 4u) + 4u;
 }
 
+#ifndef MTBLX_PLAN_LIN   // records probed one by one after ka before the 64-record chunk skip (0: 16.0 ms, 4: 14.9 ms per 3 cfg3 chunks)
+#define MTBLX_PLAN_LIN 4
+#endif
 // next(j) for a start j of a shard ending at e (j + 1 < e, interval >= 1).  The first k with
 // est(k) + gmax >= B (est grows with k) is bracketed by a gallop from `guess` (first step d) and
 // bisected -- ka, returned for the next start's guess; from there the flushing record is found
@@ -318,6 +321,12 @@ __device__ __forceinline__ uint64_t find_next(const NextArgs& a, uint64_t j, uin
   }
   ka = hi;
   uint64_t k = hi;
+  // the flushing record is usually within a few records of ka (gm bounds every record's term
+  // from above): probe those directly before skipping by 64-record chunks
+  for (uint32_t t = 0; t < MTBLX_PLAN_LIN && k <= e1; ++t, ++k) {
+    MTBLX_CHK(a.G + k, 8);
+    if (est(a, j, base_a, base_q, k) + a.G[k] >= a.B) return k;
+  }
   while (k <= e1) {
     const uint64_t cl = std::min<uint64_t>((k | 63u), e1);
     MTBLX_CHK(a.GM + (k >> 6), 8);
@@ -335,6 +344,9 @@ __device__ __forceinline__ uint64_t find_next(const NextArgs& a, uint64_t j, uin
 // one's threshold + kT, which moves by about as much as the start did -- a few probes instead of
 // a full search
 constexpr uint32_t kSweep = 8;
+#ifndef MTBLX_PLAN_D0   // first gallop step from the previous start's threshold + kT (1: 16.3 ms, 8: 15.5 ms per 3 cfg3 chunks)
+#define MTBLX_PLAN_D0 8
+#endif
 __global__ void __launch_bounds__(kT) k_plan_next(NextArgs a) {
   // the shard starts in LDS when they fit (the shard search is on every thread's chain)
   constexpr uint32_t kLsb = 1024;
@@ -371,7 +383,7 @@ __global__ void __launch_bounds__(kT) k_plan_next(NextArgs a) {
         a.pan[j] = es + a.G[j + 1] >= a.B ? 0 : 1;
         nx = j + 1;
       } else if (e == pe && pka < pe) {   // the same shard: from the previous threshold
-        nx = find_next(a, j, e, pka + kT, 1, gm, pka);
+        nx = find_next(a, j, e, pka + kT, MTBLX_PLAN_D0, gm, pka);
       } else {
         nx = find_next(a, j, e, j + hint, hint / 16 + 1, gm, pka);
       }

@@ -79,6 +79,13 @@ encpmc)   # k_encode LDS / wait counters (one PMC pass each): product vs build/l
     L=""; [ "$v" = prod ] || L="--lib oxidized-mtbl_amd/build/libmtblx_$v.so"
     step encpmc_$v 200 rocprofv3 --output-format csv --kernel-include-regex k_encode --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS -d $O/encpmc_$v -o run -- python3 $A $L
   done ;;
+planab)   # block-cut A/B on three cfg3 chunks (writer_GiB_per_s, plan_ms_total): product vs build/libmtblx_<v>.so for v in $PLANV
+  B="python bench.py --config cfg3 --cfg3-blocks 300000 --steps 1 --warmup 0 --no-cpu-baseline --no-get"
+  for r in 1 2; do
+    step planab_prod$r 300 $B
+    for v in ${PLANV:-}; do step planab_${v}_$r 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
+  done
+  grep -H -o '"plan_ms_total": [0-9.]*\|"writer_GiB_per_s": [0-9.]*' $O/planab_*.log || true ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

@@ -86,6 +86,8 @@ planab)   # block-cut A/B on three cfg3 chunks (writer_GiB_per_s, plan_ms_total)
     for v in ${PLANV:-}; do step planab_${v}_$r 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
   done
   grep -H -o '"plan_ms_total": [0-9.]*\|"writer_GiB_per_s": [0-9.]*' $O/planab_*.log || true ;;
+planprof)   # block-cut kernel breakdown: one cfg3 chunk (65 930 240 records, 64 shards), kernel trace
+  step planprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/planprof -o run -- python3 scripts/plan_probe.py 65930240 64 ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

@@ -25,8 +25,18 @@
 #include <stdlib.h>
 
 #include <initializer_list>
+#include <mutex>
 
 extern "C" void mtblx_bounds_note(const char* kernel, uint64_t line, uint64_t addr, uint64_t nbytes, int fault);
+
+// The table and the first-violation record are one per translation unit: launches from several
+// host threads (the concurrent-cut test) would overwrite each other's table between a set_ranges
+// and its launch, so the diagnostic build serializes set_ranges + launch + after process-wide
+// (an inline function with external linkage: one mutex for the whole library).
+inline std::mutex& mtblx_bounds_launch_lock() {
+  static std::mutex m;
+  return m;
+}
 
 namespace {   // one copy per translation unit: its kernels read their own table
 namespace mtblx_bounds {
@@ -138,6 +148,7 @@ inline void after(const char* name, hipStream_t s) {
 #define MTBLX_R(p, n) mtblx_bounds::Rng((const void*)(p), (uint64_t)(n))
 #define MTBLX_LAUNCH(ptrs, kern, g, b, sh, s, ...)                                        \
   do {                                                                                    \
+    std::lock_guard<std::mutex> bounds_lock_(mtblx_bounds_launch_lock());                   \
     mtblx_bounds::set_ranges((s), std::initializer_list<mtblx_bounds::Rng> MTBLX_PTRS ptrs); \
     hipLaunchKernelGGL(kern, g, b, sh, s, __VA_ARGS__);                              \
     mtblx_bounds::after(#kern, (s));                                                 \

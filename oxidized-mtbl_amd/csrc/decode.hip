@@ -1236,7 +1236,13 @@ struct PipeCfg {
 };
 // (PipeLarge with four loaders and ten copy waves: +0.8 % on 16 B keys, -16 % on cfg3's long
 // Zipf keys, whose copy is the longer half of the iteration)
-using PipeSmall = PipeCfg<49152, 3, 16, 56>;   // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
+// PipeSmall's staging bytes per tile buffer (three buffers in LDS).  49 664 fits twelve 4 KiB blocks
+// (cfg2) or three 16 KiB blocks (cfg4's middle leg) per tile with their framing; 49 152 fitted
+// eleven / two: cfg4 2302 -> 2544 GiB/s (16 KiB leg 2182 -> 2794), profiles/r06/small_tb/
+#ifndef MTBLX_SMALL_TB
+#define MTBLX_SMALL_TB 49664
+#endif
+using PipeSmall = PipeCfg<MTBLX_SMALL_TB, 3, 16, 56>;   // blocks up to ~48 KiB (cfg2 4 KiB, cfg4 16 KiB)
 #ifndef MTBLX_LARGE_LOADW
 #define MTBLX_LARGE_LOADW 2
 #endif
@@ -2759,11 +2765,13 @@ static bool fit_plan(uint32_t max_len, uint32_t tb, uint32_t maxblk, Plan& p) {
   return true;
 }
 
-Plan make_plan(uint32_t nblk, uint32_t max_len) {
+// (the fused-verify kernels may stage fewer bytes than their plain twins: the tile shape follows
+// the kernel that will run)
+Plan make_plan(uint32_t nblk, uint32_t max_len, bool verify) {
   Plan p{};
-  if (fit_plan(max_len, PipeSmall::TB, PipeSmall::MAXBLK, p)) {
+  if (fit_plan(max_len, verify ? PipeSmallV::TB : PipeSmall::TB, PipeSmall::MAXBLK, p)) {
     p.kind = 0;
-  } else if (fit_plan(max_len, PipeLarge::TB, PipeLarge::MAXBLK, p)) {
+  } else if (fit_plan(max_len, verify ? PipeLargeV::TB : PipeLarge::TB, PipeLarge::MAXBLK, p)) {
     p.kind = 1;
   } else {
     const uint32_t usable = CfgLarge::TB - 48;
@@ -2841,7 +2849,7 @@ extern "C" int mtblx_impl_run(const mtblx_block_batch* in, const mtblx_decoded* 
   const uint32_t nblk = in->nblk;
   const uint64_t cap64 = ws_bytes > 320u ? (ws_bytes - 320u) / (8u * kTileWords) : 0u;
   const uint32_t wscap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;
-  const Plan p = make_plan(nblk, in->max_blk_len);
+  const Plan p = make_plan(nblk, in->max_blk_len, verify != 0);
   uint64_t* dbg = reinterpret_cast<uint64_t*>(ws);
   WsHdr* hdr = reinterpret_cast<WsHdr*>(reinterpret_cast<uint8_t*>(ws) + 128);
   uint64_t* lbw = dbg + 32;

@@ -88,6 +88,17 @@ planab)   # block-cut A/B on three cfg3 chunks (writer_GiB_per_s, plan_ms_total)
   grep -H -o '"plan_ms_total": [0-9.]*\|"writer_GiB_per_s": [0-9.]*' $O/planab_*.log || true ;;
 planprof)   # block-cut kernel breakdown: one cfg3 chunk (65 930 240 records, 64 shards), kernel trace
   step planprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/planprof -o run -- python3 scripts/plan_probe.py 65930240 64 ;;
+cfg2ab)   # cfg2 decode A/B (bench value, 100 steps): product vs build/libmtblx_<v>.so for v in $DECV, twice; cfg4 legs with $CFG4=1
+  B="python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-e2e --no-get --no-ceiling"
+  for r in 1 2; do
+    step cfg2ab_prod$r 300 $B
+    for v in ${DECV:-}; do step cfg2ab_${v}_$r 300 $B --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
+  done
+  if [ "${CFG4:-0}" = 1 ]; then
+    step cfg4ab_prod 600 python bench.py --config cfg4 --no-cpu-baseline --no-e2e
+    for v in ${DECV:-}; do step cfg4ab_$v 600 python bench.py --config cfg4 --no-cpu-baseline --no-e2e --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
+  fi
+  grep -H -o '"value": [0-9.]*' $O/cfg2ab_*.log $O/cfg4ab_*.log 2>/dev/null || true ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

@@ -22,7 +22,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PEAK = 8000.0
 RND = os.environ.get("ROUND", "r04")
-SMALL = "PipeCfg<49152, 3, 16, 56, false"
+SMALL = ", 3, 16, 56, false"   # PipeSmall (any staging size: 49 152 before round 6, 49 664 since)
 LARGE = "PipeCfg<65664, 2, 2, 64, false"
 
 

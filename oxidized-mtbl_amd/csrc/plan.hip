@@ -363,7 +363,10 @@ __device__ __forceinline__ uint64_t find_next(const NextArgs& a, uint64_t j, uin
 // coalesce): the first from a probe at the typical block length, each next one from the previous
 // one's threshold + kT, which moves by about as much as the start did -- a few probes instead of
 // a full search
-constexpr uint32_t kSweep = 8;
+#ifndef MTBLX_PLAN_SWEEP   // starts per thread in k_plan_next
+#define MTBLX_PLAN_SWEEP 8
+#endif
+constexpr uint32_t kSweep = MTBLX_PLAN_SWEEP;
 #ifndef MTBLX_PLAN_D0   // first gallop step from the previous start's threshold + kT (1: 16.3 ms, 8: 15.5 ms per 3 cfg3 chunks)
 #define MTBLX_PLAN_D0 8
 #endif

@@ -99,6 +99,12 @@ cfg2ab)   # cfg2 decode A/B (bench value, 100 steps): product vs build/libmtblx_
     for v in ${DECV:-}; do step cfg4ab_$v 600 python bench.py --config cfg4 --no-cpu-baseline --no-e2e --lib oxidized-mtbl_amd/build/libmtblx_$v.so; done
   fi
   grep -H -o '"value": [0-9.]*' $O/cfg2ab_*.log $O/cfg4ab_*.log 2>/dev/null || true ;;
+snaplib)   # device snappy (lanes routing) A/B across libraries: product vs build/libmtblx_<v>.so for v in $SNAPV, twice
+  for r in 1 2; do
+    step snaplib_prod_$r 200 env MTBLX_SNAPPY_KERNEL=lanes python3 scripts/snappy_probe.py --blocks 100000 --tile 4 --compressible --reps 10
+    for v in ${SNAPV:-}; do step snaplib_${v}_$r 200 env MTBLX_LIB=oxidized-mtbl_amd/build/libmtblx_$v.so MTBLX_SNAPPY_KERNEL=lanes python3 scripts/snappy_probe.py --blocks 100000 --tile 4 --compressible --reps 10; done
+  done
+  grep -H "decompress" $O/snaplib_*.log || true ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
 done

@@ -711,8 +711,8 @@ __global__ void __launch_bounds__(kWave) k_snappy_deferred(const uint8_t* src, c
 // kernel's (the oracle's): CORRUPT / TOO_SMALL / OK.  DESIGN.md §4 has the measurements.
 namespace lanes {
 typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(1)));
-#ifndef MTBLX_LANE_THREADS   // decoding lanes per workgroup (as many writer lanes again)
-#define MTBLX_LANE_THREADS 256
+#ifndef MTBLX_LANE_THREADS   // decoding lanes per workgroup (as many writer lanes again); 128: 1.045-1.049 ms vs 1.073-1.074 at 256, 1.091 at 64 (round 6)
+#define MTBLX_LANE_THREADS 128
 #endif
 #ifndef MTBLX_LANE_RING_ALL5   // ring_put writes all five words (no per-word branch)
 #define MTBLX_LANE_RING_ALL5 1
@@ -817,7 +817,8 @@ __device__ __forceinline__ Q4 ring_get(const uint32_t (*R)[kThreads], int t, uin
 // v3: the HBM stores move to WRITER waves.  A vector-memory wait is in issue order over loads and
 // stores alike, so every header / literal load a decoding lane waited for also waited for all the
 // 16-byte stores it had issued before (an ablation without stores ran 1.63 -> 1.04 ms).  Here the
-// workgroup is 256 decoding lanes + 256 writer lanes, lane t + 256 writing lane t's block: the
+// workgroup is kThreads decoding lanes + kThreads writer lanes (128 + 128 since round 6), lane
+// t + kThreads writing lane t's block: the
 // decoder appends to its LDS ring and publishes its position (dpos); the writer copies whole
 // 16-byte chunks [fpos, dpos) from the ring to HBM and publishes fpos (issued) and fvis (stores
 // completed).  The decoder never overwrites ring words the writer has not taken (it waits on
